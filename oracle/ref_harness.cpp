@@ -1,0 +1,439 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY (never shipped, never measured as the product).
+//
+// Compiles the UNMODIFIED header-only reference (pvac-hfhe 0.1.0) from
+// /root/reference/include and drives it deterministically to mint the golden fixtures
+// under tests/golden/. Built by oracle/Makefile into oracle/_ref/ (git-ignored).
+//
+// Determinism: every byte of entropy in the reference flows through libc getrandom(2)
+// (reference include/pvac/core/random.hpp:40-56, csprng_u64 at :106-110). We interpose
+// getrandom with a seeded splitmix64 stream (one 64-bit value per 8 requested bytes) and
+// LOG every produced word, so the exact nonce/salt stream consumed by each ct_* call can be
+// handed to the GPU engine's ABI as its explicit `nonces` / `salts` inputs.
+//
+// Output formats (all little-endian):
+//   *.ct          — the reference's own on-disk format (tests/add.cpp:22-155 layout),
+//                   written by our own writer below; "weights-only" files use nbits=0 sigmas.
+//   *.u64         — raw u64 arrays.
+//   manifest.json — metadata (counts, digests, plaintexts).
+#include <pvac/pvac.hpp>
+
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+#include <chrono>
+#include <thread>
+
+using namespace pvac;
+
+// ---------------------------------------------------------------- getrandom interposer
+static uint64_t g_sm_state = 0x5EED0001ULL;
+static std::vector<uint64_t> g_log;
+static bool g_logging = true;
+
+static uint64_t splitmix64_next() {
+    uint64_t z = (g_sm_state += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+extern "C" ssize_t getrandom(void* buf, size_t n, unsigned int) {
+    uint8_t* p = (uint8_t*)buf;
+    size_t off = 0;
+    while (off < n) {
+        uint64_t v = splitmix64_next();
+        if (g_logging) g_log.push_back(v);
+        size_t take = (n - off < 8) ? (n - off) : 8;
+        std::memcpy(p + off, &v, take);
+        off += take;
+    }
+    return (ssize_t)n;
+}
+
+static void reseed(uint64_t s) { g_sm_state = s; }
+
+// ---------------------------------------------------------------- writers
+static void put32(std::ostream& o, uint32_t x) { o.write((const char*)&x, 4); }
+static void put64(std::ostream& o, uint64_t x) { o.write((const char*)&x, 8); }
+
+static void write_ct(const std::string& path, const std::vector<Cipher>& cts, bool with_sigma) {
+    std::ofstream o(path, std::ios::binary);
+    put32(o, 0x66699666u);
+    put32(o, 1u);
+    put64(o, (uint64_t)cts.size());
+    for (const auto& C : cts) {
+        put32(o, (uint32_t)C.L.size());
+        put32(o, (uint32_t)C.E.size());
+        for (const auto& L : C.L) {
+            o.put((char)(uint8_t)L.rule);
+            if (L.rule == RRule::BASE) {
+                put64(o, L.seed.ztag); put64(o, L.seed.nonce.lo); put64(o, L.seed.nonce.hi);
+            } else {
+                put32(o, L.pa); put32(o, L.pb);
+            }
+        }
+        for (const auto& e : C.E) {
+            put32(o, e.layer_id);
+            o.write((const char*)&e.idx, 2);
+            o.put((char)e.ch);
+            o.put(0);
+            put64(o, e.w.lo); put64(o, e.w.hi);
+            if (with_sigma) {
+                put32(o, (uint32_t)e.s.nbits);
+                for (size_t i = 0; i < (e.s.nbits + 63) / 64; ++i) put64(o, e.s.w[i]);
+            } else {
+                put32(o, 0u);
+            }
+        }
+    }
+}
+
+// PROD layers carry seeds too (ct_mul sets them, arithmetic.hpp:59-70) but the .ct format
+// drops them for PROD. Dump the full layer table separately: rule,pa,pb,ztag,nlo,nhi.
+static void write_layers(const std::string& path, const Cipher& C) {
+    std::ofstream o(path, std::ios::binary);
+    for (const auto& L : C.L) {
+        put64(o, (uint64_t)L.rule);
+        put64(o, L.rule == RRule::PROD ? (uint64_t)L.pa : 0);
+        put64(o, L.rule == RRule::PROD ? (uint64_t)L.pb : 0);
+        put64(o, L.seed.ztag); put64(o, L.seed.nonce.lo); put64(o, L.seed.nonce.hi);
+    }
+}
+
+static void write_u64(const std::string& path, const std::vector<uint64_t>& v) {
+    std::ofstream o(path, std::ios::binary);
+    o.write((const char*)v.data(), (std::streamsize)(v.size() * 8));
+}
+
+static std::string hex(const uint8_t* d, size_t n) {
+    static const char* H = "0123456789abcdef";
+    std::string s;
+    for (size_t i = 0; i < n; ++i) { s += H[d[i] >> 4]; s += H[d[i] & 15]; }
+    return s;
+}
+
+// per-edge sigma digest: first 8 bytes (LE) of SHA-256 over the sigma words (LE)
+static std::vector<uint64_t> sigma_digests(const Cipher& C) {
+    std::vector<uint64_t> out;
+    out.reserve(C.E.size());
+    for (const auto& e : C.E) {
+        Sha256 s; s.init();
+        for (uint64_t w : e.s.w) sha256_acc_u64(s, w);
+        uint8_t d[32]; s.finish(d);
+        out.push_back(load_le64(d));
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------- Fp vectors
+static const uint64_t MAXU = ~0ULL;
+
+static void cmd_fp(const std::string& dir) {
+    reseed(0x5EED0F00ULL);
+    std::vector<Fp> A, B;
+    // edge cases: 0,1,2,p-1,p-2,2^64-1,2^64,2^126,2^127-2, and
+    // non-canonical values (hi >= 2^63, == p) for the fp_add truncation / fp_neg quirks.
+    std::vector<Fp> edge = {
+        {0, 0}, {1, 0}, {2, 0}, {MAXU - 1, MASK63}, {MAXU - 2, MASK63}, {MAXU, 0}, {0, 1},
+        {0, 1ULL << 62}, {MAXU - 2, MASK63}, {MAXU, MASK63} /* p */, {0, 1ULL << 63} /* 2^127 */,
+        {MAXU, MAXU}, {MAXU, 1ULL << 63}, {1, 1ULL << 63}, {MAXU - 1, MAXU}, {12345, MASK63},
+        {0x8000000000000000ULL, 0x4000000000000000ULL}, {MAXU, 0x7FFFFFFFFFFFFFFEULL},
+        {3, 0xC000000000000000ULL}, {0xDEADBEEFULL, 0xFFFFFFFF00000000ULL},
+        {MAXU, 0x3FFFFFFFFFFFFFFFULL}, {1, MASK63}, {0, MASK63}, {MAXU - 1, MASK63 - 1},
+        {0x0123456789ABCDEFULL, 0x7EDCBA9876543210ULL}, {0x1ULL << 63, 0},
+        {MAXU, 0x8000000000000001ULL}, {5, 0xFFFFFFFFFFFFFFF0ULL},
+        {0xAAAAAAAAAAAAAAAAULL, 0x5555555555555555ULL}, {0x5555555555555555ULL, 0xAAAAAAAAAAAAAAAAULL},
+        {2, MASK63}, {MAXU - 3, MASK63},
+    };
+    for (size_t i = 0; i < edge.size(); ++i)
+        for (size_t j = 0; j < edge.size(); ++j) { A.push_back(edge[i]); B.push_back(edge[j]); }
+    // random canonical
+    for (int i = 0; i < 2048; ++i) {
+        Fp a = fp_from_words(splitmix64_next(), splitmix64_next() & MASK63);
+        Fp b = fp_from_words(splitmix64_next(), splitmix64_next() & MASK63);
+        A.push_back(a); B.push_back(b);
+    }
+    // random arbitrary 128-bit (non-canonical allowed)
+    for (int i = 0; i < 1024; ++i) {
+        Fp a{splitmix64_next(), splitmix64_next()};
+        Fp b{splitmix64_next(), splitmix64_next()};
+        A.push_back(a); B.push_back(b);
+    }
+    size_t n = A.size();
+    std::vector<uint64_t> a_lo(n), a_hi(n), b_lo(n), b_hi(n), add_lo(n), add_hi(n), sub_lo(n),
+        sub_hi(n), neg_lo(n), neg_hi(n), mul_lo(n), mul_hi(n), fw_lo(n), fw_hi(n);
+    for (size_t i = 0; i < n; ++i) {
+        a_lo[i] = A[i].lo; a_hi[i] = A[i].hi; b_lo[i] = B[i].lo; b_hi[i] = B[i].hi;
+        Fp s = fp_add(A[i], B[i]), d = fp_sub(A[i], B[i]), g = fp_neg(A[i]), m = fp_mul(A[i], B[i]);
+        Fp f = fp_from_words(A[i].lo, A[i].hi);
+        add_lo[i] = s.lo; add_hi[i] = s.hi; sub_lo[i] = d.lo; sub_hi[i] = d.hi;
+        neg_lo[i] = g.lo; neg_hi[i] = g.hi; mul_lo[i] = m.lo; mul_hi[i] = m.hi;
+        fw_lo[i] = f.lo; fw_hi[i] = f.hi;
+    }
+    // inverses of canonical nonzero values
+    std::vector<uint64_t> inv_in_lo, inv_in_hi, inv_lo, inv_hi;
+    for (int i = 0; i < 512; ++i) {
+        Fp a = rand_fp_nonzero();
+        Fp v = fp_inv(a);
+        inv_in_lo.push_back(a.lo); inv_in_hi.push_back(a.hi); inv_lo.push_back(v.lo); inv_hi.push_back(v.hi);
+    }
+    // fp_pow_u64
+    std::vector<uint64_t> pw_lo, pw_hi, pw_e, pw_rlo, pw_rhi;
+    for (int i = 0; i < 256; ++i) {
+        Fp a = fp_from_words(splitmix64_next(), splitmix64_next() & MASK63);
+        uint64_t e = splitmix64_next() >> (i % 64);
+        Fp r = fp_pow_u64(a, e);
+        pw_lo.push_back(a.lo); pw_hi.push_back(a.hi); pw_e.push_back(e); pw_rlo.push_back(r.lo); pw_rhi.push_back(r.hi);
+    }
+    write_u64(dir + "/fp_a_lo.u64", a_lo); write_u64(dir + "/fp_a_hi.u64", a_hi);
+    write_u64(dir + "/fp_b_lo.u64", b_lo); write_u64(dir + "/fp_b_hi.u64", b_hi);
+    write_u64(dir + "/fp_add_lo.u64", add_lo); write_u64(dir + "/fp_add_hi.u64", add_hi);
+    write_u64(dir + "/fp_sub_lo.u64", sub_lo); write_u64(dir + "/fp_sub_hi.u64", sub_hi);
+    write_u64(dir + "/fp_neg_lo.u64", neg_lo); write_u64(dir + "/fp_neg_hi.u64", neg_hi);
+    write_u64(dir + "/fp_mul_lo.u64", mul_lo); write_u64(dir + "/fp_mul_hi.u64", mul_hi);
+    write_u64(dir + "/fp_fromw_lo.u64", fw_lo); write_u64(dir + "/fp_fromw_hi.u64", fw_hi);
+    write_u64(dir + "/fp_inv_in_lo.u64", inv_in_lo); write_u64(dir + "/fp_inv_in_hi.u64", inv_in_hi);
+    write_u64(dir + "/fp_inv_lo.u64", inv_lo); write_u64(dir + "/fp_inv_hi.u64", inv_hi);
+    write_u64(dir + "/fp_pow_a_lo.u64", pw_lo); write_u64(dir + "/fp_pow_a_hi.u64", pw_hi);
+    write_u64(dir + "/fp_pow_e.u64", pw_e); write_u64(dir + "/fp_pow_r_lo.u64", pw_rlo);
+    write_u64(dir + "/fp_pow_r_hi.u64", pw_rhi);
+    std::printf("fp vectors: %zu binop cases\n", n);
+}
+
+// ---------------------------------------------------------------- cipher fixtures
+struct OpRecord {
+    std::vector<uint64_t> stream;  // words consumed by the op (nonces then salts)
+};
+
+template <class F>
+static Cipher run_logged(F&& f, std::vector<uint64_t>& consumed) {
+    size_t before = g_log.size();
+    Cipher C = f();
+    consumed.assign(g_log.begin() + (long)before, g_log.end());
+    return C;
+}
+
+static std::vector<Fp> base_layer_R(const PubKey& pk, const SecKey& sk, const Cipher& C) {
+    std::vector<Fp> R;
+    for (const auto& L : C.L) {
+        if (L.rule == RRule::BASE) R.push_back(prf_R(pk, sk, L.seed));
+        else R.push_back(Fp{0, 0});
+    }
+    return R;
+}
+
+static void dump_R(const std::string& path, const std::vector<Fp>& R) {
+    std::vector<uint64_t> v;
+    for (auto& r : R) { v.push_back(r.lo); v.push_back(r.hi); }
+    write_u64(path, v);
+}
+
+static std::string fpjson(const Fp& f) {
+    char b[96];
+    std::snprintf(b, sizeof b, "[%" PRIu64 ", %" PRIu64 "]", f.lo, f.hi);
+    return b;
+}
+
+static void cmd_fixtures(const std::string& dir, int npairs, int chain_steps, int sq_steps) {
+    reseed(0x5EED0C00ULL);
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    g_logging = true;
+
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ",\n";
+    js << "  \"H_digest\": \"" << hex(pk.H_digest.data(), 32) << "\",\n";
+    js << "  \"params\": {\"B\": " << prm.B << ", \"m_bits\": " << prm.m_bits << ", \"n_bits\": " << prm.n_bits
+       << ", \"h_col_wt\": " << prm.h_col_wt << ", \"x_col_wt\": " << prm.x_col_wt << ", \"err_wt\": " << prm.err_wt
+       << ", \"edge_budget\": " << prm.edge_budget << "},\n";
+    {
+        std::vector<uint64_t> pg;
+        for (auto& f : pk.powg_B) { pg.push_back(f.lo); pg.push_back(f.hi); }
+        write_u64(dir + "/powg_B.u64", pg);
+        // H columns 0..63 dense (64 x 128 words = 64 KiB) to pin gen_H restatements cheaply.
+        std::vector<uint64_t> h;
+        for (int c = 0; c < 64; ++c) for (uint64_t w : pk.H[c].w) h.push_back(w);
+        write_u64(dir + "/H_cols0_63.u64", h);
+    }
+
+    // ---- fresh pairs: enc_value x/y, then ct_add / ct_sub / ct_mul
+    js << "  \"pairs\": [\n";
+    for (int p = 0; p < npairs; ++p) {
+        uint64_t x = splitmix64_next() % 1000003, y = splitmix64_next() % 1000003;
+        if (p == 0) { x = 2016733; y = 7083881; }   // test_main.cpp values
+        if (p == 1) { x = 0; y = 1; }
+        std::vector<uint64_t> dummy;
+        Cipher X = run_logged([&] { return enc_value(pk, sk, x); }, dummy);
+        Cipher Y = run_logged([&] { return enc_value(pk, sk, y); }, dummy);
+        std::string pre = dir + "/pair" + std::to_string(p);
+        write_ct(pre + "_x.ct", {X}, true);
+        write_ct(pre + "_y.ct", {Y}, true);
+        dump_R(pre + "_x_R.u64", base_layer_R(pk, sk, X));
+        dump_R(pre + "_y_R.u64", base_layer_R(pk, sk, Y));
+
+        std::vector<uint64_t> s_add, s_sub, s_mul;
+        Cipher S = run_logged([&] { return ct_add(pk, X, Y); }, s_add);
+        Cipher D = run_logged([&] { return ct_sub(pk, X, Y); }, s_sub);
+        auto t0 = std::chrono::steady_clock::now();
+        Cipher M = run_logged([&] { return ct_mul(pk, X, Y); }, s_mul);
+        auto t1 = std::chrono::steady_clock::now();
+        write_ct(pre + "_add.ct", {S}, true);
+        write_ct(pre + "_sub.ct", {D}, true);
+        write_ct(pre + "_mul_w.ct", {M}, false);
+        write_layers(pre + "_mul_layers.u64", M);
+        write_u64(pre + "_mul_stream.u64", s_mul);
+        write_u64(pre + "_mul_sigdig.u64", sigma_digests(M));
+        if (p == 0) write_ct(pre + "_mul.ct", {M}, true);   // one full product with sigmas
+        auto cm = commit_ct(pk, M), ca = commit_ct(pk, S), cs = commit_ct(pk, D);
+        Fp dm = dec_value(pk, sk, M);
+        js << "    {\"x\": " << x << ", \"y\": " << y << ", \"nx\": " << X.E.size() << ", \"ny\": " << Y.E.size()
+           << ", \"mul_edges\": " << M.E.size() << ", \"mul_layers\": " << M.L.size()
+           << ", \"add_stream\": " << s_add.size() << ", \"sub_stream\": " << s_sub.size()
+           << ", \"mul_stream\": " << s_mul.size()
+           << ", \"commit_mul\": \"" << hex(cm.data(), 32) << "\", \"commit_add\": \"" << hex(ca.data(), 32)
+           << "\", \"commit_sub\": \"" << hex(cs.data(), 32) << "\", \"dec_mul\": " << fpjson(dm)
+           << ", \"mul_ms\": " << std::chrono::duration<double, std::milli>(t1 - t0).count() << "}"
+           << (p + 1 < npairs ? "," : "") << "\n";
+        std::fflush(stdout);
+    }
+    js << "  ],\n";
+
+    // ---- chain x fresh (test_main.cpp:289-292 shape): c_k = c_{k-1} * x_k
+    js << "  \"chain\": [\n";
+    {
+        std::vector<uint64_t> dummy;
+        Cipher c = run_logged([&] { return enc_value(pk, sk, 2); }, dummy);
+        write_ct(dir + "/chain0.ct", {c}, true);
+        dump_R(dir + "/chain0_R.u64", base_layer_R(pk, sk, c));
+        for (int k = 1; k <= chain_steps; ++k) {
+            Cipher x = run_logged([&] { return enc_value(pk, sk, 2); }, dummy);
+            std::string pre = dir + "/chain" + std::to_string(k);
+            write_ct(pre + "_x.ct", {x}, true);
+            dump_R(pre + "_x_R.u64", base_layer_R(pk, sk, x));
+            std::vector<uint64_t> st;
+            Cipher n = run_logged([&] { return ct_mul(pk, c, x); }, st);
+            write_ct(pre + ".ct", {n}, false);
+            write_layers(pre + "_layers.u64", n);
+            write_u64(pre + "_stream.u64", st);
+            write_u64(pre + "_sigdig.u64", sigma_digests(n));
+            auto cm = commit_ct(pk, n);
+            Fp d = dec_value(pk, sk, n);
+            js << "    {\"step\": " << k << ", \"edges\": " << n.E.size() << ", \"layers\": " << n.L.size()
+               << ", \"stream\": " << st.size() << ", \"commit\": \"" << hex(cm.data(), 32)
+               << "\", \"dec\": " << fpjson(d) << "}" << (k < chain_steps ? "," : "") << "\n";
+            c = std::move(n);
+            std::printf("chain step %d edges %zu\n", k, c.E.size());
+            std::fflush(stdout);
+        }
+    }
+    js << "  ],\n";
+
+    // ---- squaring chain (test_depth.cpp:46): c <- c*c
+    js << "  \"square\": [\n";
+    {
+        std::vector<uint64_t> dummy;
+        Cipher c = run_logged([&] { return enc_value(pk, sk, 2); }, dummy);
+        write_ct(dir + "/sq0.ct", {c}, true);
+        dump_R(dir + "/sq0_R.u64", base_layer_R(pk, sk, c));
+        for (int k = 1; k <= sq_steps; ++k) {
+            std::vector<uint64_t> st;
+            Cipher n = run_logged([&] { return ct_mul(pk, c, c); }, st);
+            std::string pre = dir + "/sq" + std::to_string(k);
+            write_ct(pre + ".ct", {n}, false);
+            write_layers(pre + "_layers.u64", n);
+            write_u64(pre + "_stream.u64", st);
+            write_u64(pre + "_sigdig.u64", sigma_digests(n));
+            auto cm = commit_ct(pk, n);
+            Fp d = dec_value(pk, sk, n);
+            js << "    {\"step\": " << k << ", \"edges\": " << n.E.size() << ", \"layers\": " << n.L.size()
+               << ", \"stream\": " << st.size() << ", \"commit\": \"" << hex(cm.data(), 32)
+               << "\", \"dec\": " << fpjson(d) << "}" << (k < sq_steps ? "," : "") << "\n";
+            c = std::move(n);
+            std::printf("square step %d edges %zu\n", k, c.E.size());
+            std::fflush(stdout);
+        }
+    }
+    js << "  ],\n";
+
+    // ---- guard_budget / compact_edges on a hand-made over-budget cipher is too large to
+    // commit; instead exercise compact_edges directly on a small cipher with duplicates and
+    // non-canonical weights (encrypt.hpp:39-71) using a tiny edge_budget.
+    {
+        PubKey pk2 = pk;
+        pk2.prm.edge_budget = 16;
+        std::vector<uint64_t> dummy;
+        Cipher X = run_logged([&] { return enc_value(pk, sk, 5); }, dummy);
+        Cipher Y = run_logged([&] { return enc_value(pk, sk, 7); }, dummy);
+        // inject duplicates of (layer,idx,ch) and non-canonical weights into Y
+        Y.E[1].idx = Y.E[0].idx; Y.E[1].ch = Y.E[0].ch; Y.E[1].layer_id = Y.E[0].layer_id;
+        Y.E[2].w = Fp{MAXU, MAXU};
+        Y.E[3].w = Fp{MAXU - 7, 0x8000000000000000ULL};
+        write_ct(dir + "/guard_x.ct", {X}, true);
+        write_ct(dir + "/guard_y.ct", {Y}, true);
+        std::vector<uint64_t> st;
+        Cipher S = run_logged([&] { return ct_add(pk2, X, Y); }, st);
+        write_ct(dir + "/guard_add.ct", {S}, true);
+        auto c = commit_ct(pk, S);
+        js << "  \"guard\": {\"edge_budget\": 16, \"edges\": " << S.E.size() << ", \"layers\": " << S.L.size()
+           << ", \"commit\": \"" << hex(c.data(), 32) << "\"},\n";
+    }
+    js << "  \"generator\": \"oracle/ref_harness.cpp (reference pvac-hfhe 0.1.0, g++ -O2)\"\n}\n";
+    std::ofstream(dir + "/manifest.json") << js.str();
+}
+
+// ---------------------------------------------------------------- timing (CPU baseline leg)
+// Times the reference's own ct_mul (WITH sigma, arithmetic.hpp:47-106) on fresh pairs.
+static void cmd_time_mul(int npairs, int threads) {
+    reseed(0x5EED0D00ULL);
+    g_logging = false;
+    Params prm; PubKey pk; SecKey sk;
+    keygen(prm, pk, sk);
+    std::vector<Cipher> X, Y;
+    for (int i = 0; i < 2 * threads; ++i) { X.push_back(enc_value(pk, sk, i + 3)); Y.push_back(enc_value(pk, sk, i + 5)); }
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    size_t edges_total[256] = {0};
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            for (int i = t; i < npairs; i += threads) {
+                Cipher M = ct_mul(pk, X[(size_t)(i % (2 * threads))], Y[(size_t)(i % (2 * threads))]);
+                edges_total[t] += M.E.size();
+            }
+        });
+    for (auto& x : th) x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    double s = std::chrono::duration<double>(t1 - t0).count();
+    size_t et = 0;
+    for (int t = 0; t < threads; ++t) et += edges_total[t];
+    std::printf("{\"pairs\": %d, \"threads\": %d, \"seconds\": %.6f, \"ct_mul_per_s\": %.3f, \"edges\": %zu}\n",
+                npairs, threads, s, npairs / s, et);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) { std::fprintf(stderr, "usage: ref_harness fp|fixtures|time_mul ...\n"); return 2; }
+    std::string cmd = argv[1];
+    if (cmd == "fp" && argc >= 3) { cmd_fp(argv[2]); return 0; }
+    if (cmd == "fixtures" && argc >= 3) {
+        int np = argc > 3 ? std::atoi(argv[3]) : 8;
+        int cs = argc > 4 ? std::atoi(argv[4]) : 3;
+        int ss = argc > 5 ? std::atoi(argv[5]) : 2;
+        cmd_fixtures(argv[2], np, cs, ss);
+        return 0;
+    }
+    if (cmd == "time_mul") {
+        int np = argc > 2 ? std::atoi(argv[2]) : 64;
+        int th = argc > 3 ? std::atoi(argv[3]) : 1;
+        cmd_time_mul(np, th);
+        return 0;
+    }
+    std::fprintf(stderr, "bad args\n");
+    return 2;
+}

@@ -1,0 +1,330 @@
+"""Test-side helpers: fixture loading (.ct reader/writer in numpy) and the ctypes binding to
+the CPU oracle (oracle/liboracle.so). TEST INFRASTRUCTURE ONLY."""
+import ctypes as C
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+REF = os.path.join(GOLD, "ref")
+
+LAYER_DT = np.dtype([("rule", "<u4"), ("pa", "<u4"), ("pb", "<u4"), ("pad", "<u4"),
+                     ("ztag", "<u8"), ("nonce_lo", "<u8"), ("nonce_hi", "<u8")])
+assert LAYER_DT.itemsize == 40
+
+CT_MAGIC = 0x66699666
+P_LO, P_HI = (1 << 64) - 1, (1 << 63) - 1
+P = (1 << 127) - 1
+M64 = (1 << 64) - 1
+
+
+class Cipher:
+    """Flat SoA view of one pvac::Cipher (reference include/pvac/core/types.hpp:96-119)."""
+
+    def __init__(self, layers, meta, w_lo, w_hi, sigma=None):
+        self.layers = np.ascontiguousarray(layers, dtype=LAYER_DT)
+        self.meta = np.ascontiguousarray(meta, dtype=np.uint64)
+        self.w_lo = np.ascontiguousarray(w_lo, dtype=np.uint64)
+        self.w_hi = np.ascontiguousarray(w_hi, dtype=np.uint64)
+        self.sigma = None if sigma is None else np.ascontiguousarray(sigma, dtype=np.uint64)
+
+    @property
+    def nL(self):
+        return len(self.layers)
+
+    @property
+    def nE(self):
+        return len(self.meta)
+
+    def layer_id(self):
+        return (self.meta & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+    def idx(self):
+        return ((self.meta >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16)
+
+    def ch(self):
+        return ((self.meta >> np.uint64(48)) & np.uint64(0xFF)).astype(np.uint8)
+
+
+def pack_meta(layer, idx, ch):
+    return (np.asarray(layer, np.uint64) | (np.asarray(idx, np.uint64) << np.uint64(32))
+            | (np.asarray(ch, np.uint64) << np.uint64(48)))
+
+
+def read_ct(path):
+    """Parse the reference .ct format (reference tests/add.cpp:22-155)."""
+    with open(path, "rb") as f:
+        buf = f.read()
+    magic, ver, n = struct.unpack_from("<IIQ", buf, 0)
+    assert magic == CT_MAGIC and ver == 1, path
+    off = 16
+    out = []
+    for _ in range(n):
+        nL, nE = struct.unpack_from("<II", buf, off)
+        off += 8
+        layers = np.zeros(nL, LAYER_DT)
+        for i in range(nL):
+            rule = buf[off]
+            off += 1
+            layers[i]["rule"] = rule
+            if rule == 0:
+                z, lo, hi = struct.unpack_from("<QQQ", buf, off)
+                off += 24
+                layers[i]["ztag"], layers[i]["nonce_lo"], layers[i]["nonce_hi"] = z, lo, hi
+            elif rule == 1:
+                pa, pb = struct.unpack_from("<II", buf, off)
+                off += 8
+                layers[i]["pa"], layers[i]["pb"] = pa, pb
+            else:
+                off += 24
+        meta = np.zeros(nE, np.uint64)
+        wlo = np.zeros(nE, np.uint64)
+        whi = np.zeros(nE, np.uint64)
+        sig = []
+        nbits_seen = None
+        for e in range(nE):
+            lid, idx, ch, _pad, lo, hi, nbits = struct.unpack_from("<IHBBQQI", buf, off)
+            off += 28
+            meta[e] = lid | (idx << 32) | (ch << 48)
+            wlo[e], whi[e] = lo, hi
+            nw = (nbits + 63) // 64
+            if nw:
+                sig.append(np.frombuffer(buf, np.uint64, nw, off))
+            off += 8 * nw
+            nbits_seen = nbits
+        sigma = np.stack(sig) if sig and len(sig) == nE else None
+        c = Cipher(layers, meta, wlo, whi, sigma)
+        c.nbits = nbits_seen or 0
+        out.append(c)
+    assert off == len(buf), (path, off, len(buf))
+    return out
+
+
+def write_ct(ciphers, nbits=8192):
+    """Serialize to the reference .ct byte format (reference tests/add.cpp:86-155)."""
+    parts = [struct.pack("<IIQ", CT_MAGIC, 1, len(ciphers))]
+    for c in ciphers:
+        parts.append(struct.pack("<II", c.nL, c.nE))
+        for L in c.layers:
+            if L["rule"] == 0:
+                parts.append(struct.pack("<BQQQ", 0, int(L["ztag"]), int(L["nonce_lo"]), int(L["nonce_hi"])))
+            elif L["rule"] == 1:
+                parts.append(struct.pack("<BII", 1, int(L["pa"]), int(L["pb"])))
+            else:
+                parts.append(struct.pack("<B", int(L["rule"])) + b"\0" * 24)
+        for e in range(c.nE):
+            m = int(c.meta[e])
+            nb = nbits if c.sigma is not None else 0
+            parts.append(struct.pack("<IHBBQQI", m & 0xFFFFFFFF, (m >> 32) & 0xFFFF, (m >> 48) & 0xFF, 0,
+                                     int(c.w_lo[e]), int(c.w_hi[e]), nb))
+            if c.sigma is not None:
+                parts.append(c.sigma[e].tobytes())
+    return b"".join(parts)
+
+
+def read_u64(name):
+    return np.fromfile(os.path.join(REF, name), dtype=np.uint64)
+
+
+def read_layers_u64(name):
+    """The harness' full layer dump: rule,pa,pb,ztag,nlo,nhi as 6 u64 per layer."""
+    a = read_u64(name).reshape(-1, 6)
+    L = np.zeros(len(a), LAYER_DT)
+    L["rule"], L["pa"], L["pb"] = a[:, 0], a[:, 1], a[:, 2]
+    L["ztag"], L["nonce_lo"], L["nonce_hi"] = a[:, 3], a[:, 4], a[:, 5]
+    return L
+
+
+def to_int(lo, hi):
+    return (int(hi) << 64) | int(lo)
+
+
+# --------------------------------------------------------------------------- oracle binding
+class _OrcLayerP(C.Structure):
+    pass
+
+
+class OrcParams(C.Structure):
+    _fields_ = [("B", C.c_uint32), ("m_bits", C.c_uint32), ("n_bits", C.c_uint32), ("h_col_wt", C.c_uint32),
+                ("x_col_wt", C.c_uint32), ("err_wt", C.c_uint32), ("edge_budget", C.c_uint64),
+                ("canon_tag", C.c_uint64)]
+
+
+class OrcCipher(C.Structure):
+    _fields_ = [("nL", C.c_uint64), ("nE", C.c_uint64), ("capL", C.c_uint64), ("capE", C.c_uint64),
+                ("layers", C.c_void_p), ("meta", C.c_void_p), ("w_lo", C.c_void_p), ("w_hi", C.c_void_p),
+                ("sigma", C.c_void_p), ("sigma_words", C.c_uint32)]
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def default_params(canon_tag=0, edge_budget=1200000, B=337):
+    return OrcParams(B=B, m_bits=8192, n_bits=16384, h_col_wt=192, x_col_wt=128, err_wt=128,
+                     edge_budget=edge_budget, canon_tag=canon_tag)
+
+
+class Oracle:
+    _inst = None
+
+    @classmethod
+    def load(cls):
+        if cls._inst is None:
+            so = os.path.join(ROOT, "oracle", "liboracle.so")
+            if not os.path.exists(so):
+                subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"])
+            cls._inst = cls(C.CDLL(so))
+        return cls._inst
+
+    def __init__(self, lib):
+        self.lib = lib
+        u64p = C.c_void_p
+        for name in ("orc_fp_add", "orc_fp_sub", "orc_fp_mul"):
+            getattr(lib, name).argtypes = [u64p] * 6 + [C.c_size_t]
+        lib.orc_fp_neg.argtypes = [u64p] * 4 + [C.c_size_t]
+        lib.orc_fp_inv.argtypes = [u64p] * 4 + [C.c_size_t]
+        lib.orc_fp_from_words.argtypes = [u64p] * 4 + [C.c_size_t]
+        lib.orc_fp_pow.argtypes = [u64p] * 5 + [C.c_size_t]
+        lib.orc_fp_binop_timed.argtypes = [C.c_int] + [u64p] * 6 + [C.c_size_t, C.c_int]
+        lib.orc_fp_binop_timed.restype = C.c_double
+        lib.orc_sha256.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p]
+        lib.orc_layer_ztag.argtypes = [C.c_uint64] * 3
+        lib.orc_layer_ztag.restype = C.c_uint64
+        lib.orc_prg_choose_k.argtypes = [C.c_int, C.c_int, C.c_char_p, u64p, C.c_int, C.c_void_p]
+        lib.orc_gen_H.argtypes = [C.POINTER(OrcParams), u64p, C.c_void_p]
+        lib.orc_sigma_from_H.argtypes = [C.POINTER(OrcParams), u64p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                         C.c_uint32, C.c_uint32, C.c_uint64, u64p]
+        lib.orc_ct_add.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCipher), C.POINTER(OrcCipher), C.c_int,
+                                   C.POINTER(OrcCipher)]
+        lib.orc_ct_mul.argtypes = [C.POINTER(OrcParams), u64p, C.POINTER(OrcCipher), C.POINTER(OrcCipher), u64p,
+                                   u64p, C.POINTER(OrcCipher)]
+        lib.orc_ct_mul_caps.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCipher), C.POINTER(OrcCipher),
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        lib.orc_commit_ct.argtypes = [C.POINTER(OrcParams), C.c_void_p, C.POINTER(OrcCipher), C.c_void_p]
+        lib.orc_dec_value.argtypes = [C.POINTER(OrcParams), u64p, C.POINTER(OrcCipher), u64p, u64p]
+        lib.orc_bucket_count_after_reserve.argtypes = [C.c_uint64]
+        lib.orc_bucket_count_after_reserve.restype = C.c_uint64
+        lib.orc_ct_mul_batch_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 12 + \
+            [C.c_int, u64p, u64p]
+        lib.orc_ct_mul_batch_timed.restype = C.c_double
+
+    # ---- Fp
+    def fp(self, op, a_lo, a_hi, b_lo=None, b_hi=None):
+        a_lo = np.ascontiguousarray(a_lo, np.uint64)
+        a_hi = np.ascontiguousarray(a_hi, np.uint64)
+        n = len(a_lo)
+        o_lo, o_hi = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+        if op in ("add", "sub", "mul"):
+            b_lo = np.ascontiguousarray(b_lo, np.uint64)
+            b_hi = np.ascontiguousarray(b_hi, np.uint64)
+            getattr(self.lib, "orc_fp_" + op)(_p(a_lo), _p(a_hi), _p(b_lo), _p(b_hi), _p(o_lo), _p(o_hi), n)
+        elif op == "pow":
+            e = np.ascontiguousarray(b_lo, np.uint64)
+            self.lib.orc_fp_pow(_p(a_lo), _p(a_hi), _p(e), _p(o_lo), _p(o_hi), n)
+        else:
+            name = {"neg": "orc_fp_neg", "inv": "orc_fp_inv", "from_words": "orc_fp_from_words"}[op]
+            getattr(self.lib, name)(_p(a_lo), _p(a_hi), _p(o_lo), _p(o_hi), n)
+        return o_lo, o_hi
+
+    def sha256(self, msg: bytes):
+        out = C.create_string_buffer(32)
+        self.lib.orc_sha256(msg, len(msg), out)
+        return out.raw
+
+    def ztag(self, canon, lo, hi):
+        return self.lib.orc_layer_ztag(canon, lo, hi)
+
+    def choose_k(self, k, N, label, words):
+        w = np.ascontiguousarray(words, np.uint64)
+        out = np.zeros(max(k, 1), np.int32)
+        n = self.lib.orc_prg_choose_k(k, N, label.encode(), _p(w), len(w), out.ctypes.data_as(C.c_void_p))
+        return out[:n]
+
+    def gen_H(self, canon_tag):
+        prm = default_params(canon_tag)
+        H = np.zeros((16384, 128), np.uint64)
+        d = C.create_string_buffer(32)
+        self.lib.orc_gen_H(C.byref(prm), _p(H), d)
+        return H, d.raw
+
+    def sigma(self, canon, H, ztag, nlo, nhi, idx, ch, salt):
+        prm = default_params(canon)
+        out = np.zeros(128, np.uint64)
+        self.lib.orc_sigma_from_H(C.byref(prm), _p(H), ztag, nlo, nhi, idx, ch, salt, _p(out))
+        return out
+
+    # ---- ciphers
+    @staticmethod
+    def _view(c: Cipher):
+        v = OrcCipher(nL=c.nL, nE=c.nE, capL=c.nL, capE=c.nE, layers=_p(c.layers), meta=_p(c.meta),
+                      w_lo=_p(c.w_lo), w_hi=_p(c.w_hi), sigma=_p(c.sigma), sigma_words=128)
+        v._keep = c
+        return v
+
+    @staticmethod
+    def _out(capL, capE, with_sigma):
+        c = Cipher(np.zeros(capL, LAYER_DT), np.zeros(capE, np.uint64), np.zeros(capE, np.uint64),
+                   np.zeros(capE, np.uint64), np.zeros((capE, 128), np.uint64) if with_sigma else None)
+        return c, Oracle._view(c)
+
+    @staticmethod
+    def _trim(c: Cipher, v: OrcCipher):
+        return Cipher(c.layers[:v.nL], c.meta[:v.nE], c.w_lo[:v.nE], c.w_hi[:v.nE],
+                      None if c.sigma is None else c.sigma[:v.nE])
+
+    def ct_add(self, A, B, negate=False, canon_tag=0, edge_budget=1200000):
+        prm = default_params(canon_tag, edge_budget)
+        oc, ov = self._out(A.nL + B.nL, A.nE + B.nE, A.sigma is not None and B.sigma is not None)
+        rc = self.lib.orc_ct_add(C.byref(prm), C.byref(self._view(A)), C.byref(self._view(B)), int(negate),
+                                 C.byref(ov))
+        assert rc == 0
+        return self._trim(oc, ov)
+
+    def ct_mul(self, A, B, nonces, salts=None, H=None, canon_tag=0, edge_budget=1200000):
+        prm = default_params(canon_tag, edge_budget)
+        va, vb = self._view(A), self._view(B)
+        capL, capE = C.c_uint64(), C.c_uint64()
+        self.lib.orc_ct_mul_caps(C.byref(prm), C.byref(va), C.byref(vb), C.byref(capL), C.byref(capE))
+        oc, ov = self._out(capL.value, capE.value, H is not None)
+        nonces = np.ascontiguousarray(nonces, np.uint64)
+        salts = None if salts is None else np.ascontiguousarray(salts, np.uint64)
+        rc = self.lib.orc_ct_mul(C.byref(prm), _p(H), C.byref(va), C.byref(vb), _p(nonces), _p(salts),
+                                 C.byref(ov))
+        assert rc == 0
+        return self._trim(oc, ov)
+
+    def commit(self, c: Cipher, canon_tag, H_digest: bytes):
+        prm = default_params(canon_tag)
+        out = C.create_string_buffer(32)
+        self.lib.orc_commit_ct(C.byref(prm), H_digest, C.byref(self._view(c)), out)
+        return out.raw
+
+    def dec(self, c: Cipher, powg, R):
+        prm = default_params()
+        out = np.zeros(2, np.uint64)
+        R = np.ascontiguousarray(R, np.uint64)
+        self.lib.orc_dec_value(C.byref(prm), _p(np.ascontiguousarray(powg, np.uint64)), C.byref(self._view(c)),
+                               _p(R), _p(out))
+        return int(out[0]), int(out[1])
+
+    def bucket_count(self, n):
+        return self.lib.orc_bucket_count_after_reserve(n)
+
+
+def R_for(cipher: Cipher, R_inputs):
+    """BASE-layer R of a product/sum cipher by matching layer seeds against input ciphers'."""
+    R = np.zeros(2 * cipher.nL, np.uint64)
+    table = {}
+    for c, r in R_inputs:
+        r = r.reshape(-1, 2)
+        for i, L in enumerate(c.layers):
+            if L["rule"] == 0:
+                table[(int(L["ztag"]), int(L["nonce_lo"]), int(L["nonce_hi"]))] = r[i]
+    for i, L in enumerate(cipher.layers):
+        if L["rule"] == 0:
+            R[2 * i:2 * i + 2] = table[(int(L["ztag"]), int(L["nonce_lo"]), int(L["nonce_hi"]))]
+    return R

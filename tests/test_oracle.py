@@ -1,0 +1,201 @@
+"""Pin the CPU oracle (oracle/pvac_oracle.cpp) against golden vectors minted by the UNMODIFIED
+reference (oracle/ref_harness.cpp, tests/golden/ref) and the reference's own shipped data
+(tests/golden/bounty). CPU-only."""
+import numpy as np
+import pytest
+
+from helpers import (GOLD, REF, Cipher, read_ct, read_layers_u64, read_u64, write_ct, R_for, to_int, P)
+import os
+
+
+# ----------------------------------------------------------------------------- Fp (core/field.hpp)
+@pytest.mark.parametrize("op", ["add", "sub", "mul"])
+def test_fp_binop_golden(oracle, op):
+    a_lo, a_hi, b_lo, b_hi = (read_u64(f"fp_{n}.u64") for n in ("a_lo", "a_hi", "b_lo", "b_hi"))
+    lo, hi = oracle.fp(op, a_lo, a_hi, b_lo, b_hi)
+    assert np.array_equal(lo, read_u64(f"fp_{op}_lo.u64"))
+    assert np.array_equal(hi, read_u64(f"fp_{op}_hi.u64"))
+
+
+def test_fp_neg_fromwords_inv_pow_golden(oracle):
+    a_lo, a_hi = read_u64("fp_a_lo.u64"), read_u64("fp_a_hi.u64")
+    lo, hi = oracle.fp("neg", a_lo, a_hi)
+    assert np.array_equal(lo, read_u64("fp_neg_lo.u64")) and np.array_equal(hi, read_u64("fp_neg_hi.u64"))
+    lo, hi = oracle.fp("from_words", a_lo, a_hi)
+    assert np.array_equal(lo, read_u64("fp_fromw_lo.u64")) and np.array_equal(hi, read_u64("fp_fromw_hi.u64"))
+    lo, hi = oracle.fp("inv", read_u64("fp_inv_in_lo.u64"), read_u64("fp_inv_in_hi.u64"))
+    assert np.array_equal(lo, read_u64("fp_inv_lo.u64")) and np.array_equal(hi, read_u64("fp_inv_hi.u64"))
+    lo, hi = oracle.fp("pow", read_u64("fp_pow_a_lo.u64"), read_u64("fp_pow_a_hi.u64"), read_u64("fp_pow_e.u64"))
+    assert np.array_equal(lo, read_u64("fp_pow_r_lo.u64")) and np.array_equal(hi, read_u64("fp_pow_r_hi.u64"))
+
+
+def test_fp_canonical_matches_bigint(oracle):
+    """Canonical inputs: add/sub/mul equal exact integer arithmetic mod p (test_fp_core.cpp spirit)."""
+    rng = np.random.default_rng(7)
+    n = 2000
+    a = [int(x) % P for x in rng.integers(0, 2**63, n, dtype=np.uint64).astype(object) * (2**64) +
+         rng.integers(0, 2**63, n, dtype=np.uint64).astype(object)]
+    b = [int(x) % P for x in rng.integers(0, 2**63, n, dtype=np.uint64).astype(object) * (2**64) +
+         rng.integers(0, 2**63, n, dtype=np.uint64).astype(object)]
+    alo = np.array([x & (2**64 - 1) for x in a], np.uint64)
+    ahi = np.array([x >> 64 for x in a], np.uint64)
+    blo = np.array([x & (2**64 - 1) for x in b], np.uint64)
+    bhi = np.array([x >> 64 for x in b], np.uint64)
+    for op, f in (("add", lambda x, y: (x + y) % P), ("sub", lambda x, y: (x - y) % P),
+                  ("mul", lambda x, y: (x * y) % P)):
+        lo, hi = oracle.fp(op, alo, ahi, blo, bhi)
+        got = [to_int(l, h) for l, h in zip(lo, hi)]
+        assert got == [f(x, y) for x, y in zip(a, b)], op
+
+
+# ----------------------------------------------------------------------------- hashing / PRG
+def test_sha256_abc_kat(oracle):
+    """Known answer from the reference's own test (tests/test_prf.cpp:11-25)."""
+    assert oracle.sha256(b"abc").hex() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
+
+
+def test_gen_H_digest_and_columns(oracle, manifest, H_dense):
+    ref_cols = read_u64("H_cols0_63.u64").reshape(64, 128)
+    assert np.array_equal(H_dense[:64], ref_cols)
+    # every column has exactly h_col_wt = 192 bits
+    pc = np.unpackbits(H_dense[:256].view(np.uint8), axis=1).sum(axis=1)
+    assert (pc == 192).all()
+
+
+def test_bucket_count_matches_survey(oracle):
+    # bucket_count(1560) = 1613, bucket_count(48800) = 49201 (libstdc++ GCC 11)
+    assert oracle.bucket_count(1560) == 1613
+    assert oracle.bucket_count(48800) == 49201
+
+
+# ----------------------------------------------------------------------------- ciphertext ops
+def _pair(p):
+    x = read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0]
+    y = read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0]
+    return x, y
+
+
+def _same(a: Cipher, b: Cipher, layers=True, weights=True, sigma=False):
+    if layers:
+        for f in ("rule", "pa", "pb", "ztag", "nonce_lo", "nonce_hi"):
+            assert np.array_equal(a.layers[f], b.layers[f]), f
+    assert np.array_equal(a.meta, b.meta)
+    if weights:
+        assert np.array_equal(a.w_lo, b.w_lo) and np.array_equal(a.w_hi, b.w_hi)
+    if sigma:
+        assert np.array_equal(a.sigma, b.sigma)
+
+
+def _ct_layers_view(c: Cipher):
+    """.ct drops seeds of PROD layers and pa/pb of BASE layers; project accordingly."""
+    L = c.layers.copy()
+    prod = L["rule"] == 1
+    L["ztag"][prod] = 0
+    L["nonce_lo"][prod] = 0
+    L["nonce_hi"][prod] = 0
+    L["pa"][~prod] = 0
+    L["pb"][~prod] = 0
+    return Cipher(L, c.meta, c.w_lo, c.w_hi, c.sigma)
+
+
+@pytest.mark.parametrize("p", range(8))
+def test_ct_add_sub_golden(oracle, manifest, p):
+    x, y = _pair(p)
+    for op, neg in (("add", False), ("sub", True)):
+        got = oracle.ct_add(x, y, negate=neg)
+        ref = read_ct(os.path.join(REF, f"pair{p}_{op}.ct"))[0]
+        _same(_ct_layers_view(got), ref, sigma=True)
+        H_digest = bytes.fromhex(manifest["H_digest"])
+        assert oracle.commit(got, manifest["canon_tag"], H_digest).hex() == manifest["pairs"][p][f"commit_{op}"]
+
+
+@pytest.mark.parametrize("p", range(8))
+def test_ct_mul_weights_golden(oracle, manifest, p):
+    x, y = _pair(p)
+    stream = read_u64(f"pair{p}_mul_stream.u64")
+    nn = 2 * x.nL * y.nL
+    got = oracle.ct_mul(x, y, stream[:nn], stream[nn:], canon_tag=manifest["canon_tag"])
+    ref = read_ct(os.path.join(REF, f"pair{p}_mul_w.ct"))[0]
+    _same(_ct_layers_view(got), ref)
+    full_layers = read_layers_u64(f"pair{p}_mul_layers.u64")
+    for f in ("rule", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(got.layers[f], full_layers[f]), f
+    assert len(stream) == nn + got.nE            # one salt per emitted edge (arithmetic.hpp:90-94)
+    # decryption round trip with fixture R values (ops/decrypt.hpp)
+    powg = read_u64("powg_B.u64")
+    R = R_for(got, [(x, read_u64(f"pair{p}_x_R.u64")), (y, read_u64(f"pair{p}_y_R.u64"))])
+    assert list(oracle.dec(got, powg, R)) == manifest["pairs"][p]["dec_mul"]
+    m = manifest["pairs"][p]
+    assert oracle.dec(got, powg, R)[0] == (m["x"] * m["y"]) % P
+
+
+@pytest.mark.parametrize("p", [0, 3])
+def test_ct_mul_sigma_golden(oracle, manifest, H_dense, p):
+    x, y = _pair(p)
+    stream = read_u64(f"pair{p}_mul_stream.u64")
+    nn = 2 * x.nL * y.nL
+    got = oracle.ct_mul(x, y, stream[:nn], stream[nn:], H=H_dense, canon_tag=manifest["canon_tag"])
+    H_digest = bytes.fromhex(manifest["H_digest"])
+    assert oracle.commit(got, manifest["canon_tag"], H_digest).hex() == manifest["pairs"][p]["commit_mul"]
+    if p == 0:
+        ref = read_ct(os.path.join(REF, "pair0_mul.ct"))[0]
+        _same(_ct_layers_view(got), ref, sigma=True)
+
+
+def _chain_inputs():
+    c0 = read_ct(os.path.join(REF, "chain0.ct"))[0]
+    return c0
+
+
+@pytest.mark.parametrize("kind,steps", [("chain", 3), ("sq", 2)])
+def test_chain_and_square_golden(oracle, manifest, kind, steps):
+    c = read_ct(os.path.join(REF, f"{kind}0.ct"))[0]
+    Rin = [(c, read_u64(f"{kind}0_R.u64"))]
+    cur = c
+    for k in range(1, steps + 1):
+        if kind == "chain":
+            x = read_ct(os.path.join(REF, f"chain{k}_x.ct"))[0]
+            Rin.append((x, read_u64(f"chain{k}_x_R.u64")))
+        else:
+            x = cur
+        stream = read_u64(f"{kind}{k}_stream.u64")
+        nn = 2 * cur.nL * x.nL
+        got = oracle.ct_mul(cur, x, stream[:nn], stream[nn:], canon_tag=manifest["canon_tag"])
+        ref = read_ct(os.path.join(REF, f"{kind}{k}.ct"))[0]
+        _same(_ct_layers_view(got), ref)
+        full = read_layers_u64(f"{kind}{k}_layers.u64")
+        assert np.array_equal(got.layers["ztag"], full["ztag"])
+        rec = manifest["chain" if kind == "chain" else "square"][k - 1]
+        assert got.nE == rec["edges"] and got.nL == rec["layers"]
+        R = R_for(got, Rin)
+        assert list(oracle.dec(got, read_u64("powg_B.u64"), R)) == rec["dec"]
+        # the next step multiplies the full (layer-seeded) product
+        cur = Cipher(full, got.meta, got.w_lo, got.w_hi)
+
+
+def test_guard_compact_edges_golden(oracle, manifest):
+    """guard_budget -> compact_edges (encrypt.hpp:39-71,106-111) with duplicates + non-canonical w."""
+    x = read_ct(os.path.join(REF, "guard_x.ct"))[0]
+    y = read_ct(os.path.join(REF, "guard_y.ct"))[0]
+    got = oracle.ct_add(x, y, edge_budget=16)
+    ref = read_ct(os.path.join(REF, "guard_add.ct"))[0]
+    _same(_ct_layers_view(got), ref, sigma=True)
+    H_digest = bytes.fromhex(manifest["H_digest"])
+    assert oracle.commit(got, manifest["canon_tag"], H_digest).hex() == manifest["guard"]["commit"]
+
+
+def test_bounty2_sum_is_ct_add_bytewise(oracle):
+    """The reference ships sum.ct = combine_ciphers(a.ct, b.ct) (tests/add.cpp:220-228)."""
+    a = read_ct(os.path.join(GOLD, "bounty", "a.ct"))[0]
+    b = read_ct(os.path.join(GOLD, "bounty", "b.ct"))[0]
+    s = oracle.ct_add(a, b)
+    with open(os.path.join(GOLD, "bounty", "sum.ct"), "rb") as f:
+        assert write_ct([_ct_layers_view(s)]) == f.read()
+
+
+def test_ct_reader_roundtrip_seed3():
+    path = os.path.join(GOLD, "bounty", "seed3.ct")
+    cts = read_ct(path)
+    assert len(cts) == 9
+    with open(path, "rb") as f:
+        assert write_ct(cts) == f.read()
