@@ -1,0 +1,332 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X pvac-hfhe engine (driver contract).
+
+Workload (BASELINE.json cfg 3): batched weights-only ct_mul over fresh-shaped Cipher pairs
+(2 BASE layers x 20 distinct (idx, ch) edges per layer, default Params B=337), 2^20 pairs per
+GPU, inputs resident in HBM. One step = plan (sizing) + exec over the whole batch. Multi-GPU:
+one process per GPU; each rank owns an independent shard (weak scaling); the only collective
+is the gather of per-rank output totals (global CSR offsets), over RCCL.
+
+Also reported (side fields): cfg 2 element-wise Fp127 add/mul at 2^24, and full ct_mul WITH
+sigma (the reference's complete ct_mul) on a smaller batch, each with its CPU baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "ct_mul/sec (batched Cipher) + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU")
+    ap.add_argument("--epl", type=int, default=20, help="edges per BASE layer")
+    ap.add_argument("--cpu-pairs", type=int, default=1 << 17)
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--sigma-pairs", type=int, default=1 << 12)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from pvac_hfhe_cppbyv_amd import Engine
+
+    eng = Engine(device=local, canon_tag=0x5EED0003)
+    dev = eng.device
+    n = args.pairs
+    seed = 0x5EED0003 + 0x1000 * rank
+    A = eng.gen_fresh(n, seed, args.epl)
+    B = eng.gen_fresh(n, seed + 1, args.epl)
+    nonces = None
+    totals = torch.zeros(world, dtype=torch.int64, device=dev)
+    mine = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        nonlocal nonces
+        Cb, plan = eng.ct_mul_plan(A, B)
+        if nonces is None or nonces.numel() < 2 * plan.total_layer_slots:
+            nonces = torch.empty(2 * plan.total_layer_slots, dtype=torch.int64, device=dev)
+            eng.fill_random(nonces, seed + 2)
+        out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+        if world > 1:   # gather-only: per-rank output totals -> global offsets of the sharded result
+            mine.copy_(out.e_cnt[:n].sum().view(1))
+            dist.all_gather_into_tensor(totals, mine)
+        return out, plan
+
+    for _ in range(args.warmup):
+        out, plan = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.timing_reset()
+    eng.timing(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, plan = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.timing(False)
+    kern_ms, kern_launches = eng.timing_get("ct_mul_small")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * n / (elapsed / args.steps)
+
+    # ---- algorithmic bytes of the dominant kernel: per pair
+    #   24 B x (|A.E| + |B.E| + |C.E|)  edge records (meta 8 + w 16) read / written
+    # + 40 B x (|A.L| + |B.L| + |C.L|)  layer records
+    # + 16 B x |A.L||B.L|               nonces
+    # + 96 B                            offsets / counts of A, B, C
+    e_cnt = out.e_cnt[:n].to(torch.float64)
+    l_cnt = out.l_cnt[:n].to(torch.float64)
+    la, lb = A.l_cnt[:n].to(torch.float64), B.l_cnt[:n].to(torch.float64)
+    na, nb = A.e_cnt[:n].to(torch.float64), B.e_cnt[:n].to(torch.float64)
+    alg_bytes = float((24 * (na + nb + e_cnt) + 40 * (la + lb + l_cnt) + 16 * la * lb + 96).sum().item())
+    avg_kernel_ms = kern_ms / max(kern_launches, 1)
+    achieved = alg_bytes / (avg_kernel_ms / 1000.0) / 1e9 if avg_kernel_ms > 0 else None
+    out_edges = float(e_cnt.sum().item())
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "ct_mul/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (device splitmix64 generator, cfg-3 fresh-shaped ciphers)",
+        "config": {
+            "workload": "cfg3: 2^20 fresh-shaped Cipher pairs per GPU, batched ct_mul (weights + layers + "
+                        "reference emit order; sigma in side field), default Params B=337",
+            "pairs_per_gpu": n,
+            "edges_per_layer": args.epl,
+            "global_pairs": world * n,
+            "output_edges_per_pair": out_edges / n,
+            "parallelism": f"dp{world} (independent pair shards, gather of totals over RCCL)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_ct_mul_small",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": None,
+            "alg_bytes_per_launch": alg_bytes,
+            "avg_kernel_ms": avg_kernel_ms,
+            "kernel_launches": kern_launches,
+        },
+        "cpu_baseline": None,
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_ct_mul_small.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pm = json.load(f)
+            if pm.get("pairs") == n and pm.get("epl") == args.epl:
+                result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+                result["roofline"]["traffic_source"] = pm.get("source")
+        except Exception:
+            pass
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(eng, A, B, out, n, args)
+    if rank == 0 and not args.no_extras:
+        try:
+            result["extras"] = extras(eng, args, world == 1 and not args.no_cpu)
+        except Exception as ex:   # side measurements must not hide the headline
+            result["extras"] = {"error": repr(ex)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(eng, A, B, out, n, args):
+    """The pinned CPU port (oracle/pvac_oracle.cpp: same algorithm as the reference's
+    ct_mul minus sigma, std::unordered_map aggregation) on a bounded sample of the SAME
+    device-resident inputs; digests are cross-checked against the GPU output."""
+    import numpy as np
+    import torch
+    from helpers import Oracle, default_params
+    orc = Oracle.load()
+    k = min(args.cpu_pairs, n)
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    a_loff, a_eoff = u(A.l_off[:k]), u(A.e_off[:k])
+    b_loff, b_eoff = u(B.l_off[:k]), u(B.e_off[:k])
+    a_lend = int(a_loff[-1] + u(A.l_cnt[k - 1:k])[0])
+    a_eend = int(a_eoff[-1] + u(A.e_cnt[k - 1:k])[0])
+    b_lend = int(b_loff[-1] + u(B.l_cnt[k - 1:k])[0])
+    b_eend = int(b_eoff[-1] + u(B.e_cnt[k - 1:k])[0])
+    cs = lambda x: np.ascontiguousarray(x)
+    al = cs(np.append(a_loff, a_lend)); ae = cs(np.append(a_eoff, a_eend))
+    bl = cs(np.append(b_loff, b_lend)); be = cs(np.append(b_eoff, b_eend))
+    a_lay = cs(A.layers[:a_lend].cpu().numpy()); b_lay = cs(B.layers[:b_lend].cpu().numpy())
+    am, awl, awh = u(A.meta[:a_eend]), u(A.w_lo[:a_eend]), u(A.w_hi[:a_eend])
+    bm, bwl, bwh = u(B.meta[:b_eend]), u(B.w_lo[:b_eend]), u(B.w_hi[:b_eend])
+    counts = np.zeros(k, np.uint64)
+    digests = np.zeros(k, np.uint64)
+    prm = default_params(0x5EED0003)
+    import ctypes as C
+    P = lambda x: x.ctypes.data_as(C.c_void_p)
+    secs = orc.lib.orc_ct_mul_batch_timed(C.byref(prm), k, P(al), P(a_lay), P(ae), P(am), P(awl), P(awh),
+                                          P(bl), P(b_lay), P(be), P(bm), P(bwl), P(bwh), args.cpu_threads,
+                                          P(counts), P(digests))
+    gpu_dig = u(eng.digest(out)[:k])
+    gpu_cnt = u(out.e_cnt[:k])
+    return {
+        "value": k / secs,
+        "unit": "ct_mul/s",
+        "cores": args.cpu_threads,
+        "kind": "port",
+        "sample": f"{k} of the {n} device-resident pairs (first k), weights-only ct_mul incl. layer ztags, "
+                  f"{secs:.2f} s",
+        "impl": "oracle/pvac_oracle.cpp (pinned to the reference by tests/test_oracle.py)",
+        "cpu_model": _cpu_model(),
+        "gpu_output_matches": bool(np.array_equal(gpu_dig, digests) and np.array_equal(gpu_cnt, counts)),
+    }
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return None
+
+
+def extras(eng, args, with_cpu):
+    """cfg 2 (2^24 Fp127 add/mul) and full ct_mul WITH sigma on a smaller batch."""
+    import numpy as np
+    import torch
+    from pvac_hfhe_cppbyv_amd import FP_ADD, FP_MUL, MUL_WITH_SIGMA
+    dev = eng.device
+    res = {}
+    # ---- cfg 2: element-wise Fp127
+    nfp = 1 << 24
+    bufs = [torch.empty(nfp, dtype=torch.int64, device=dev) for _ in range(6)]
+    for i, t in enumerate(bufs[:4]):
+        eng.fill_random(t, 0x5EED0002 + i)
+    bufs[1] &= (1 << 63) - 1
+    bufs[3] &= (1 << 63) - 1
+    fp = {}
+    for name, op in (("add", FP_ADD), ("mul", FP_MUL)):
+        for _ in range(3):
+            eng.fp_binop(op, *bufs[:4], out=(bufs[4], bufs[5]))
+        eng.timing_reset()
+        eng.timing(True)
+        for _ in range(20):
+            eng.fp_binop(op, *bufs[:4], out=(bufs[4], bufs[5]))
+        eng.timing(False)
+        ms, cnt = eng.timing_get("fp_binop")
+        avg = ms / max(cnt, 1)
+        gbs = 48.0 * nfp / (avg / 1000.0) / 1e9
+        fp[name] = {"elements": nfp, "avg_kernel_ms": avg, "Gop_s": nfp / (avg / 1000.0) / 1e9,
+                    "achieved_GBs": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS}
+        if with_cpu:
+            from helpers import Oracle
+            orc = Oracle.load()
+            m = 1 << 22
+            h = [t[:m].cpu().numpy().view(np.uint64).copy() for t in bufs[:4]]
+            olo, ohi = np.zeros(m, np.uint64), np.zeros(m, np.uint64)
+            import ctypes as C
+            P = lambda x: x.ctypes.data_as(C.c_void_p)
+            secs = orc.lib.orc_fp_binop_timed(0 if name == "add" else 2, *(P(x) for x in h), P(olo), P(ohi), m, 1)
+            fp[name]["cpu_baseline"] = {"value": m / secs / 1e9, "unit": "Gop/s", "cores": 1, "kind": "port",
+                                        "sample": f"{m} elements"}
+            glo = bufs[4][:m].cpu().numpy().view(np.uint64)
+            fp[name]["gpu_output_matches"] = bool(np.array_equal(glo, olo))
+    res["fp127_cfg2"] = fp
+    del bufs
+    # ---- full ct_mul WITH sigma (reference-complete ct_mul)
+    ns = args.sigma_pairs
+    eng.gen_H()
+    A = eng.gen_fresh(ns, 0x51, args.epl)
+    B = eng.gen_fresh(ns, 0x52, args.epl)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    nonces = torch.empty(2 * plan.total_layer_slots, dtype=torch.int64, device=dev)
+    salts = torch.empty(plan.total_edge_slots, dtype=torch.int64, device=dev)
+    eng.fill_random(nonces, 0x53)
+    eng.fill_random(salts, 0x54)
+    eng.ct_mul(A, B, nonces=nonces, salts=salts, flags=MUL_WITH_SIGMA, C_=Cb, plan=plan)
+    torch.cuda.synchronize(dev)
+    eng.timing_reset()
+    eng.timing(True)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        Cb, plan = eng.ct_mul_plan(A, B)
+        Cs = eng.ct_mul(A, B, nonces=nonces, salts=salts, flags=MUL_WITH_SIGMA, C_=Cb, plan=plan)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / reps
+    eng.timing(False)
+    sms, scnt = eng.timing_get("sigma")
+    edges = float(Cs.e_cnt[:ns].sum().item())
+    sig_avg = sms / max(scnt, 1)
+    sig_bytes = edges * 1024.0 + edges * (8 + 8) + edges * 8   # sigma written + meta/salt read
+    full = {"pairs": ns, "ct_mul_per_s": ns / el, "ms_per_batch": el * 1000,
+            "sigma_kernel_ms": sig_avg, "sigma_GBs": sig_bytes / (sig_avg / 1000.0) / 1e9,
+            "edges": edges}
+    if with_cpu:
+        full["cpu_baseline"] = _ref_full_baseline()
+    res["ct_mul_with_sigma"] = full
+    return res
+
+
+def _ref_full_baseline():
+    """The UNMODIFIED reference ct_mul (with sigma) when oracle/_ref was built here and shipped;
+    otherwise None."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    try:
+        outp = subprocess.run([exe, "time_mul", "96", "1"], capture_output=True, text=True, timeout=120)
+        line = [l for l in outp.stdout.splitlines() if l.startswith("{")][-1]
+        r = json.loads(line)
+        return {"value": r["ct_mul_per_s"], "unit": "ct_mul/s", "cores": 1, "kind": "reference",
+                "sample": f"{r['pairs']} fresh x fresh ct_mul (reference pvac-hfhe 0.1.0, with sigma), "
+                          f"{r['seconds']:.2f} s"}
+    except Exception as ex:
+        return {"error": repr(ex)}
+
+
+if __name__ == "__main__":
+    main()

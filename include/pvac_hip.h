@@ -1,0 +1,191 @@
+/* pvac_hip.h — C ABI of the MI355X (gfx950) batched ciphertext-arithmetic engine.
+ *
+ * Drop-in boundary for the pvac-hfhe 0.1.0 hot path (reference: include/pvac/...). The
+ * reference exposes a header-only, by-value C++ API and no FFI; every entry point below
+ * names the reference function it replaces. The C++ shim headers under include/pvac/ keep
+ * the reference's type names and signatures and route through these entry points.
+ *
+ * Conventions
+ *  - All functions are noexcept, never throw, and return int status: 0 = ok, <0 = error
+ *    (PVAC_E*); pvac_hip_last_error(ctx) gives a message.
+ *  - Pointers inside batches/arrays are DEVICE pointers (hipMalloc / torch CUDA tensors)
+ *    unless a parameter says "host". Work is enqueued on the ctx stream; functions that
+ *    must return sizes to the host synchronise that stream (documented per function).
+ *  - One thread per ctx. Contexts are independent (one per device / per host thread).
+ *  - Fp values are p = 2^127-1 field elements as two u64 limbs (lo, hi) in SoA arrays.
+ *  - Randomness is an explicit input: the reference draws nonces/salts from getrandom(2)
+ *    inside ct_mul (core/random.hpp:40-110); here the caller passes those words, which
+ *    makes outputs reproducible and testable. The C++ shim fills them from getrandom.
+ */
+#ifndef PVAC_HIP_H
+#define PVAC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PVAC_HIP_ABI_VERSION 1
+
+/* status codes */
+#define PVAC_OK 0
+#define PVAC_EINVAL (-22)
+#define PVAC_ENOMEM (-12)
+#define PVAC_ENOSYS (-38)
+#define PVAC_EDEVICE (-5)
+#define PVAC_ERANGE (-34)
+
+/* fp binop codes (core/field.hpp:50-71,209-213; ops/arithmetic.hpp:33-37 for SCALE) */
+#define PVAC_FP_ADD 0
+#define PVAC_FP_SUB 1
+#define PVAC_FP_MUL 2
+#define PVAC_FP_NEG 3   /* b ignored */
+#define PVAC_FP_SCALE 4 /* b is ONE element, broadcast: c[i] = a[i] * b[0] */
+
+/* ct_mul flags */
+#define PVAC_MUL_WITH_SIGMA 0x1u      /* also generate per-edge sigma (crypto/matrix.hpp:267-303) */
+#define PVAC_MUL_ORDER_CANONICAL 0x2u /* emit (layer, idx, P<M) sorted instead of the reference hash order */
+
+typedef struct pvac_hip_ctx pvac_hip_ctx;
+
+/* Mirrors the subset of pvac::Params + PubKey that the hot path reads
+ * (core/types.hpp:36-70, 121-129). */
+typedef struct pvac_hip_params {
+    uint32_t B;          /* 337 */
+    uint32_t m_bits;     /* 8192: sigma bits */
+    uint32_t n_bits;     /* 16384: H columns */
+    uint32_t h_col_wt;   /* 192 */
+    uint32_t x_col_wt;   /* 128 */
+    uint32_t err_wt;     /* 128 */
+    uint64_t edge_budget;/* 1200000 (guard_budget, ops/encrypt.hpp:106-111) */
+    uint64_t canon_tag;  /* pk.canon_tag */
+} pvac_hip_params;
+
+/* pvac::Layer (core/types.hpp:96-101) as a 40-byte record. rule: 0 = BASE, 1 = PROD. */
+typedef struct pvac_layer {
+    uint32_t rule, pa, pb, pad;
+    uint64_t ztag, nonce_lo, nonce_hi;
+} pvac_layer;
+
+/* A batch of n ciphers (pvac::Cipher, core/types.hpp:116-119), SoA with per-cipher
+ * (offset, count) ranges so both dense CSR and capacity-padded outputs are expressible.
+ * Edge meta packs pvac::Edge{layer_id, idx, ch} exactly like the .ct edge header:
+ *   meta = layer_id | (u64)idx << 32 | (u64)ch << 48.
+ * sigma (nullable) holds sigma_words u64 per edge slot (edge slot e -> sigma[e*sigma_words]). */
+typedef struct pvac_ct_batch {
+    uint64_t n;
+    uint64_t* l_off;   /* [n] first layer slot of cipher i */
+    uint64_t* l_cnt;   /* [n] layers of cipher i */
+    pvac_layer* layers;
+    uint64_t* e_off;   /* [n] first edge slot of cipher i */
+    uint64_t* e_cnt;   /* [n] edges of cipher i */
+    uint64_t* meta;
+    uint64_t* w_lo;
+    uint64_t* w_hi;
+    uint64_t* sigma;
+    uint32_t sigma_words;
+    uint32_t pad;
+} pvac_ct_batch;
+
+/* Output sizing of a batched ct_mul / ct_add (filled by the *_plan calls). */
+typedef struct pvac_hip_plan {
+    uint64_t total_layer_slots;   /* sum of per-pair layer capacities */
+    uint64_t total_edge_slots;    /* sum of per-pair edge capacities */
+    uint64_t n_pairs;
+    uint64_t n_small;             /* pairs served by the LDS-resident fresh-shape kernel */
+    uint64_t n_large;             /* pairs served by the layer-dense path */
+    uint64_t n_invalid;           /* pairs rejected (bad layer/idx refs) */
+    uint32_t max_keys, max_prod, max_na, max_nb, max_buckets, max_layers;  /* launch sizing */
+    uint32_t kind;                /* 1 = mul, 2 = add, 3 = sub */
+    uint32_t reserved[5];
+} pvac_hip_plan;
+
+/* ---------------------------------------------------------------- context */
+int pvac_hip_abi_version(void);
+/* Create a context on `device`. Replaces the implicit PubKey plumbing of the reference. */
+int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** out);
+int pvac_hip_ctx_destroy(pvac_hip_ctx* ctx);
+/* Run on the caller's stream (e.g. torch.cuda.current_stream().cuda_stream). NULL = ctx-owned stream. */
+int pvac_hip_ctx_set_stream(pvac_hip_ctx* ctx, void* hip_stream);
+void* pvac_hip_ctx_stream(pvac_hip_ctx* ctx);
+int pvac_hip_ctx_synchronize(pvac_hip_ctx* ctx);
+const char* pvac_hip_last_error(pvac_hip_ctx* ctx);
+/* Upload the public parity matrix H (pk.H, crypto/matrix.hpp:191-251) from a HOST dense
+ * array of n_bits columns x ceil(m_bits/64) words; stored on device as per-column sparse
+ * row lists. Required only for PVAC_MUL_WITH_SIGMA / pvac_hip_sigma_batch. Synchronous. */
+int pvac_hip_ctx_set_H(pvac_hip_ctx* ctx, const uint64_t* H_dense_host, uint32_t n_cols, uint32_t words_per_col);
+/* Regenerate H on the device from params.canon_tag (gen_H, crypto/matrix.hpp:191-251) and
+ * return its H_digest (host, 32 bytes). */
+int pvac_hip_ctx_gen_H(pvac_hip_ctx* ctx, uint8_t digest_out[32]);
+
+/* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */
+int pvac_hip_timing_enable(pvac_hip_ctx* ctx, int on);
+/* kernel_name: "fp_binop", "ct_mul_small", "ct_mul_large", "ct_add", "sigma", ... ; returns
+ * accumulated milliseconds and launch count since the last reset (synchronises). */
+int pvac_hip_timing_get(pvac_hip_ctx* ctx, const char* kernel_name, double* ms, uint64_t* launches);
+int pvac_hip_timing_reset(pvac_hip_ctx* ctx);
+
+/* ---------------------------------------------------------------- element-wise Fp
+ * Replaces fp_add / fp_sub / fp_mul / fp_neg (core/field.hpp:50-71, 209-213) applied over
+ * arrays; results are bit-identical to the reference including its quirks for non-canonical
+ * inputs (fp_add truncates the high-word carry, field.hpp:53-55). In-place (c == a) allowed. */
+int pvac_hip_fp_binop(pvac_hip_ctx* ctx, int op, const uint64_t* a_lo, const uint64_t* a_hi, const uint64_t* b_lo,
+                      const uint64_t* b_hi, uint64_t* c_lo, uint64_t* c_hi, size_t n);
+
+/* ---------------------------------------------------------------- batched ciphertext ops
+ * ct_mul (ops/arithmetic.hpp:47-106) over n independent pairs C[i] = A[i] * B[i].
+ * Two-phase sizing:
+ *   1. pvac_hip_ct_mul_plan: writes C->l_off / C->e_off (device) with per-pair capacities
+ *      (layers |A.L|+|B.L|+|A.L||B.L|, edges 2*min(|A.E||B.E|, |A.L||B.L|B)) and fills *plan
+ *      (synchronises the stream once to read totals back).
+ *   2. caller allocates C->layers (total_layer_slots), C->meta/w_lo/w_hi (total_edge_slots),
+ *      optional C->sigma, then pvac_hip_ct_mul_exec writes C->l_cnt/e_cnt and the records.
+ * Randomness (replaces the getrandom draws of arithmetic.hpp:59-70,90-94):
+ *   nonces: 2 words per OUTPUT layer slot (device, parallel to C->layers): for the product
+ *           layer of (la, lb) at slot l_off+|A.L|+|B.L|+la*|B.L|+lb, words [2s]=lo, [2s+1]=hi.
+ *   salts : 1 word per OUTPUT edge slot (device, parallel to C->meta), in emit order; used only
+ *           with PVAC_MUL_WITH_SIGMA (nullable otherwise).
+ * Output edge order is the reference's std::unordered_map iteration order (bit-exact), unless
+ * PVAC_MUL_ORDER_CANONICAL. guard_budget/compact_layers semantics are applied per pair. */
+int pvac_hip_ct_mul_plan(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
+                         pvac_hip_plan* plan);
+int pvac_hip_ct_mul_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pvac_ct_batch* A, const pvac_ct_batch* B,
+                         const uint64_t* nonces, const uint64_t* salts, pvac_ct_batch* C, uint32_t flags);
+
+/* ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45; combine_ciphers ops/encrypt.hpp:260-279).
+ * negate_b != 0 gives ct_sub (B's weights scaled by p-1). Dense CSR output: the plan writes
+ * C->l_off/e_off as exclusive scans of |A.L|+|B.L| and |A.E|+|B.E|. Sigmas are carried when
+ * A, B and C all have sigma != NULL. */
+int pvac_hip_ct_add_plan(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
+                         pvac_hip_plan* plan);
+int pvac_hip_ct_add_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pvac_ct_batch* A, const pvac_ct_batch* B,
+                         int negate_b, pvac_ct_batch* C);
+
+/* ct_scale / ct_neg (ops/arithmetic.hpp:33-41): in-place w <- w * s over every edge of the
+ * batch (s host scalar). */
+int pvac_hip_ct_scale(pvac_hip_ctx* ctx, pvac_ct_batch* X, uint64_t s_lo, uint64_t s_hi);
+
+/* sigma_from_H for every edge of a batch (crypto/matrix.hpp:267-303): sigma of edge slot e
+ * from its layer's (ztag, nonce), idx, ch and salts[e]. Requires H (set_H / gen_H). */
+int pvac_hip_sigma_batch(pvac_hip_ctx* ctx, pvac_ct_batch* X, const uint64_t* salts);
+
+/* ---------------------------------------------------------------- synthetic inputs / checks
+ * Fresh-shaped cipher generator used by bench.py (SURVEY §8(d) cfg 3 generator): per cipher
+ * 2 BASE layers (random ztag/nonce), per layer `edges_per_layer` distinct (idx, ch), uniform
+ * nonzero canonical weights, edges grouped by layer and Fisher-Yates shuffled within a layer.
+ * Writes a dense CSR batch whose arrays the caller allocated for n*2 layers, n*2*epl edges. */
+int pvac_hip_gen_fresh_batch(pvac_hip_ctx* ctx, uint64_t seed, uint32_t edges_per_layer, pvac_ct_batch* X);
+/* splitmix64 stream fill (device): out[i] = splitmix64(seed + (i+1)*golden). */
+int pvac_hip_fill_random(pvac_hip_ctx* ctx, uint64_t seed, uint64_t* out, size_t n);
+/* Host-only: the bucket count std::unordered_map::reserve(n) picks on this libstdc++ (the
+ * emit-order pin of ct_mul, ops/arithmetic.hpp:75-76). No device access. */
+uint64_t pvac_hip_bucket_count(uint64_t n);
+/* per-cipher FNV-1a digest over (meta, w_lo, w_hi) of its edges in order (device out[n]). */
+int pvac_hip_batch_digest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PVAC_HIP_H */

@@ -1,0 +1,337 @@
+"""pvac_hfhe_cppbyv_amd — MI355X batched ciphertext-arithmetic engine for pvac-hfhe.
+
+Python view of the C ABI in include/pvac_hip.h (libpvac_hip.so). PyTorch is used only for
+device memory and streams; every operation runs in the hand-written HIP kernels of
+csrc/. There is NO CPU fallback: if the native library is missing this module raises.
+
+Host-side cipher representation mirrors pvac::Cipher (reference core/types.hpp:96-119):
+  layers : numpy structured array LAYER_DT (rule, pa, pb, pad, ztag, nonce_lo, nonce_hi)
+  meta   : u64 = layer_id | idx << 32 | ch << 48   (the .ct edge header)
+  w_lo/hi: u64 limbs of the Fp weight
+  sigma  : (nE, 128) u64 or None
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "lib", "libpvac_hip.so")
+
+LAYER_DT = np.dtype([("rule", "<u4"), ("pa", "<u4"), ("pb", "<u4"), ("pad", "<u4"),
+                     ("ztag", "<u8"), ("nonce_lo", "<u8"), ("nonce_hi", "<u8")])
+
+FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE = 0, 1, 2, 3, 4
+MUL_WITH_SIGMA, MUL_ORDER_CANONICAL = 0x1, 0x2
+
+P = (1 << 127) - 1
+
+
+class PvacError(RuntimeError):
+    pass
+
+
+class Params(C.Structure):
+    _fields_ = [("B", C.c_uint32), ("m_bits", C.c_uint32), ("n_bits", C.c_uint32), ("h_col_wt", C.c_uint32),
+                ("x_col_wt", C.c_uint32), ("err_wt", C.c_uint32), ("edge_budget", C.c_uint64),
+                ("canon_tag", C.c_uint64)]
+
+
+class CtBatch(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("l_off", C.c_void_p), ("l_cnt", C.c_void_p), ("layers", C.c_void_p),
+                ("e_off", C.c_void_p), ("e_cnt", C.c_void_p), ("meta", C.c_void_p), ("w_lo", C.c_void_p),
+                ("w_hi", C.c_void_p), ("sigma", C.c_void_p), ("sigma_words", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Plan(C.Structure):
+    _fields_ = [("total_layer_slots", C.c_uint64), ("total_edge_slots", C.c_uint64), ("n_pairs", C.c_uint64),
+                ("n_small", C.c_uint64), ("n_large", C.c_uint64), ("n_invalid", C.c_uint64),
+                ("max_keys", C.c_uint32), ("max_prod", C.c_uint32), ("max_na", C.c_uint32),
+                ("max_nb", C.c_uint32), ("max_buckets", C.c_uint32), ("max_layers", C.c_uint32),
+                ("kind", C.c_uint32), ("reserved", C.c_uint32 * 5)]
+
+
+def load_library(path: str = _LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise PvacError(f"native engine not built: {path} missing (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    sig = {
+        "pvac_hip_abi_version": ([], i32),
+        "pvac_hip_ctx_create": ([i32, C.POINTER(Params), C.POINTER(vp)], i32),
+        "pvac_hip_ctx_destroy": ([vp], i32),
+        "pvac_hip_ctx_set_stream": ([vp, vp], i32),
+        "pvac_hip_ctx_stream": ([vp], vp),
+        "pvac_hip_ctx_synchronize": ([vp], i32),
+        "pvac_hip_last_error": ([vp], C.c_char_p),
+        "pvac_hip_ctx_set_H": ([vp, vp, u32, u32], i32),
+        "pvac_hip_ctx_gen_H": ([vp, vp], i32),
+        "pvac_hip_timing_enable": ([vp, i32], i32),
+        "pvac_hip_timing_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(u64)], i32),
+        "pvac_hip_timing_reset": ([vp], i32),
+        "pvac_hip_fp_binop": ([vp, i32, vp, vp, vp, vp, vp, vp, C.c_size_t], i32),
+        "pvac_hip_ct_mul_plan": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch),
+                                  C.POINTER(Plan)], i32),
+        "pvac_hip_ct_mul_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
+                                  C.POINTER(CtBatch), u32], i32),
+        "pvac_hip_ct_add_plan": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch),
+                                  C.POINTER(Plan)], i32),
+        "pvac_hip_ct_add_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), i32,
+                                  C.POINTER(CtBatch)], i32),
+        "pvac_hip_ct_scale": ([vp, C.POINTER(CtBatch), u64, u64], i32),
+        "pvac_hip_sigma_batch": ([vp, C.POINTER(CtBatch), vp], i32),
+        "pvac_hip_gen_fresh_batch": ([vp, u64, u32, C.POINTER(CtBatch)], i32),
+        "pvac_hip_fill_random": ([vp, u64, vp, C.c_size_t], i32),
+        "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
+        "pvac_hip_bucket_count": ([u64], u64),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    return lib
+
+
+# ------------------------------------------------------------------------------ host ciphers
+@dataclass
+class HostCipher:
+    layers: np.ndarray
+    meta: np.ndarray
+    w_lo: np.ndarray
+    w_hi: np.ndarray
+    sigma: np.ndarray | None = None
+
+    @property
+    def nL(self):
+        return len(self.layers)
+
+    @property
+    def nE(self):
+        return len(self.meta)
+
+
+def _t(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x).view(np.int64))
+
+
+class DeviceBatch:
+    """A pvac_ct_batch whose arrays are torch CUDA tensors (int64 storage of u64 data)."""
+
+    def __init__(self, n, l_off, l_cnt, layers, e_off, e_cnt, meta, w_lo, w_hi, sigma=None):
+        self.n = n
+        self.l_off, self.l_cnt, self.layers = l_off, l_cnt, layers
+        self.e_off, self.e_cnt = e_off, e_cnt
+        self.meta, self.w_lo, self.w_hi, self.sigma = meta, w_lo, w_hi, sigma
+
+    def struct(self) -> CtBatch:
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        return CtBatch(n=self.n, l_off=p(self.l_off), l_cnt=p(self.l_cnt), layers=p(self.layers),
+                       e_off=p(self.e_off), e_cnt=p(self.e_cnt), meta=p(self.meta), w_lo=p(self.w_lo),
+                       w_hi=p(self.w_hi), sigma=p(self.sigma), sigma_words=128, pad=0)
+
+    @staticmethod
+    def empty(n, layer_slots, edge_slots, device, sigma=False):
+        import torch
+        z = lambda k: torch.zeros(max(int(k), 1), dtype=torch.int64, device=device)
+        return DeviceBatch(n, z(n), z(n), torch.zeros((max(int(layer_slots), 1), 5), dtype=torch.int64,
+                                                       device=device),
+                           z(n), z(n), z(edge_slots), z(edge_slots), z(edge_slots),
+                           torch.zeros((max(int(edge_slots), 1), 128), dtype=torch.int64, device=device)
+                           if sigma else None)
+
+    @staticmethod
+    def from_host(ciphers, device, sigma=False):
+        import torch
+        n = len(ciphers)
+        lc = np.array([c.nL for c in ciphers], np.uint64)
+        ec = np.array([c.nE for c in ciphers], np.uint64)
+        lo = np.concatenate([[0], np.cumsum(lc)[:-1]]).astype(np.uint64) if n else lc
+        eo = np.concatenate([[0], np.cumsum(ec)[:-1]]).astype(np.uint64) if n else ec
+        layers = np.concatenate([c.layers for c in ciphers]) if n else np.zeros(0, LAYER_DT)
+        cat = lambda f: np.concatenate([getattr(c, f) for c in ciphers]).astype(np.uint64) if n else \
+            np.zeros(0, np.uint64)
+        meta, wlo, whi = cat("meta"), cat("w_lo"), cat("w_hi")
+        sg = None
+        if sigma:
+            sg = np.concatenate([c.sigma if c.sigma is not None else np.zeros((c.nE, 128), np.uint64)
+                                 for c in ciphers]).astype(np.uint64)
+        dev = lambda a: _t(a if len(a) else np.zeros(1, np.uint64)).to(device)
+        lay = torch.from_numpy(np.ascontiguousarray(layers).view(np.int64).reshape(-1, 5) if len(layers)
+                               else np.zeros((1, 5), np.int64)).to(device)
+        return DeviceBatch(n, dev(lo), dev(lc), lay, dev(eo), dev(ec), dev(meta), dev(wlo), dev(whi),
+                           None if sg is None else torch.from_numpy(sg.view(np.int64) if len(sg) else
+                                                                    np.zeros((1, 128), np.int64)).to(device))
+
+    def to_host(self):
+        u = lambda t: t.cpu().numpy().view(np.uint64)
+        lo, lc, eo, ec = u(self.l_off), u(self.l_cnt), u(self.e_off), u(self.e_cnt)
+        layers = self.layers.cpu().numpy().reshape(-1).view(LAYER_DT)
+        meta, wlo, whi = u(self.meta), u(self.w_lo), u(self.w_hi)
+        sg = None if self.sigma is None else self.sigma.cpu().numpy().view(np.uint64)
+        out = []
+        for i in range(self.n):
+            a, b = int(lo[i]), int(lo[i] + lc[i])
+            c, d = int(eo[i]), int(eo[i] + ec[i])
+            out.append(HostCipher(layers[a:b].copy(), meta[c:d].copy(), wlo[c:d].copy(), whi[c:d].copy(),
+                                  None if sg is None else sg[c:d].copy()))
+        return out
+
+
+# ------------------------------------------------------------------------------ engine
+class Engine:
+    """One pvac_hip_ctx on one GPU, bound to torch's current stream on that device."""
+
+    def __init__(self, device=0, B=337, m_bits=8192, n_bits=16384, h_col_wt=192, x_col_wt=128, err_wt=128,
+                 edge_budget=1200000, canon_tag=0, lib: C.CDLL | None = None):
+        import torch
+        self.torch = torch
+        self.lib = lib or load_library()
+        self.device = torch.device("cuda", device)
+        self.params = Params(B=B, m_bits=m_bits, n_bits=n_bits, h_col_wt=h_col_wt, x_col_wt=x_col_wt,
+                             err_wt=err_wt, edge_budget=edge_budget, canon_tag=canon_tag)
+        ctx = C.c_void_p()
+        self._check(self.lib.pvac_hip_ctx_create(device, C.byref(self.params), C.byref(ctx)), None)
+        self.ctx = ctx
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device)
+        self._check(self.lib.pvac_hip_ctx_set_stream(self.ctx, C.c_void_p(stream.cuda_stream)))
+
+    def __del__(self):
+        try:
+            if getattr(self, "ctx", None):
+                self.lib.pvac_hip_ctx_destroy(self.ctx)
+                self.ctx = None
+        except Exception:
+            pass
+
+    def _check(self, rc, ctx="self"):
+        if rc != 0:
+            msg = ""
+            if ctx == "self" and getattr(self, "ctx", None):
+                msg = self.lib.pvac_hip_last_error(self.ctx).decode(errors="replace")
+            raise PvacError(f"pvac_hip error {rc}: {msg}")
+
+    def sync(self):
+        self._check(self.lib.pvac_hip_ctx_synchronize(self.ctx))
+
+    # ---- field
+    def fp_binop(self, op, a_lo, a_hi, b_lo=None, b_hi=None, out=None):
+        torch = self.torch
+        n = a_lo.numel()
+        c_lo, c_hi = out if out is not None else (torch.empty_like(a_lo), torch.empty_like(a_hi))
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        self._check(self.lib.pvac_hip_fp_binop(self.ctx, op, p(a_lo), p(a_hi), p(b_lo), p(b_hi), p(c_lo), p(c_hi),
+                                               n))
+        return c_lo, c_hi
+
+    # ---- ciphertext ops
+    def ct_mul_plan(self, A: DeviceBatch, B: DeviceBatch):
+        torch = self.torch
+        C_ = DeviceBatch(A.n, torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device),
+                         torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device), None,
+                         torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device),
+                         torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device), None, None, None)
+        plan = Plan()
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        self._check(self.lib.pvac_hip_ct_mul_plan(self.ctx, C.byref(sa), C.byref(sb), C.byref(sc), C.byref(plan)))
+        return C_, plan
+
+    def ct_mul(self, A: DeviceBatch, B: DeviceBatch, nonces=None, salts=None, flags=0, C_=None, plan=None,
+               nonce_seed=None):
+        """Batched ct_mul. nonces: device int64 tensor parallel to output layer slots (2 words each);
+        if None, filled from a splitmix stream (nonce_seed) on the device."""
+        torch = self.torch
+        if C_ is None or plan is None:
+            C_, plan = self.ct_mul_plan(A, B)
+        if C_.layers is None:
+            C_.layers = torch.empty((max(plan.total_layer_slots, 1), 5), dtype=torch.int64, device=self.device)
+            e = max(plan.total_edge_slots, 1)
+            C_.meta = torch.empty(e, dtype=torch.int64, device=self.device)
+            C_.w_lo = torch.empty(e, dtype=torch.int64, device=self.device)
+            C_.w_hi = torch.empty(e, dtype=torch.int64, device=self.device)
+            if flags & MUL_WITH_SIGMA:
+                C_.sigma = torch.empty((e, 128), dtype=torch.int64, device=self.device)
+        if nonces is None:
+            nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=self.device)
+            self.fill_random(nonces, 0x5EED0003 if nonce_seed is None else nonce_seed)
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        self._check(self.lib.pvac_hip_ct_mul_exec(self.ctx, C.byref(plan), C.byref(sa), C.byref(sb), p(nonces),
+                                                  p(salts), C.byref(sc), flags))
+        return C_
+
+    def ct_add(self, A: DeviceBatch, B: DeviceBatch, negate=False, sigma=False):
+        torch = self.torch
+        n = A.n
+        z = lambda: torch.zeros(max(n, 1), dtype=torch.int64, device=self.device)
+        C_ = DeviceBatch(n, z(), z(), None, z(), z(), None, None, None)
+        plan = Plan()
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        self._check(self.lib.pvac_hip_ct_add_plan(self.ctx, C.byref(sa), C.byref(sb), C.byref(sc), C.byref(plan)))
+        e = max(plan.total_edge_slots, 1)
+        C_.layers = torch.empty((max(plan.total_layer_slots, 1), 5), dtype=torch.int64, device=self.device)
+        C_.meta = torch.empty(e, dtype=torch.int64, device=self.device)
+        C_.w_lo = torch.empty(e, dtype=torch.int64, device=self.device)
+        C_.w_hi = torch.empty(e, dtype=torch.int64, device=self.device)
+        if sigma:
+            C_.sigma = torch.empty((e, 128), dtype=torch.int64, device=self.device)
+        sc = C_.struct()
+        self._check(self.lib.pvac_hip_ct_add_exec(self.ctx, C.byref(plan), C.byref(sa), C.byref(sb), int(negate),
+                                                  C.byref(sc)))
+        return C_
+
+    def ct_scale(self, X: DeviceBatch, s: int):
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_ct_scale(self.ctx, C.byref(sx), s & ((1 << 64) - 1), s >> 64))
+        return X
+
+    def sigma(self, X: DeviceBatch, salts):
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_sigma_batch(self.ctx, C.byref(sx), C.c_void_p(salts.data_ptr())))
+        return X
+
+    def set_H(self, H_dense: np.ndarray):
+        H = np.ascontiguousarray(H_dense, np.uint64)
+        self._check(self.lib.pvac_hip_ctx_set_H(self.ctx, H.ctypes.data_as(C.c_void_p), H.shape[0], H.shape[1]))
+
+    def gen_H(self) -> bytes:
+        d = C.create_string_buffer(32)
+        self._check(self.lib.pvac_hip_ctx_gen_H(self.ctx, d))
+        return d.raw
+
+    # ---- synthetic inputs / checks
+    def fill_random(self, t, seed):
+        self._check(self.lib.pvac_hip_fill_random(self.ctx, seed, C.c_void_p(t.data_ptr()), t.numel()))
+        return t
+
+    def gen_fresh(self, n, seed, edges_per_layer=20):
+        X = DeviceBatch.empty(n, 2 * n, 2 * edges_per_layer * n, self.device)
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_gen_fresh_batch(self.ctx, seed, edges_per_layer, C.byref(sx)))
+        return X
+
+    def digest(self, X: DeviceBatch):
+        out = self.torch.empty(max(X.n, 1), dtype=self.torch.int64, device=self.device)
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_batch_digest(self.ctx, C.byref(sx), C.c_void_p(out.data_ptr())))
+        return out[:X.n]
+
+    # ---- timing
+    def timing(self, on=True):
+        self._check(self.lib.pvac_hip_timing_enable(self.ctx, int(on)))
+
+    def timing_get(self, name):
+        ms, n = C.c_double(), C.c_uint64()
+        self._check(self.lib.pvac_hip_timing_get(self.ctx, name.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def timing_reset(self):
+        self._check(self.lib.pvac_hip_timing_reset(self.ctx))
+
+
+__all__ = ["Engine", "DeviceBatch", "HostCipher", "PvacError", "LAYER_DT", "load_library", "FP_ADD", "FP_SUB",
+           "FP_MUL", "FP_NEG", "FP_SCALE", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL"]

@@ -1,0 +1,122 @@
+// fp127.hpp — Fp over p = 2^127 - 1 on CDNA4 (gfx950), bit-exact with the reference
+// include/pvac/core/field.hpp (the product's own implementation).
+//
+// Layout: an element is two u64 limbs (lo, hi). gfx950 has no 64x64->128 multiply; the
+// 64x64 partial products lower to v_mad_u64_u32 chains (4 per partial product). All
+// branches of the reference (fp_from_words' conditional subtract) become selects so a
+// wavefront never diverges on data.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pvhip {
+
+struct fp { uint64_t lo, hi; };
+
+constexpr uint64_t kM63 = 0x7FFFFFFFFFFFFFFFULL;
+constexpr uint64_t kAll = ~0ULL;
+
+// 64x64 -> 128
+__device__ __forceinline__ void mul_64x64(uint64_t a, uint64_t b, uint64_t& lo, uint64_t& hi) {
+    lo = a * b;
+    hi = __umul64hi(a, b);
+}
+
+// add with carry-out
+__device__ __forceinline__ uint64_t add_co(uint64_t a, uint64_t b, uint64_t& carry) {
+    uint64_t s = a + b;
+    carry = s < a;
+    return s;
+}
+
+// field.hpp:26-48. Canonical for every 128-bit input.
+__device__ __forceinline__ fp fp_from_words(uint64_t lo, uint64_t hi) {
+    const uint64_t top = hi >> 63;
+    hi &= kM63;
+    uint64_t c;
+    lo = add_co(lo, top, c);
+    hi += c;
+    const bool reduce = (hi >> 63) | ((hi == kM63) & (lo == kAll));
+    const uint64_t borrow = lo != kAll;          // (old_lo < UINT64_MAX)
+    const uint64_t rlo = lo + 1;                 // lo - (2^64 - 1)
+    const uint64_t rhi = hi - kM63 - borrow;
+    return fp{reduce ? rlo : lo, reduce ? rhi : hi};
+}
+
+// field.hpp:50-56 — the high sum is truncated to 64 bits before the fold (reference quirk
+// for non-canonical inputs, reproduced exactly).
+__device__ __forceinline__ fp fp_add(const fp& a, const fp& b) {
+    uint64_t c;
+    const uint64_t lo = add_co(a.lo, b.lo, c);
+    return fp_from_words(lo, a.hi + b.hi + c);
+}
+
+// field.hpp:58-67: (2^64-1) - lo never borrows, so neg = fold(~lo, M63 - hi).
+__device__ __forceinline__ fp fp_neg(const fp& a) { return fp_from_words(kAll - a.lo, kM63 - a.hi); }
+
+__device__ __forceinline__ fp fp_sub(const fp& a, const fp& b) { return fp_add(a, fp_neg(b)); }
+
+// field.hpp:113-213: exact 256-bit product, two Mersenne folds, canonicalise.
+__device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
+    uint64_t p00l, p00h, p01l, p01h, p10l, p10h, p11l, p11h;
+    mul_64x64(a.lo, b.lo, p00l, p00h);
+    mul_64x64(a.lo, b.hi, p01l, p01h);
+    mul_64x64(a.hi, b.lo, p10l, p10h);
+    mul_64x64(a.hi, b.hi, p11l, p11h);
+    // z1 = p00h + p01l + p10l ; carries into z2
+    uint64_t c1, c2;
+    uint64_t z1 = add_co(p00h, p01l, c1);
+    z1 = add_co(z1, p10l, c2);
+    const uint64_t k1 = c1 + c2;
+    uint64_t c3, c4, c5;
+    uint64_t z2 = add_co(p01h, p10h, c3);
+    z2 = add_co(z2, p11l, c4);
+    z2 = add_co(z2, k1, c5);
+    const uint64_t z3 = p11h + c3 + c4 + c5;
+    const uint64_t z0 = p00l;
+    // fold 1: (z mod 2^127) + (z >> 127)
+    const uint64_t h0 = (z1 >> 63) | (z2 << 1);
+    const uint64_t h1 = (z2 >> 63) | (z3 << 1);
+    const uint64_t h2 = z3 >> 63;
+    uint64_t d0, d1, d2;
+    const uint64_t x0 = add_co(z0, h0, d0);
+    uint64_t x1 = add_co(z1 & kM63, h1, d1);
+    x1 = add_co(x1, d0, d2);
+    const uint64_t x2 = h2 + d1 + d2;
+    // fold 2
+    const uint64_t yh = (x1 >> 63) | (x2 << 1);
+    uint64_t e0;
+    const uint64_t y0 = add_co(x0, yh, e0);
+    const uint64_t y1 = (x1 & kM63) + e0;
+    return fp_from_words(y0, y1);
+}
+
+__device__ __forceinline__ bool fp_nonzero(const fp& a) { return (a.lo | a.hi) != 0; }
+
+// ---- exact multi-product accumulation for LDS atomics ----------------------------------
+// A canonical value v < 2^127 splits into three limbs of 43/42/42 bits. Up to 2^21 such
+// values summed limb-wise in u64 accumulators cannot overflow; fold_limbs recombines and
+// reduces mod p. The result equals the reference's sequential fp_add chain for canonical
+// addends (that chain computes the exact sum mod p).
+__device__ __forceinline__ void fp_split3(const fp& v, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
+    l0 = v.lo & ((1ULL << 43) - 1);
+    l1 = ((v.lo >> 43) | (v.hi << 21)) & ((1ULL << 42) - 1);
+    l2 = v.hi >> 21;
+}
+
+__device__ __forceinline__ fp fp_fold3(uint64_t l0, uint64_t l1, uint64_t l2) {
+    // V = l0 + l1*2^43 + l2*2^85  (< 2^150)
+    uint64_t c0, c1, c2;
+    const uint64_t w0 = add_co(l0, l1 << 43, c0);
+    uint64_t w1 = add_co(l1 >> 21, l2 << 21, c1);
+    w1 = add_co(w1, c0, c2);
+    const uint64_t w2 = (l2 >> 43) + c1 + c2;
+    // V mod p = (V mod 2^127) + (V >> 127)
+    const uint64_t top = (w1 >> 63) | (w2 << 1);
+    uint64_t d;
+    const uint64_t lo = add_co(w0, top, d);
+    const uint64_t hi = (w1 & kM63) + d;
+    return fp_from_words(lo, hi);
+}
+
+}  // namespace pvhip

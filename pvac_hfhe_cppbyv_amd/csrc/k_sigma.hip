@@ -1,0 +1,403 @@
+// k_sigma.hip — sigma_from_H (crypto/matrix.hpp:267-303) and gen_H (matrix.hpp:191-251)
+// on CDNA4.
+//
+// sigma = XOR of x_col_wt columns of the public sparse matrix H, then err_wt noise-bit
+// flips. Column / row choices come from prg_choose_k (matrix.hpp:15-92): a SHA-256
+// counter-mode stream over (label || le64 words... || le64 ctr), four little-endian u64
+// draws per digest, rejection-bounded to [0, N), and the FIRST k DISTINCT values in draw
+// order.
+//
+// Mapping: one wavefront per edge. Lanes 0..31 run the "pvac.dom.x_seed" stream and lanes
+// 32..63 the "pvac.dom.noise" stream, each lane one counter per pass (4 draws). The first
+// 64-byte block of both messages does not depend on the counter, so it is compressed once
+// per edge (midstate) and each pass costs one compression per lane. Exact "first k
+// distinct in draw order" is restored per pass: a draw is new if its value was selected by
+// no earlier pass (LDS bitmap) and by no earlier position of this pass (wave shuffles);
+// ranks come from a 32-lane prefix count. Selected columns are expanded through the sparse
+// H rows with LDS atomic XOR into a 1 KiB sigma image, written out as one 16-byte store per
+// lane.
+#include <vector>
+#include <cstring>
+
+#include "common.hpp"
+#include "sha256.hpp"
+#include "sigma.hpp"
+
+namespace pvhip {
+
+namespace {
+
+constexpr int kSigBlock = 256;   // 4 waves, one edge each at a time
+constexpr uint32_t kMaxPasses = 4096;   // >> the ~2-3 passes a random stream needs
+
+template <int N>
+struct cstr { char c[N]; };
+
+// Pack message byte `b` at absolute position `pos` of a message into block `blk` words.
+__device__ __forceinline__ void put(uint32_t (&w)[16], int blk, int pos, uint32_t b) {
+    const int p = pos - 64 * blk;
+    if (p >= 0 && p < 64) w[p >> 2] |= (b & 0xFFu) << (24 - 8 * (p & 3));
+}
+
+// Block `blk` of SHA-256 padding of the message  label(LL) || le64 words[NW] || le64 ctr.
+template <int LL, int NW>
+__device__ __forceinline__ void build_block(uint32_t (&w)[16], int blk, const char* label, const uint64_t* words,
+                                            uint64_t ctr) {
+    constexpr int T = LL + 8 * NW + 8;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = 0;
+#pragma unroll
+    for (int i = 0; i < LL; ++i) put(w, blk, i, (uint32_t)label[i]);
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) put(w, blk, LL + 8 * k + i, (uint32_t)(words[k] >> (8 * i)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) put(w, blk, LL + 8 * NW + i, (uint32_t)(ctr >> (8 * i)));
+    put(w, blk, T, 0x80u);
+    // big-endian bit length in the last 8 bytes of the final block
+    constexpr int nblk = (T + 9 + 63) / 64;
+    if (blk == nblk - 1) {
+        const uint64_t bits = (uint64_t)T * 8;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+    }
+}
+
+__device__ constexpr char kLabX[] = "pvac.dom.x_seed";   // 15
+__device__ constexpr char kLabN[] = "pvac.dom.noise";    // 14
+__device__ constexpr char kLabH[] = "pvac.dom.h_gen";    // 14
+
+// One pass of "first K distinct in draw order" over a group of GS lanes (GS = 32 or 64,
+// groups aligned). Each lane holds 4 consecutive draws (positions 4*li+q of this pass).
+// `bm` is the group's LDS bitmap of already-selected values. Returns, per q, the rank
+// (0-based, over the whole selection) of a newly selected value, or -1.
+template <int GS>
+__device__ __forceinline__ void select_pass(const uint32_t (&val)[4], uint32_t* bm, uint32_t K, uint32_t& have,
+                                            int (&rank)[4]) {
+    const int lane = threadIdx.x & 63;
+    const int li = lane & (GS - 1);
+    const int gbase = lane & ~(GS - 1);
+    bool isnew[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t v = val[q];
+        isnew[q] = v != 0xFFFFFFFFu && !((bm[v >> 5] >> (v & 31)) & 1u);
+    }
+    // earlier positions of this pass with the same value
+    for (int s = 0; s < GS; ++s) {
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+            const uint32_t o = __shfl(val[q2], gbase + s, 64);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool earlier = s < li || (s == li && q2 < q);
+                if (earlier && o == val[q]) isnew[q] = false;
+            }
+        }
+    }
+    const uint32_t mine = (uint32_t)isnew[0] + isnew[1] + isnew[2] + isnew[3];
+    // inclusive prefix over the group
+    uint32_t x = mine;
+#pragma unroll
+    for (int d = 1; d < GS; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, GS);
+        if (li >= d) x += y;
+    }
+    const uint32_t group_total = __shfl(x, gbase + GS - 1, 64);
+    uint32_t r = have + x - mine;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        rank[q] = -1;
+        if (isnew[q]) {
+            if (r < K) {
+                rank[q] = (int)r;
+                atomicOr(&bm[val[q] >> 5], 1u << (val[q] & 31));
+            }
+            ++r;
+        }
+    }
+    have = have + group_total < K ? have + group_total : K;
+}
+
+struct sig_args {
+    pvac_ct_batch X;
+    const uint64_t* salts;
+    const uint32_t* salt_pos;
+    const uint16_t* rows;
+    const uint32_t* counts;
+    uint32_t width;
+    uint64_t canon;
+    uint32_t n_bits, m_bits, x_col_wt, err_wt;
+    uint32_t sub_blocks;
+};
+
+// per-wave LDS: sigma [m_bits/32] | bmX [n_bits/32] | bmN [m_bits/32] | cols [x_col_wt] u16
+__global__ __launch_bounds__(kSigBlock) void k_sigma(sig_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t slds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t sw32 = a.m_bits / 32, bx32 = a.n_bits / 32, bn32 = a.m_bits / 32;
+    const uint32_t per_wave = sw32 + bx32 + bn32 + (a.x_col_wt + 1) / 2;
+    uint32_t* sig = slds + (size_t)wave * ((per_wave + 3) & ~3u);
+    uint32_t* bmX = sig + sw32;
+    uint32_t* bmN = bmX + bx32;
+    uint16_t* cols = (uint16_t*)(bmN + bn32);
+    for (uint32_t w = lane; w < sw32 + bx32 + bn32; w += 64) sig[w] = 0;
+
+    const bool isX = lane < 32;
+    const uint32_t Nmod = isX ? a.n_bits : a.m_bits;
+    const uint32_t K = isX ? a.x_col_wt : a.err_wt;
+    const uint64_t lim = ~0ULL - (~0ULL % (uint64_t)Nmod);
+    uint32_t* bm = isX ? bmX : bmN;
+    const uint64_t words_per_sigma = a.X.sigma_words;
+    const uint32_t sub = blockIdx.y * 4 + wave, nsub = a.sub_blocks * 4;
+
+    for (uint64_t ci = blockIdx.x; ci < a.X.n; ci += gridDim.x) {
+        const uint64_t eo = a.X.e_off[ci], ne = a.X.e_cnt[ci], lo = a.X.l_off[ci], nl = a.X.l_cnt[ci];
+        for (uint64_t k = sub; k < ne; k += nsub) {
+            const uint64_t e = eo + k;
+            const uint64_t m = a.X.meta[e];
+            const uint32_t lid = meta_layer(m);
+            pvac_layer L{};
+            if (lid < nl) L = a.X.layers[lo + lid];
+            const uint64_t salt = a.salt_pos ? a.salts[eo + a.salt_pos[e]] : a.salts[e];
+            const uint64_t words[7] = {a.canon, L.ztag, L.nonce_lo, L.nonce_hi, (uint64_t)meta_idx(m),
+                                       (uint64_t)meta_ch(m), salt};
+            // midstates: block 0 of both messages, selected per lane group
+            uint32_t bx[16], bn[16], blk[16];
+            build_block<15, 7>(bx, 0, kLabX, words, 0);
+            build_block<14, 7>(bn, 0, kLabN, words, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) blk[i] = isX ? bx[i] : bn[i];
+            sha_state mid;
+            sha_init(mid);
+            sha_compress(mid, blk);
+            uint32_t have = 0;
+            for (uint32_t pass = 0; pass < kMaxPasses; ++pass) {   // bounded: never hang the GPU
+                const uint64_t ctr = (uint64_t)pass * 32 + (lane & 31);
+                build_block<15, 7>(bx, 1, kLabX, words, ctr);
+                build_block<14, 7>(bn, 1, kLabN, words, ctr);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) blk[i] = isX ? bx[i] : bn[i];
+                sha_state s = mid;
+                sha_compress(s, blk);
+                uint32_t val[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t x = (uint64_t)bswap32(s.h[2 * q]) | ((uint64_t)bswap32(s.h[2 * q + 1]) << 32);
+                    val[q] = (have < K && x <= lim) ? (uint32_t)(x % Nmod) : 0xFFFFFFFFu;
+                }
+                int rank[4];
+                select_pass<32>(val, bm, K, have, rank);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (rank[q] >= 0) {
+                        if (isX) cols[rank[q]] = (uint16_t)val[q];
+                        else atomicXor(&sig[val[q] >> 5], 1u << (val[q] & 31));   // noise bit
+                    }
+                }
+                const bool doneX = __shfl(have, 0, 64) >= a.x_col_wt;
+                const bool doneN = __shfl(have, 32, 64) >= a.err_wt;
+                if (doneX && doneN) break;
+            }
+            // XOR the selected H columns: K*width row flips spread over the wave
+            const uint32_t W = a.width;
+            const uint32_t nflip = a.x_col_wt * W;
+            for (uint32_t f = lane; f < nflip; f += 64) {
+                const uint32_t ci2 = f / W, kk = f - ci2 * W;
+                const uint32_t col = cols[ci2];
+                if (kk < a.counts[col]) {
+                    const uint32_t r = a.rows[(size_t)col * W + kk];
+                    atomicXor(&sig[r >> 5], 1u << (r & 31));
+                }
+            }
+            // write 8192 bits: one 16-byte store per lane, then clear the wave's LDS
+            uint64_t* out = a.X.sigma + e * words_per_sigma;
+            for (uint32_t w4 = lane; w4 * 4 < sw32; w4 += 64) {
+                const uint4 v = *(const uint4*)(sig + w4 * 4);
+                ((ulonglong2*)out)[w4] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
+                                                         (uint64_t)v.z | ((uint64_t)v.w << 32));
+            }
+            for (uint32_t w = lane; w < sw32 + bx32 + bn32; w += 64) sig[w] = 0;
+        }
+    }
+}
+
+// gen_H: one wave per column; 64 lanes x 4 draws per pass ("pvac.dom.h_gen", 5 words)
+__global__ __launch_bounds__(256) void k_gen_H(uint16_t* rows, uint32_t* counts, uint32_t width, uint32_t m_bits,
+                                               uint32_t n_bits, uint32_t wt, uint64_t canon) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hlds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t bw = m_bits / 32;
+    uint32_t* bm = hlds + (size_t)wave * bw;
+    const uint64_t lim = ~0ULL - (~0ULL % (uint64_t)m_bits);
+    for (uint32_t c = blockIdx.x * 4 + wave; c < n_bits; c += gridDim.x * 4) {
+        for (uint32_t w = lane; w < bw; w += 64) bm[w] = 0;
+        const uint64_t words[5] = {m_bits, n_bits, wt, c, canon};
+        uint32_t have = 0;
+        for (uint32_t pass = 0; have < wt && pass < kMaxPasses; ++pass) {
+            const uint64_t ctr = (uint64_t)pass * 64 + lane;
+            uint32_t blk[16];
+            sha_state s;
+            sha_init(s);
+            build_block<14, 5>(blk, 0, kLabH, words, ctr);
+            sha_compress(s, blk);
+            build_block<14, 5>(blk, 1, kLabH, words, ctr);
+            sha_compress(s, blk);
+            uint32_t val[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t x = (uint64_t)bswap32(s.h[2 * q]) | ((uint64_t)bswap32(s.h[2 * q + 1]) << 32);
+                val[q] = x <= lim ? (uint32_t)(x % m_bits) : 0xFFFFFFFFu;
+            }
+            int rank[4];
+            select_pass<64>(val, bm, wt, have, rank);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (rank[q] >= 0) rows[(size_t)c * width + rank[q]] = (uint16_t)val[q];
+        }
+        if (lane == 0) counts[c] = wt;
+    }
+}
+
+// host SHA-256 over a contiguous buffer
+void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]) {
+    sha_state s;
+    sha_init(s);
+    size_t off = 0;
+    uint32_t w[16];
+    auto load = [&](const uint8_t* b) {
+        for (int i = 0; i < 16; ++i)
+            w[i] = (uint32_t)b[4 * i] << 24 | (uint32_t)b[4 * i + 1] << 16 | (uint32_t)b[4 * i + 2] << 8 | b[4 * i + 3];
+    };
+    for (; off + 64 <= n; off += 64) { load(p + off); sha_compress(s, w); }
+    uint8_t tail[128] = {0};
+    const size_t r = n - off;
+    std::memcpy(tail, p + off, r);
+    tail[r] = 0x80;
+    const size_t tl = (r + 9 <= 64) ? 64 : 128;
+    const uint64_t bits = (uint64_t)n * 8;
+    for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    for (size_t b = 0; b < tl; b += 64) { load(tail + b); sha_compress(s, w); }
+    for (int i = 0; i < 8; ++i) {
+        out[4 * i] = (uint8_t)(s.h[i] >> 24); out[4 * i + 1] = (uint8_t)(s.h[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(s.h[i] >> 8); out[4 * i + 3] = (uint8_t)s.h[i];
+    }
+}
+
+}  // namespace
+
+void sigma_tables_free(sigma_tables& T) {
+    hipFree(T.rows);
+    hipFree(T.counts);
+    T = sigma_tables{};
+}
+
+static hipError_t alloc_tables(sigma_tables& T, uint32_t n_cols, uint32_t width) {
+    sigma_tables_free(T);
+    hipError_t e = hipMalloc(&T.rows, (size_t)n_cols * width * 2);
+    if (e == hipSuccess) e = hipMalloc(&T.counts, (size_t)n_cols * 4);
+    if (e != hipSuccess) { sigma_tables_free(T); return e; }
+    T.width = width;
+    T.n_cols = n_cols;
+    return hipSuccess;
+}
+
+hipError_t sigma_tables_from_dense(sigma_tables& T, const pvac_hip_params& prm, const uint64_t* H, hipStream_t st) {
+    const uint32_t wpc = (prm.m_bits + 63) / 64;
+    uint32_t width = 0;
+    std::vector<uint32_t> cnt(prm.n_bits);
+    for (uint32_t c = 0; c < prm.n_bits; ++c) {
+        uint32_t k = 0;
+        for (uint32_t w = 0; w < wpc; ++w) k += (uint32_t)__builtin_popcountll(H[(size_t)c * wpc + w]);
+        cnt[c] = k;
+        width = k > width ? k : width;
+    }
+    if (width == 0) width = 1;
+    std::vector<uint16_t> rows((size_t)prm.n_bits * width, 0);
+    for (uint32_t c = 0; c < prm.n_bits; ++c) {
+        uint32_t k = 0;
+        for (uint32_t w = 0; w < wpc; ++w) {
+            uint64_t x = H[(size_t)c * wpc + w];
+            while (x) {
+                const int b = __builtin_ctzll(x);
+                rows[(size_t)c * width + k++] = (uint16_t)(w * 64 + b);
+                x &= x - 1;
+            }
+        }
+    }
+    hipError_t e = alloc_tables(T, prm.n_bits, width);
+    if (e == hipSuccess) e = hipMemcpyAsync(T.rows, rows.data(), rows.size() * 2, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(T.counts, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    T.ready = e == hipSuccess;
+    return e;
+}
+
+hipError_t sigma_tables_generate(sigma_tables& T, const pvac_hip_params& prm, uint8_t digest[32], hipStream_t st) {
+    if (prm.h_col_wt == 0 || prm.h_col_wt > prm.m_bits || prm.m_bits % 32 || prm.m_bits > 65536)
+        return hipErrorInvalidValue;
+    hipError_t e = alloc_tables(T, prm.n_bits, prm.h_col_wt);
+    if (e != hipSuccess) return e;
+    const size_t lds = (size_t)4 * (prm.m_bits / 32) * 4;
+    hipLaunchKernelGGL(k_gen_H, dim3(2048), dim3(256), lds, st, T.rows, T.counts, T.width, prm.m_bits, prm.n_bits,
+                       prm.h_col_wt, prm.canon_tag);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (digest) {
+        std::vector<uint16_t> rows((size_t)prm.n_bits * T.width);
+        e = hipMemcpyAsync(rows.data(), T.rows, rows.size() * 2, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        // H_digest = SHA-256("H|v2" || le64 m || le64 n || le64 wt || column bytes) (matrix.hpp:218-250)
+        const size_t colbytes = (prm.m_bits + 7) / 8;
+        std::vector<uint8_t> msg(4 + 24 + (size_t)prm.n_bits * colbytes, 0);
+        std::memcpy(msg.data(), "H|v2", 4);
+        const uint64_t hdr[3] = {prm.m_bits, prm.n_bits, prm.h_col_wt};
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < 8; ++i) msg[4 + 8 * k + i] = (uint8_t)(hdr[k] >> (8 * i));
+        uint8_t* cols = msg.data() + 28;
+        for (uint32_t c = 0; c < prm.n_bits; ++c)
+            for (uint32_t k = 0; k < T.width; ++k) {
+                const uint32_t r = rows[(size_t)c * T.width + k];
+                cols[(size_t)c * colbytes + (r >> 3)] |= (uint8_t)(1u << (r & 7));
+            }
+        sha256_host(msg.data(), msg.size(), digest);
+    } else {
+        e = hipStreamSynchronize(st);
+    }
+    T.ready = e == hipSuccess;
+    return e;
+}
+
+hipError_t launch_sigma(const sigma_tables& T, const pvac_hip_params& prm, const pvac_ct_batch& X,
+                        const uint64_t* salts, const uint32_t* salt_pos, int num_cus, hipStream_t st) {
+    if (!X.n) return hipSuccess;
+    if (!T.ready || prm.m_bits % 128 || prm.n_bits % 32 || prm.x_col_wt > prm.n_bits || prm.err_wt > prm.m_bits ||
+        X.sigma_words != prm.m_bits / 64 || prm.n_bits > 65536)
+        return hipErrorInvalidValue;
+    sig_args a;
+    a.X = X;
+    a.salts = salts;
+    a.salt_pos = salt_pos;
+    a.rows = T.rows;
+    a.counts = T.counts;
+    a.width = T.width;
+    a.canon = prm.canon_tag;
+    a.n_bits = prm.n_bits;
+    a.m_bits = prm.m_bits;
+    a.x_col_wt = prm.x_col_wt;
+    a.err_wt = prm.err_wt;
+    const uint32_t per_wave = prm.m_bits / 32 + prm.n_bits / 32 + prm.m_bits / 32 + (prm.x_col_wt + 1) / 2;
+    const size_t lds = (size_t)4 * ((per_wave + 3) & ~3u) * 4;
+    uint64_t gx = X.n < 4096 ? X.n : 4096;
+    uint64_t sub = 1;
+    const uint64_t want = (uint64_t)num_cus * 8;
+    if (gx < want) sub = (want + gx - 1) / gx;
+    if (sub > 64) sub = 64;
+    a.sub_blocks = (uint32_t)sub;
+    hipLaunchKernelGGL(k_sigma, dim3((unsigned)gx, (unsigned)sub), dim3(kSigBlock), lds, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace pvhip

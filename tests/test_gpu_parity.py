@@ -1,0 +1,299 @@
+"""GPU parity: the MI355X engine (libpvac_hip.so, via its C ABI) against the reference's golden
+vectors and the pinned CPU oracle. Bit-exact everywhere (integer/byte work)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import (REF, Cipher, read_ct, read_layers_u64, read_u64, R_for, P)
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev_batch(engine, ciphers, sigma=False):
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, HostCipher
+    hc = [HostCipher(c.layers, c.meta, c.w_lo, c.w_hi, c.sigma) for c in ciphers]
+    return DeviceBatch.from_host(hc, engine.device, sigma=sigma)
+
+
+def _i64(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64))
+
+
+# ------------------------------------------------------------------ element-wise Fp (cfg 2)
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "neg"])
+def test_fp_binop_golden(engine, op):
+    from pvac_hfhe_cppbyv_amd import FP_ADD, FP_SUB, FP_MUL, FP_NEG
+    code = {"add": FP_ADD, "sub": FP_SUB, "mul": FP_MUL, "neg": FP_NEG}[op]
+    d = engine.device
+    a_lo, a_hi, b_lo, b_hi = (_i64(read_u64(f"fp_{n}.u64")).to(d) for n in ("a_lo", "a_hi", "b_lo", "b_hi"))
+    lo, hi = engine.fp_binop(code, a_lo, a_hi, b_lo, b_hi)
+    assert np.array_equal(lo.cpu().numpy().view(np.uint64), read_u64(f"fp_{op}_lo.u64"))
+    assert np.array_equal(hi.cpu().numpy().view(np.uint64), read_u64(f"fp_{op}_hi.u64"))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4095, 65537])
+def test_fp_binop_ragged_and_unaligned(engine, oracle, n):
+    """Odd sizes take the scalar tail; 8-byte-misaligned views take the scalar kernel."""
+    from pvac_hfhe_cppbyv_amd import FP_MUL, FP_ADD, FP_SUB
+    rng = np.random.default_rng(n + 1)
+    buf = [rng.integers(0, 2**63, n + 1, dtype=np.uint64) * np.uint64(2) + np.uint64(1) for _ in range(4)]
+    t = [_i64(b).to(engine.device) for b in buf]
+    for off in (0, 1):
+        views = [x[off:off + n] for x in t]
+        for code, name in ((FP_MUL, "mul"), (FP_ADD, "add"), (FP_SUB, "sub")):
+            lo, hi = engine.fp_binop(code, *views)
+            ref_lo, ref_hi = oracle.fp(name, *(b[off:off + n] for b in buf))
+            assert np.array_equal(lo.cpu().numpy().view(np.uint64), ref_lo)
+            assert np.array_equal(hi.cpu().numpy().view(np.uint64), ref_hi)
+
+
+def test_fp_scale_broadcast(engine, oracle):
+    from pvac_hfhe_cppbyv_amd import FP_SCALE
+    rng = np.random.default_rng(3)
+    n = 10001
+    a_lo = rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2)
+    a_hi = rng.integers(0, 2**63, n, dtype=np.uint64)
+    s_lo, s_hi = np.array([12345678901234567], np.uint64), np.array([987654321], np.uint64)
+    d = engine.device
+    lo, hi = engine.fp_binop(FP_SCALE, _i64(a_lo).to(d), _i64(a_hi).to(d), _i64(s_lo).to(d), _i64(s_hi).to(d))
+    r_lo, r_hi = oracle.fp("mul", a_lo, a_hi, np.repeat(s_lo, n), np.repeat(s_hi, n))
+    assert np.array_equal(lo.cpu().numpy().view(np.uint64), r_lo)
+    assert np.array_equal(hi.cpu().numpy().view(np.uint64), r_hi)
+
+
+def test_fp_full_size_properties(engine, oracle):
+    """cfg 2 size (2^24): sample vs oracle + size-independent identities on every element:
+    (a + b) - b == a and a * 1 == a for canonical inputs."""
+    import torch
+    from pvac_hfhe_cppbyv_amd import FP_ADD, FP_SUB, FP_MUL
+    n = 1 << 24
+    d = engine.device
+    a_lo = torch.empty(n, dtype=torch.int64, device=d)
+    a_hi = torch.empty(n, dtype=torch.int64, device=d)
+    b_lo = torch.empty(n, dtype=torch.int64, device=d)
+    b_hi = torch.empty(n, dtype=torch.int64, device=d)
+    for t, s in ((a_lo, 1), (a_hi, 2), (b_lo, 3), (b_hi, 4)):
+        engine.fill_random(t, 0x5EED0002 + s)
+    a_hi &= (1 << 62) - 1   # canonical (< 2^126)
+    b_hi &= (1 << 62) - 1
+    s_lo, s_hi = engine.fp_binop(FP_ADD, a_lo, a_hi, b_lo, b_hi)
+    r_lo, r_hi = engine.fp_binop(FP_SUB, s_lo, s_hi, b_lo, b_hi)
+    assert torch.equal(r_lo, a_lo) and torch.equal(r_hi, a_hi)
+    one_lo = torch.ones(n, dtype=torch.int64, device=d)
+    one_hi = torch.zeros(n, dtype=torch.int64, device=d)
+    m_lo, m_hi = engine.fp_binop(FP_MUL, a_lo, a_hi, one_lo, one_hi)
+    assert torch.equal(m_lo, a_lo) and torch.equal(m_hi, a_hi)
+    p_lo, p_hi = engine.fp_binop(FP_MUL, a_lo, a_hi, b_lo, b_hi)
+    idx = torch.randint(0, n, (20000,), device=d)
+    u = lambda t: t[idx].cpu().numpy().view(np.uint64)
+    o_lo, o_hi = oracle.fp("mul", u(a_lo), u(a_hi), u(b_lo), u(b_hi))
+    assert np.array_equal(u(p_lo), o_lo) and np.array_equal(u(p_hi), o_hi)
+
+
+# ------------------------------------------------------------------ ct_add / ct_sub
+def _ct_layers_view(c):
+    L = c.layers.copy()
+    prod = L["rule"] == 1
+    for f in ("ztag", "nonce_lo", "nonce_hi"):
+        L[f][prod] = 0
+    L["pa"][~prod] = 0
+    L["pb"][~prod] = 0
+    return L
+
+
+def _assert_same(got, ref, sigma=False, layers_view=True):
+    L = _ct_layers_view(got) if layers_view else got.layers
+    for f in ("rule", "pa", "pb", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(L[f], ref.layers[f]), f
+    assert np.array_equal(got.meta, ref.meta)
+    assert np.array_equal(got.w_lo, ref.w_lo) and np.array_equal(got.w_hi, ref.w_hi)
+    if sigma:
+        assert np.array_equal(got.sigma, ref.sigma)
+
+
+def test_ct_add_sub_golden_batched(engine):
+    xs = [read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0] for p in range(8)]
+    ys = [read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0] for p in range(8)]
+    A, B = _dev_batch(engine, xs, sigma=True), _dev_batch(engine, ys, sigma=True)
+    for op, neg in (("add", False), ("sub", True)):
+        out = engine.ct_add(A, B, negate=neg, sigma=True).to_host()
+        for p in range(8):
+            _assert_same(out[p], read_ct(os.path.join(REF, f"pair{p}_{op}.ct"))[0], sigma=True)
+
+
+def test_bounty2_sum_gpu(engine):
+    from helpers import GOLD, write_ct
+    a = read_ct(os.path.join(GOLD, "bounty", "a.ct"))[0]
+    b = read_ct(os.path.join(GOLD, "bounty", "b.ct"))[0]
+    s = engine.ct_add(_dev_batch(engine, [a], True), _dev_batch(engine, [b], True), sigma=True).to_host()[0]
+    c = Cipher(_ct_layers_view(s), s.meta, s.w_lo, s.w_hi, s.sigma)
+    with open(os.path.join(GOLD, "bounty", "sum.ct"), "rb") as f:
+        assert write_ct([c]) == f.read()
+
+
+# ------------------------------------------------------------------ ct_mul (fresh pairs)
+def _nonce_buffer(engine, Cb, x_list, y_list, streams):
+    """Place each pair's reference nonce stream at its product-layer slots."""
+    loff = Cb.l_off.cpu().numpy().view(np.uint64)
+    total = int(loff[-1]) + x_list[-1].nL + y_list[-1].nL + x_list[-1].nL * y_list[-1].nL
+    buf = np.zeros(2 * total, np.uint64)
+    for p, (x, y, st) in enumerate(zip(x_list, y_list, streams)):
+        base = int(loff[p]) + x.nL + y.nL
+        nn = 2 * x.nL * y.nL
+        buf[2 * base:2 * base + nn] = st[:nn]
+    return _i64(buf).to(engine.device)
+
+
+def test_ct_mul_weights_golden_batched(engine, manifest):
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=manifest["canon_tag"])
+    xs = [read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0] for p in range(8)]
+    ys = [read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0] for p in range(8)]
+    streams = [read_u64(f"pair{p}_mul_stream.u64") for p in range(8)]
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    assert plan.n_small == 8 and plan.n_large == 0
+    nonces = _nonce_buffer(eng, Cb, xs, ys, streams)
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+    powg = read_u64("powg_B.u64")
+    for p in range(8):
+        ref = read_ct(os.path.join(REF, f"pair{p}_mul_w.ct"))[0]
+        _assert_same(out[p], ref)
+        full = read_layers_u64(f"pair{p}_mul_layers.u64")
+        for f in ("rule", "ztag", "nonce_lo", "nonce_hi"):
+            assert np.array_equal(out[p].layers[f], full[f]), f
+        assert len(streams[p]) == 2 * xs[p].nL * ys[p].nL + out[p].nE
+
+
+def test_ct_mul_sigma_golden(engine, manifest, oracle):
+    """WITH_SIGMA: device gen_H must reproduce H_digest, and every product sigma must match the
+    reference (pair 0 byte-for-byte, pairs 0..7 through commit_ct)."""
+    from pvac_hfhe_cppbyv_amd import Engine, MUL_WITH_SIGMA
+    eng = Engine(device=0, canon_tag=manifest["canon_tag"])
+    assert eng.gen_H().hex() == manifest["H_digest"]
+    xs = [read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0] for p in range(8)]
+    ys = [read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0] for p in range(8)]
+    streams = [read_u64(f"pair{p}_mul_stream.u64") for p in range(8)]
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    nonces = _nonce_buffer(eng, Cb, xs, ys, streams)
+    eoff = Cb.e_off.cpu().numpy().view(np.uint64)
+    salts = np.zeros(plan.total_edge_slots, np.uint64)
+    for p in range(8):
+        nn = 2 * xs[p].nL * ys[p].nL
+        s = streams[p][nn:]
+        salts[int(eoff[p]):int(eoff[p]) + len(s)] = s
+    out = eng.ct_mul(A, B, nonces=nonces, salts=_i64(salts).to(eng.device), flags=MUL_WITH_SIGMA, C_=Cb,
+                     plan=plan).to_host()
+    ref0 = read_ct(os.path.join(REF, "pair0_mul.ct"))[0]
+    _assert_same(out[0], ref0, sigma=True)
+    Hd = bytes.fromhex(manifest["H_digest"])
+    for p in range(8):
+        c = out[p]
+        got = Cipher(c.layers, c.meta, c.w_lo, c.w_hi, c.sigma)
+        assert oracle.commit(got, manifest["canon_tag"], Hd).hex() == manifest["pairs"][p]["commit_mul"], p
+
+
+def test_ct_mul_synthetic_vs_oracle(engine, oracle):
+    """4096 synthetic fresh-shaped pairs (cfg-3 generator, also 19/21-edge layers): every pair
+    bit-exact vs the oracle, including emit order."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0x1234)
+    for epl in (20, 19, 21, 1):
+        n = 4096 if epl == 20 else 256
+        A = eng.gen_fresh(n, 0xA000 + epl, epl)
+        B = eng.gen_fresh(n, 0xB000 + epl, epl)
+        Cb, plan = eng.ct_mul_plan(A, B)
+        nonces = eng.torch.empty(2 * plan.total_layer_slots, dtype=eng.torch.int64, device=eng.device)
+        eng.fill_random(nonces, 77)
+        out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+        ha, hb = A.to_host(), B.to_host()
+        nz = nonces.cpu().numpy().view(np.uint64)
+        loff = Cb.l_off.cpu().numpy().view(np.uint64)
+        for p in range(n):
+            x, y = ha[p], hb[p]
+            base = int(loff[p]) + x.nL + y.nL
+            nn = 2 * x.nL * y.nL
+            ref = oracle.ct_mul(Cipher(x.layers, x.meta, x.w_lo, x.w_hi), Cipher(y.layers, y.meta, y.w_lo, y.w_hi),
+                                nz[2 * base:2 * base + nn], canon_tag=0x1234)
+            _assert_same(out[p], ref, layers_view=False)
+
+
+def test_ct_mul_edge_cases(engine, oracle):
+    """Empty ciphers, single-edge ciphers, 1-layer ciphers, and a tiny edge_budget that triggers
+    guard_budget -> compact_edges ordering (encrypt.hpp:106-111)."""
+    from pvac_hfhe_cppbyv_amd import Engine, HostCipher, LAYER_DT
+    rng = np.random.default_rng(11)
+
+    def mk(nl, ne):
+        L = np.zeros(nl, LAYER_DT)
+        L["ztag"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+        L["nonce_lo"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+        if nl == 0:
+            ne = 0
+        lay = rng.integers(0, max(nl, 1), ne).astype(np.uint64)
+        idx = rng.integers(0, 337, ne).astype(np.uint64)
+        ch = rng.integers(0, 2, ne).astype(np.uint64)
+        meta = lay | (idx << np.uint64(32)) | (ch << np.uint64(48))
+        lo = rng.integers(0, 2**63, ne, dtype=np.uint64)
+        hi = rng.integers(0, 2**62, ne, dtype=np.uint64)
+        return Cipher(L, meta, lo, hi)
+
+    shapes = [((2, 40), (2, 0)), ((2, 0), (2, 40)), ((0, 0), (2, 40)), ((1, 1), (1, 1)), ((1, 30), (2, 40)),
+              ((2, 64), (2, 64)), ((1, 100), (1, 40)), ((3, 60), (1, 60)), ((2, 40), (2, 40))]
+    for budget in (1200000, 500):
+        eng = Engine(device=0, canon_tag=99, edge_budget=budget)
+        xs = [mk(*a) for a, _ in shapes]
+        ys = [mk(*b) for _, b in shapes]
+        A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+        Cb, plan = eng.ct_mul_plan(A, B)
+        nonces = eng.torch.empty(2 * max(plan.total_layer_slots, 1), dtype=eng.torch.int64, device=eng.device)
+        eng.fill_random(nonces, 5)
+        out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+        nz = nonces.cpu().numpy().view(np.uint64)
+        loff = Cb.l_off.cpu().numpy().view(np.uint64)
+        for p, (x, y) in enumerate(zip(xs, ys)):
+            base = int(loff[p]) + x.nL + y.nL
+            ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=99, edge_budget=budget)
+            _assert_same(out[p], ref, layers_view=False)
+
+
+def test_ct_mul_roundtrip_decrypt(engine, manifest, oracle):
+    """dec(ct_mul(enc x, enc y)) == x*y with fixture R values (reference test_main.cpp:178-188)."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=manifest["canon_tag"])
+    powg = read_u64("powg_B.u64")
+    for p in range(8):
+        x = read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0]
+        y = read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0]
+        out = eng.ct_mul(_dev_batch(eng, [x]), _dev_batch(eng, [y]), nonce_seed=p).to_host()[0]
+        c = Cipher(out.layers, out.meta, out.w_lo, out.w_hi)
+        R = R_for(c, [(x, read_u64(f"pair{p}_x_R.u64")), (y, read_u64(f"pair{p}_y_R.u64"))])
+        m = manifest["pairs"][p]
+        assert oracle.dec(c, powg, R)[0] == (m["x"] * m["y"]) % P
+
+
+def test_sigma_batch_matches_oracle(engine, oracle):
+    """pvac_hip_sigma_batch on arbitrary (layer, idx, ch, salt) edges vs the oracle's sigma_from_H,
+    with H uploaded from a host dense matrix (set_H)."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=4242)
+    H, _ = oracle.gen_H(4242)
+    eng.set_H(H)
+    X = eng.gen_fresh(6, 31, 20)
+    X.sigma = eng.torch.zeros((X.meta.numel(), 128), dtype=eng.torch.int64, device=eng.device)
+    salts = eng.torch.empty(X.meta.numel(), dtype=eng.torch.int64, device=eng.device)
+    eng.fill_random(salts, 9)
+    eng.sigma(X, salts)
+    hs = X.to_host()
+    sl = salts.cpu().numpy().view(np.uint64)
+    k = 0
+    for c in hs:
+        for e in range(c.nE):
+            L = c.layers[int(c.meta[e]) & 0xFFFFFFFF]
+            ref = oracle.sigma(4242, H, int(L["ztag"]), int(L["nonce_lo"]), int(L["nonce_hi"]),
+                               (int(c.meta[e]) >> 32) & 0xFFFF, (int(c.meta[e]) >> 48) & 0xFF, int(sl[k]))
+            assert np.array_equal(c.sigma[e], ref), (k,)
+            k += 1
