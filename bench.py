@@ -193,8 +193,11 @@ def cpu_baseline(eng, A, B, out, n, args):
     b_lend = int(b_loff[-1] + u(B.l_cnt[k - 1:k])[0])
     b_eend = int(b_eoff[-1] + u(B.e_cnt[k - 1:k])[0])
     cs = lambda x: np.ascontiguousarray(x)
-    al = cs(np.append(a_loff, a_lend)); ae = cs(np.append(a_eoff, a_eend))
-    bl = cs(np.append(b_loff, b_lend)); be = cs(np.append(b_eoff, b_eend))
+    # keep u64 (np.append with a Python int would promote uint64 + int64 -> float64)
+    app = lambda a, v: cs(np.concatenate([a, np.array([v], np.uint64)]))
+    al, ae = app(a_loff, a_lend), app(a_eoff, a_eend)
+    bl, be = app(b_loff, b_lend), app(b_eoff, b_eend)
+    assert al.dtype == np.uint64 and be.dtype == np.uint64
     a_lay = cs(A.layers[:a_lend].cpu().numpy()); b_lay = cs(B.layers[:b_lend].cpu().numpy())
     am, awl, awh = u(A.meta[:a_eend]), u(A.w_lo[:a_eend]), u(A.w_hi[:a_eend])
     bm, bwl, bwh = u(B.meta[:b_eend]), u(B.w_lo[:b_eend]), u(B.w_hi[:b_eend])

@@ -107,7 +107,8 @@ int pvac_hip_abi_version(void);
 /* Create a context on `device`. Replaces the implicit PubKey plumbing of the reference. */
 int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** out);
 int pvac_hip_ctx_destroy(pvac_hip_ctx* ctx);
-/* Run on the caller's stream (e.g. torch.cuda.current_stream().cuda_stream). NULL = ctx-owned stream. */
+/* Run on the caller's stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = the legacy
+ * null stream. A fresh context starts on a private non-blocking stream of its own. */
 int pvac_hip_ctx_set_stream(pvac_hip_ctx* ctx, void* hip_stream);
 void* pvac_hip_ctx_stream(pvac_hip_ctx* ctx);
 int pvac_hip_ctx_synchronize(pvac_hip_ctx* ctx);

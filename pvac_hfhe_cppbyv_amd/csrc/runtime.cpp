@@ -195,13 +195,10 @@ int pvac_hip_ctx_set_stream(pvac_hip_ctx* c, void* s) {
         c->stream = nullptr;
         c->own_stream = false;
     }
-    if (s) {
-        c->stream = (hipStream_t)s;
-        c->own_stream = false;
-    } else {
-        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return PVAC_EDEVICE;
-        c->own_stream = true;
-    }
+    // NULL selects the legacy null stream (torch's default stream is 0): every launch and copy
+    // is then ordered with the caller's own work on that stream.
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
     return PVAC_OK;
 }
 
@@ -381,13 +378,21 @@ int pvac_hip_ct_scale(pvac_hip_ctx* c, pvac_ct_batch* X, uint64_t s_lo, uint64_t
 int pvac_hip_ctx_set_H(pvac_hip_ctx* c, const uint64_t* H, uint32_t n_cols, uint32_t wpc) {
     if (!c || !H) return PVAC_EINVAL;
     if (n_cols != c->prm.n_bits || wpc != (c->prm.m_bits + 63) / 64) return fail(c, PVAC_EINVAL, "set_H: shape");
-    return hip_fail(c, sigma_tables_from_dense(c->H, c->prm, H, c->stream), "set_H");
+    try {
+        return hip_fail(c, sigma_tables_from_dense(c->H, c->prm, H, c->stream), "set_H");
+    } catch (const std::exception& ex) {
+        return fail(c, PVAC_ENOMEM, std::string("set_H: ") + ex.what());
+    }
 }
 
 int pvac_hip_ctx_gen_H(pvac_hip_ctx* c, uint8_t digest[32]) {
     if (!c) return PVAC_EINVAL;
-    scoped_timer t(c, "gen_H");
-    return hip_fail(c, sigma_tables_generate(c->H, c->prm, digest, c->stream), "gen_H");
+    try {
+        scoped_timer t(c, "gen_H");
+        return hip_fail(c, sigma_tables_generate(c->H, c->prm, digest, c->stream), "gen_H");
+    } catch (const std::exception& ex) {
+        return fail(c, PVAC_ENOMEM, std::string("gen_H: ") + ex.what());
+    }
 }
 
 int pvac_hip_sigma_batch(pvac_hip_ctx* c, pvac_ct_batch* X, const uint64_t* salts) {
