@@ -93,7 +93,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.timing(False)
-    kern_ms, kern_launches = eng.timing_get("ct_mul_small")
+    kern_ms, kern_launches = eng.timing_get("ct_mul_fresh")
+    lay_ms, lay_launches = eng.timing_get("mul_layers_fresh")
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -101,16 +102,18 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * n / (elapsed / args.steps)
 
-    # ---- algorithmic bytes of the dominant kernel: per pair
+    # ---- algorithmic bytes of the dominant kernel k_ct_mul_fresh: per pair
     #   24 B x (|A.E| + |B.E| + |C.E|)  edge records (meta 8 + w 16) read / written
-    # + 40 B x (|A.L| + |B.L| + |C.L|)  layer records
-    # + 16 B x |A.L||B.L|               nonces
-    # + 96 B                            offsets / counts of A, B, C
+    # + 16 B x (|A.L| + |B.L|)          rule/pa/pb of the input layers (compact_layers parents)
+    # + 104 B                           offsets / counts / class / status of A, B, C
+    # (the product-layer records, 40 B x |C.L| + 16 B nonces x |A.L||B.L|, are written by
+    #  k_mul_layers_fresh and reported as step bytes below)
     e_cnt = out.e_cnt[:n].to(torch.float64)
     l_cnt = out.l_cnt[:n].to(torch.float64)
     la, lb = A.l_cnt[:n].to(torch.float64), B.l_cnt[:n].to(torch.float64)
     na, nb = A.e_cnt[:n].to(torch.float64), B.e_cnt[:n].to(torch.float64)
-    alg_bytes = float((24 * (na + nb + e_cnt) + 40 * (la + lb + l_cnt) + 16 * la * lb + 96).sum().item())
+    alg_bytes = float((24 * (na + nb + e_cnt) + 16 * (la + lb) + 104).sum().item())
+    step_bytes = alg_bytes + float((40 * (la + lb + l_cnt) + 16 * la * lb).sum().item())
     avg_kernel_ms = kern_ms / max(kern_launches, 1)
     achieved = alg_bytes / (avg_kernel_ms / 1000.0) / 1e9 if avg_kernel_ms > 0 else None
     out_edges = float(e_cnt.sum().item())
@@ -139,7 +142,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_ct_mul_small",
+            "kernel": "k_ct_mul_fresh",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -148,10 +151,13 @@ def main():
             "alg_bytes_per_launch": alg_bytes,
             "avg_kernel_ms": avg_kernel_ms,
             "kernel_launches": kern_launches,
+            "step_alg_bytes": step_bytes,
+            "layers_kernel_avg_ms": lay_ms / max(lay_launches, 1),
+            "step_GBs": step_bytes / (ms_per_step / 1000.0) / 1e9,
         },
         "cpu_baseline": None,
     }
-    pmc = os.path.join(ROOT, "profiles", "pmc_ct_mul_small.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_ct_mul_fresh.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:

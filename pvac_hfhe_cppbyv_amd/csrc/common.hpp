@@ -57,6 +57,20 @@ hipError_t launch_gen_fresh(uint64_t seed, uint32_t epl, uint32_t B, const pvac_
 hipError_t launch_batch_digest(const pvac_ct_batch& X, uint64_t* out, hipStream_t st);
 hipError_t launch_ct_scale(const pvac_ct_batch& X, uint64_t slo, uint64_t shi, hipStream_t st);
 
+// x mod d for a runtime divisor d < 2^32 without a 64-bit division: m = floor((2^64-1)/d),
+// q = mulhi(x, m) undershoots floor(x/d) by at most 2, so two conditional subtracts finish.
+struct fastmod64 {
+    uint64_t d, m;
+};
+__host__ __device__ inline fastmod64 make_fastmod64(uint64_t d) { return fastmod64{d, d ? ~0ull / d : 0}; }
+__device__ __forceinline__ uint64_t fmod64(uint64_t x, const fastmod64& f) {
+    const uint64_t q = __umul64hi(x, f.m);
+    uint64_t r = x - q * f.d;
+    r = r >= f.d ? r - f.d : r;
+    r = r >= f.d ? r - f.d : r;
+    return r;
+}
+
 // plan statistics written by the plan kernels (device, zeroed before launch)
 struct plan_stats {
     unsigned long long total_layers, total_edges;
@@ -64,9 +78,14 @@ struct plan_stats {
     unsigned int max_keys, max_prod, max_na, max_nb, max_buckets, max_layers;
 };
 
+// pair classes written by the mul plan
+enum : uint8_t { PAIR_EMPTY = 0, PAIR_SMALL = 1, PAIR_LARGE = 2 };
+
 hipError_t launch_plan_mul(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, uint8_t* pair_class,
-                           plan_stats* stats, const uint32_t* nb_table, uint32_t nb_table_len, uint32_t Bm,
-                           uint32_t ks_small_max, uint32_t prod_small_max, hipStream_t st);
+                           uint64_t* large_ids, plan_stats* stats, const uint32_t* nb_table, uint32_t nb_table_len,
+                           uint32_t Bm, hipStream_t st);
+hipError_t launch_gather_large(const pvac_ct_batch& A, const pvac_ct_batch& B, const uint64_t* ids, uint64_t n,
+                               uint64_t* out, hipStream_t st);
 hipError_t launch_plan_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, plan_stats* stats,
                            hipStream_t st);
 // in-place exclusive scan of n u64 values; scratch >= scan_scratch_words(n) u64
@@ -74,13 +93,20 @@ size_t scan_scratch_words(size_t n);
 hipError_t launch_exclusive_scan_u64(uint64_t* data, size_t n, uint64_t* scratch, unsigned long long* total_out,
                                      hipStream_t st);
 
-struct mul_small_args {
+// ---- ct_mul, fresh-shape path (k_mul_fresh.hip): LDS-resident, one workgroup per pair
+constexpr uint32_t kFreshKeysMax = 1536;    // |A.L||B.L|B key slots
+constexpr uint32_t kFreshProdMax = 4096;    // |A.E||B.E| products
+constexpr uint32_t kFreshEdgesMax = 256;    // |A.E|, |B.E|
+constexpr uint32_t kFreshLayersMax = 64;    // |C.L| before compaction
+
+struct mul_fresh_args {
     pvac_ct_batch A, B, C;
     const uint64_t* nonces;
-    uint32_t* salt_pos;          // nullable: hash-order index of each output edge (salt stream position)
     const uint8_t* pair_class;
-    uint32_t* pair_status;
-    const uint32_t* nb_table;
+    uint32_t* pair_status;       // 0 = reference order, 1 = canonical order, 2 = rejected (bad refs)
+    const uint32_t* nb_table;    // libstdc++ bucket count after reserve(n), n <= kFreshProdMax
+    const uint64_t* nb_magic;    // fastmod64 multipliers for nb_table
+    uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
     uint64_t canon_tag;
     uint64_t edge_budget;
     uint32_t Bm;
@@ -88,7 +114,67 @@ struct mul_small_args {
     // launch sizing (maxima over the small pairs of the batch)
     uint32_t ks_max, prod_max, na_max, nb_max, buckets_max, layers_max;
 };
-hipError_t launch_ct_mul_small(const mul_small_args& a, int num_cus, hipStream_t st, int* blocks_used);
+hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st);
+hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, int num_cus, hipStream_t st);
+
+// ---- ct_mul, general path (k_mul_large.hip): multi-kernel, global scratch, one workgroup
+// per (A-layer, B-layer) product task. The host prepares one descriptor per large pair with
+// ABSOLUTE u32-word offsets into one scratch arena (64-bit arrays on even offsets).
+constexpr uint32_t kLargeLayersMax = 16384;   // |A.L| + |B.L| + |A.L||B.L| handled in LDS
+constexpr uint32_t kLargeDenseMin = 48;       // dense-owner product mode from this many edges
+
+struct large_desc {
+    uint64_t pair;               // index of the pair in the batch
+    uint64_t n;                  // |A.E| * |B.E|  (< 2^32)
+    uint64_t S;                  // |A.L| |B.L| B dense key slots
+    uint64_t Lc;                 // |A.L| + |B.L| + |A.L||B.L|  (layers before compaction)
+    uint64_t nblk;               // ceil(n / 64) first-insert-time blocks
+    uint64_t capE;               // 2 min(n, S) output edge capacity
+    fastmod64 nbm;               // libstdc++ bucket count after reserve(n)
+    uint32_t LA, LB, nA, nB;
+    uint32_t hbits, pad;         // bucket hash table capacity = 2^hbits >= 2 S
+    // zero-initialised block [o_zero, o_zero + zero_words): cnt | hkey | hhead | bmask | bcnt | used
+    uint64_t o_zero, zero_words;
+    uint64_t o_cnt;              // [8] neA, neB, invalid, total edges, canonical
+    uint64_t o_hkey;             // [2^hbits] u64 bucket ids + 1
+    uint64_t o_hhead;            // [2^hbits] chain heads (slot + 1)
+    uint64_t o_bmask;            // [nblk] u64 bucket-leader masks over first-insert times
+    uint64_t o_bcnt;             // [nblk + 1] emitted edges per block -> exclusive suffix offsets
+    uint64_t o_used;             // [Lc] product-layer used flags -> compact_layers remap
+    // 0xFF-initialised: [S] first-insert time per key slot (INF = key absent)
+    uint64_t o_tkey;
+    // written before read
+    uint64_t o_lstA, o_lstB;     // [2 LA] start,count per layer ++ [nA] edge ids; same for B
+    uint64_t o_neA, o_neB;       // [LA] / [LB] non-empty layer lists
+    uint64_t o_info;             // [S] ebits (2 bits) | hash slot << 2
+    uint64_t o_sums;             // [S] x 4 u64: P lo, P hi, M lo, M hi
+    uint64_t o_nxt;              // [S] bucket chain links
+    uint64_t o_tb;               // [S] bucket first-insert time
+    uint64_t o_within;           // [S] edges of the same bucket emitted before this key
+    uint64_t o_etot;             // [S] edges of the bucket (leaders only)
+    uint64_t o_cpos;             // [S] canonical positions (guard_budget order)
+    uint64_t o_order;            // [capE] emit order: slot << 1 | ch
+    uint64_t o_hpos;             // [capE] hash-order index of each canonical-order edge
+    uint64_t words;              // end of this pair's scratch (absolute)
+};
+
+struct mul_large_args {
+    pvac_ct_batch A, B, C;
+    const uint64_t* nonces;
+    uint32_t* pair_status;
+    const large_desc* desc;      // [nl]
+    uint32_t* scratch;           // arena (u32 words)
+    uint32_t nl;
+    uint32_t Bm;
+    uint64_t canon_tag;
+    uint64_t edge_budget;
+    uint32_t flags;
+    uint32_t pad;
+    uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
+    // launch sizing (maxima over the nl descriptors)
+    uint64_t max_S, max_zero, max_tasks, max_capE, max_lay;
+};
+hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
 
 hipError_t launch_ct_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, int negate_b,
                          uint32_t max_layers, hipStream_t st);

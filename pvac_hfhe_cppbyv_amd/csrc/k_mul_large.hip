@@ -1,0 +1,600 @@
+// k_mul_large.hip — batched ct_mul for general pairs (reference ops/arithmetic.hpp:47-106):
+// chains c_k = c_{k-1} * x (test_main.cpp:289-295), squares (test_depth.cpp:46), any pair the
+// LDS-resident fresh kernel cannot hold.
+//
+// The reference aggregates |A.E||B.E| products in one std::unordered_map. Here the product
+// space is cut along its natural independence: every product of an A edge in layer la and a
+// B edge in layer lb lands in product layer lp = la*LB + lb, a cyclic convolution of length B
+// over Fp with +/- channels. One workgroup owns one (la, lb) TASK:
+//   dense-owner mode : the side with more edges becomes a dense [B][2] table in LDS; one lane
+//                      per output index r loops over the other side's edges, multiplies, and
+//                      accumulates P/M sums and the key's first-insert time in REGISTERS (no
+//                      atomics). For saturated chain layers (674 edges) every probe is useful.
+//   scatter mode     : sparse x sparse tasks (and inputs with duplicate (layer, idx, ch) edges)
+//                      accumulate 43/42/42-bit limbs with LDS atomics, as the fresh kernel.
+// Results go to a dense per-pair key-slot array [|A.L||B.L|][B] in global scratch.
+//
+// The reference's emit order (hash-table list order: bucket first-insert time DESC, key
+// first-insert time DESC; see k_mul_fresh.hip) is rebuilt without sorting:
+//   link  : key -> libstdc++ bucket (hash * 0x9E37... mod bucket_count), bucket chains through
+//           a global open-addressing table keyed by bucket id;
+//   rank  : each key walks its (short) chain: bucket first-insert time t_b, edges of its bucket
+//           emitted before it; bucket leaders mark bit t_b in a 64-bit mask per 64 first-insert
+//           times and add their bucket's edge count to that block;
+//   scan  : suffix scan over blocks (n/64 entries, not n);
+//   order : position = block offset + edges of leaders later in the same block (mask bits above,
+//           each resolved to its key slot from the leader's (i, j) = (t / |B.E|, t % |B.E|)) +
+//           rank inside the bucket; slot ids are scattered into an order array (4 B each);
+//   write : one coalesced pass writes (meta, w) in order.
+// compact_layers (encrypt.hpp:73-104) runs per pair between aggregation and write, so edges
+// are written once with their final layer ids; guard_budget (encrypt.hpp:106-111) switches a
+// pair to (layer, idx, P<M) order when its edge count exceeds edge_budget.
+#include "common.hpp"
+#include "sha256.hpp"
+
+namespace pvhip {
+
+namespace {
+
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr int kLB = 256;            // threads per workgroup (task / grid-stride kernels)
+constexpr int kLBig = 1024;         // threads per workgroup (per-pair kernels)
+
+__device__ __forceinline__ uint64_t* w64(uint32_t* s, uint64_t o) { return (uint64_t*)(s + o); }
+
+__device__ __forceinline__ uint32_t mod_small(uint32_t x, uint32_t B) { return x >= B ? x - B : x; }
+
+// workgroup exclusive scan for any multiple-of-64 block size
+template <int BS>
+__device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* part, uint32_t& total) {
+    return block_exclusive_scan<BS>(v, part, total);
+}
+
+// ---------------------------------------------------------------- init
+__global__ __launch_bounds__(kLB) void k_large_init(mul_large_args g) {
+    const large_desc& d = g.desc[blockIdx.y];
+    const uint64_t stride = (uint64_t)gridDim.x * kLB;
+    const uint64_t lim = d.zero_words > d.S ? d.zero_words : d.S;
+    for (uint64_t w = (uint64_t)blockIdx.x * kLB + threadIdx.x; w < lim; w += stride) {
+        if (w < d.zero_words) g.scratch[d.o_zero + w] = 0;
+        if (w < d.S) g.scratch[d.o_tkey + w] = kInf;
+    }
+}
+
+// ---------------------------------------------------------------- per-layer edge lists
+// One workgroup per pair: validates edges (layer < |L|, idx < B, ch <= 1), buckets edge ids
+// by layer (any order inside a layer: first-insert times are minima, not positions) and
+// lists the non-empty layers of both sides.
+__global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // [LA + LB] counts, then cursors
+    __shared__ uint32_t flag;
+    const large_desc& d = g.desc[blockIdx.x];
+    const uint64_t pr = d.pair;
+    const uint32_t LA = d.LA, LB = d.LB, nA = d.nA, nB = d.nB, Bm = g.Bm;
+    const uint64_t aeo = g.A.e_off[pr], beo = g.B.e_off[pr];
+    uint32_t* S = g.scratch;
+    uint32_t* cnt = S + d.o_cnt;
+    const int tid = threadIdx.x;
+    for (uint32_t l = tid; l < LA + LB; l += kLBig) hist[l] = 0;
+    if (tid == 0) flag = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < nA; i += kLBig) {
+        const uint64_t m = g.A.meta[aeo + i];
+        const uint32_t la = meta_layer(m);
+        if (la >= LA || meta_idx(m) >= Bm || meta_ch(m) > 1) flag = 1;
+        else atomicAdd(&hist[la], 1u);
+    }
+    for (uint32_t j = tid; j < nB; j += kLBig) {
+        const uint64_t m = g.B.meta[beo + j];
+        const uint32_t lb = meta_layer(m);
+        if (lb >= LB || meta_idx(m) >= Bm || meta_ch(m) > 1) flag = 1;
+        else atomicAdd(&hist[LA + lb], 1u);
+    }
+    __syncthreads();
+    if (flag) {   // invalid references: reject the pair (reference behaviour is UB)
+        if (tid == 0) {
+            cnt[2] = 1;
+            g.pair_status[pr] = 2;
+            g.C.l_cnt[pr] = 0;
+            g.C.e_cnt[pr] = 0;
+        }
+        return;
+    }
+    // layer ranges by atomic allocation; non-empty layer lists by atomic append
+    for (uint32_t l = tid; l < LA + LB; l += kLBig) {
+        const uint32_t c = hist[l];
+        const bool a = l < LA;
+        uint32_t* lst = a ? S + d.o_lstA : S + d.o_lstB;
+        const uint32_t ll = a ? l : l - LA;
+        const uint32_t L = a ? LA : LB;
+        uint32_t start = 0;
+        if (c) {
+            start = atomicAdd(&cnt[a ? 5 : 6], c);
+            const uint32_t k = atomicAdd(&cnt[a ? 0 : 1], 1u);
+            (S + (a ? d.o_neA : d.o_neB))[k] = ll;
+        }
+        lst[ll] = start;
+        lst[L + ll] = c;
+        hist[l] = start;   // cursor
+    }
+    __syncthreads();
+    uint32_t* idsA = S + d.o_lstA + 2 * LA;
+    uint32_t* idsB = S + d.o_lstB + 2 * LB;
+    for (uint32_t i = tid; i < nA; i += kLBig) {
+        const uint32_t la = meta_layer(g.A.meta[aeo + i]);
+        idsA[atomicAdd(&hist[la], 1u)] = i;
+    }
+    for (uint32_t j = tid; j < nB; j += kLBig) {
+        const uint32_t lb = meta_layer(g.B.meta[beo + j]);
+        idsB[atomicAdd(&hist[LA + lb], 1u)] = j;
+    }
+}
+
+// ---------------------------------------------------------------- products (one task per WG)
+constexpr int kLP = 384;                 // products workgroup: one lane per output index r (B = 337)
+constexpr int kLPRows = 3;               // B <= kLP * kLPRows
+constexpr uint32_t kBmax = kLP * kLPRows;
+constexpr uint32_t kChunk = 384;         // sparse-side edges staged per round
+
+__host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
+// dense mode: dw[2B] (16 B) | di[2B] | sw[kChunk] (16 B) | sinf[kChunk] | sid[kChunk] | dup
+// scatter   : acc[2B x 3] (u64) | tk[B]
+__host__ __device__ inline uint32_t prod_lds_bytes(uint32_t Bm) {
+    const uint32_t dense = al16(40u * Bm) + 24u * kChunk + 16u;
+    const uint32_t scat = 48u * Bm + 4u * Bm;
+    return dense > scat ? dense : scat;
+}
+
+__global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
+    const large_desc& d = g.desc[blockIdx.y];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
+    const uint32_t tl = blockIdx.x;
+    const uint32_t la_i = tl / LB, lb_i = tl - la_i * LB;
+    if (la_i >= cnt[0] || lb_i >= cnt[1]) return;
+    const uint32_t la = S[d.o_neA + la_i], lb = S[d.o_neB + lb_i];
+    const uint32_t a0 = S[d.o_lstA + la], na = S[d.o_lstA + LA + la];
+    const uint32_t b0 = S[d.o_lstB + lb], nb = S[d.o_lstB + LB + lb];
+    const uint32_t* idsA = S + d.o_lstA + 2 * LA + a0;
+    const uint32_t* idsB = S + d.o_lstB + 2 * LB + b0;
+    const uint64_t pr = d.pair;
+    const uint64_t aeo = g.A.e_off[pr], beo = g.B.e_off[pr];
+    const uint32_t lp = la * LB + lb;
+    const uint64_t slot0 = (uint64_t)lp * Bm;
+    const int tid = threadIdx.x;
+    const bool denseA = na >= nb;
+    const uint32_t nd = denseA ? na : nb, ns = denseA ? nb : na;
+    uint32_t* tkey = S + d.o_tkey;
+    uint32_t* info = S + d.o_info;
+    ulonglong2* sums = (ulonglong2*)(S + d.o_sums);
+    bool any = false;
+
+    bool dense = nd >= kLargeDenseMin;
+    if (dense) {
+        ulonglong2* dw = (ulonglong2*)plds;
+        uint32_t* di = (uint32_t*)(plds + 32u * Bm);
+        ulonglong2* swv = (ulonglong2*)(plds + al16(40u * Bm));
+        uint32_t* sinf = (uint32_t*)(swv + kChunk);
+        uint32_t* sidv = sinf + kChunk;
+        uint32_t* dup = sidv + kChunk;
+        for (uint32_t k = tid; k < 2 * Bm; k += kLP) di[k] = kInf;
+        if (tid == 0) *dup = 0;
+        __syncthreads();
+        const uint32_t* dids = denseA ? idsA : idsB;
+        const pvac_ct_batch& D = denseA ? g.A : g.B;
+        const uint64_t deo = denseA ? aeo : beo;
+        for (uint32_t k = tid; k < nd; k += kLP) {
+            const uint32_t e = dids[k];
+            const uint64_t m = D.meta[deo + e];
+            const uint32_t sl = meta_idx(m) * 2 + meta_ch(m);
+            if (atomicCAS(&di[sl], kInf, e) != kInf) *dup = 1;
+            else dw[sl] = make_ulonglong2(D.w_lo[deo + e], D.w_hi[deo + e]);
+        }
+        __syncthreads();
+        dense = *dup == 0;   // duplicate (layer, idx, ch) edges: use the scatter mode instead
+        if (dense) {
+            const uint32_t* sids = denseA ? idsB : idsA;
+            const pvac_ct_batch& Sp = denseA ? g.B : g.A;
+            const uint64_t seo = denseA ? beo : aeo;
+            // lanes own output indices r (at most kLPRows per lane)
+            fp P[kLPRows], M[kLPRows];
+            uint32_t tmin[kLPRows];
+#pragma unroll
+            for (int u = 0; u < kLPRows; ++u) { P[u] = fp{0, 0}; M[u] = fp{0, 0}; tmin[u] = kInf; }
+            for (uint32_t c0 = 0; c0 < ns; c0 += kChunk) {
+                const uint32_t cn = min(kChunk, ns - c0);
+                __syncthreads();
+                for (uint32_t k = tid; k < cn; k += kLP) {
+                    const uint32_t e = sids[c0 + k];
+                    const uint64_t m = Sp.meta[seo + e];
+                    swv[k] = make_ulonglong2(Sp.w_lo[seo + e], Sp.w_hi[seo + e]);
+                    sinf[k] = meta_idx(m) | (meta_ch(m) << 16);
+                    sidv[k] = e;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < kLPRows; ++u) {
+                    const uint32_t r = tid + u * kLP;
+                    if (r >= Bm) break;
+                    for (uint32_t q = 0; q < cn; ++q) {
+                        const uint32_t si = sinf[q];
+                        const uint32_t sidx = si & 0xFFFFu, sch = si >> 16;
+                        const uint32_t dd = r >= sidx ? r - sidx : r + Bm - sidx;
+                        const ulonglong2 sw = swv[q];
+                        const uint32_t se = sidv[q];
+#pragma unroll
+                        for (uint32_t c = 0; c < 2; ++c) {
+                            const uint32_t e = di[2 * dd + c];
+                            if (e != kInf) {
+                                const ulonglong2 dv = dw[2 * dd + c];
+                                const fp pv = fp_mul(fp{dv.x, dv.y}, fp{sw.x, sw.y});
+                                if (c == sch) P[u] = fp_add(P[u], pv);
+                                else M[u] = fp_add(M[u], pv);
+                                const uint32_t t = denseA ? e * nB + se : se * nB + e;
+                                tmin[u] = t < tmin[u] ? t : tmin[u];
+                            }
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kLPRows; ++u) {
+                const uint32_t r = tid + u * kLP;
+                if (r >= Bm) break;
+                const uint64_t s = slot0 + r;
+                tkey[s] = tmin[u];
+                if (tmin[u] != kInf) {
+                    const uint32_t eb = (fp_nonzero(P[u]) ? 1u : 0u) | (fp_nonzero(M[u]) ? 2u : 0u);
+                    info[s] = eb;
+                    sums[2 * s] = make_ulonglong2(P[u].lo, P[u].hi);
+                    sums[2 * s + 1] = make_ulonglong2(M[u].lo, M[u].hi);
+                    any |= eb != 0;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!dense) {
+        unsigned long long* acc = (unsigned long long*)plds;
+        uint32_t* tk = (uint32_t*)(plds + 48u * Bm);
+        for (uint32_t k = tid; k < 6 * Bm; k += kLP) acc[k] = 0ull;
+        for (uint32_t k = tid; k < Bm; k += kLP) tk[k] = kInf;
+        __syncthreads();
+        const uint64_t np = (uint64_t)na * nb;
+        for (uint64_t t = tid; t < np; t += kLP) {
+            const uint32_t ai = (uint32_t)(t / nb), bj = (uint32_t)(t - (uint64_t)ai * nb);
+            const uint32_t i = idsA[ai], j = idsB[bj];
+            const uint64_t ma = g.A.meta[aeo + i], mb = g.B.meta[beo + j];
+            const uint32_t r = mod_small(meta_idx(ma) + meta_idx(mb), Bm);
+            const uint32_t chn = meta_ch(ma) ^ meta_ch(mb);
+            const fp pv = fp_mul(fp{g.A.w_lo[aeo + i], g.A.w_hi[aeo + i]}, fp{g.B.w_lo[beo + j], g.B.w_hi[beo + j]});
+            uint64_t l0, l1, l2;
+            fp_split3(pv, l0, l1, l2);
+            unsigned long long* q = acc + (size_t)(r * 2 + chn) * 3;
+            atomicAdd(q + 0, (unsigned long long)l0);
+            atomicAdd(q + 1, (unsigned long long)l1);
+            atomicAdd(q + 2, (unsigned long long)l2);
+            atomicMin(&tk[r], i * nB + j);
+        }
+        __syncthreads();
+        for (uint32_t r = tid; r < Bm; r += kLP) {
+            const uint64_t s = slot0 + r;
+            const uint32_t tkr = tk[r];
+            tkey[s] = tkr;
+            if (tkr != kInf) {
+                const unsigned long long* q = acc + (size_t)r * 6;
+                const fp p = fp_fold3(q[0], q[1], q[2]);
+                const fp m = fp_fold3(q[3], q[4], q[5]);
+                const uint32_t eb = (fp_nonzero(p) ? 1u : 0u) | (fp_nonzero(m) ? 2u : 0u);
+                info[s] = eb;
+                sums[2 * s] = make_ulonglong2(p.lo, p.hi);
+                sums[2 * s + 1] = make_ulonglong2(m.lo, m.hi);
+                any |= eb != 0;
+            }
+        }
+    }
+    if (any) S[d.o_used + (LA + LB) + lp] = 1;   // benign race: every writer stores 1
+}
+
+// ---------------------------------------------------------------- compact_layers + layer records
+// One workgroup per pair (encrypt.hpp:73-104): keep = product layers with emitted edges, plus
+// transitive PROD parents; remap by exclusive count; write the kept records (product-layer
+// ztags computed here, only for kept layers) and leave the remap in scratch for the writer.
+__device__ __forceinline__ void layer_parents(const mul_large_args& g, uint64_t alo, uint64_t blo, uint32_t LA,
+                                              uint32_t LB, uint32_t l, uint32_t& rule, uint32_t& pa, uint32_t& pb) {
+    const uint32_t base = LA + LB;
+    if (l < LA) {
+        const pvac_layer& x = g.A.layers[alo + l];
+        rule = x.rule; pa = x.pa; pb = x.pb;
+    } else if (l < base) {
+        const pvac_layer& x = g.B.layers[blo + (l - LA)];
+        rule = x.rule; pa = x.pa + LA; pb = x.pb + LA;
+    } else {
+        rule = 1; pa = (l - base) / LB; pb = LA + (l - base) % LB;
+    }
+}
+
+__global__ __launch_bounds__(kLBig) void k_large_layers(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t keep[];   // [Lc]
+    __shared__ uint32_t changed;
+    __shared__ uint32_t part[kLBig / 64];
+    const large_desc& d = g.desc[blockIdx.x];
+    uint32_t* S = g.scratch;
+    if (S[d.o_cnt + 2]) return;
+    const uint64_t pr = d.pair;
+    const uint32_t LA = d.LA, LB = d.LB, Lc = (uint32_t)d.Lc, base = LA + LB;
+    const uint64_t alo = g.A.l_off[pr], blo = g.B.l_off[pr], clo = g.C.l_off[pr];
+    uint32_t* used = S + d.o_used;
+    const int tid = threadIdx.x;
+    for (uint32_t l = tid; l < Lc; l += kLBig) keep[l] = l >= base ? (used[l] != 0) : 0u;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) changed = 0;
+        __syncthreads();
+        for (uint32_t l = tid; l < Lc; l += kLBig) {
+            if (!keep[l]) continue;
+            uint32_t rule, pa, pb;
+            layer_parents(g, alo, blo, LA, LB, l, rule, pa, pb);
+            if (rule != 1) continue;
+            if (pa < Lc && !keep[pa]) { keep[pa] = 1; changed = 1; }
+            if (pb < Lc && !keep[pb]) { keep[pb] = 1; changed = 1; }
+        }
+        __syncthreads();
+        if (!changed) break;
+    }
+    // remap = exclusive count of kept layers (chunked block scan)
+    const uint32_t per = (Lc + kLBig - 1) / kLBig;
+    uint32_t local = 0;
+    for (uint32_t l = tid * per; l < (tid + 1) * per && l < Lc; ++l) local += keep[l];
+    uint32_t kept;
+    uint32_t run = wg_exclusive_scan<kLBig>(local, part, kept);
+    for (uint32_t l = tid * per; l < (tid + 1) * per && l < Lc; ++l) {
+        const uint32_t k = keep[l];
+        keep[l] = k ? run : kInf;
+        run += k;
+    }
+    __syncthreads();
+    const bool identity = kept == Lc;
+    for (uint32_t l = tid; l < Lc; l += kLBig) {
+        const uint32_t to = keep[l];
+        used[l] = to;   // remap for the edge writer
+        if (to == kInf) continue;
+        pvac_layer y;
+        if (l < LA) {
+            y = g.A.layers[alo + l];
+        } else if (l < base) {
+            y = g.B.layers[blo + (l - LA)];
+            if (y.rule == 1) { y.pa += LA; y.pb += LA; }
+        } else {
+            const uint32_t lp = l - base;
+            const uint64_t slot = clo + l;
+            y.rule = 1; y.pad = 0;
+            y.pa = lp / LB; y.pb = LA + lp % LB;
+            y.nonce_lo = g.nonces[2 * slot];
+            y.nonce_hi = g.nonces[2 * slot + 1];
+            y.ztag = layer_ztag(g.canon_tag, y.nonce_lo, y.nonce_hi);
+        }
+        if (!identity && y.rule == 1) {
+            y.pa = y.pa < Lc ? keep[y.pa] : kInf;
+            y.pb = y.pb < Lc ? keep[y.pb] : kInf;
+        }
+        g.C.layers[clo + to] = y;
+    }
+    if (tid == 0) g.C.l_cnt[pr] = kept;
+}
+
+// ---------------------------------------------------------------- bucket chains
+__global__ __launch_bounds__(kLB) void k_large_link(mul_large_args g) {
+    const large_desc& d = g.desc[blockIdx.y];
+    uint32_t* S = g.scratch;
+    if (S[d.o_cnt + 2]) return;
+    const uint32_t Bm = g.Bm;
+    const uint32_t* tkey = S + d.o_tkey;
+    uint32_t* info = S + d.o_info;
+    uint32_t* nxt = S + d.o_nxt;
+    unsigned long long* hkey = (unsigned long long*)w64(S, d.o_hkey);
+    uint32_t* hhead = S + d.o_hhead;
+    const uint64_t hmask = (1ull << d.hbits) - 1;
+    for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
+        if (tkey[s] == kInf) continue;
+        const uint64_t lp = s / Bm, r = s - lp * Bm;
+        const uint64_t key = (lp << 32) | r;
+        const uint64_t b = fmod64(key * kGolden, d.nbm);          // std::hash -> bucket
+        uint64_t h = ((b + 1) * kGolden) >> (64 - d.hbits);
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&hkey[h], 0ull, (unsigned long long)(b + 1));
+            if (prev == 0ull || prev == b + 1) break;
+            h = (h + 1) & hmask;
+        }
+        nxt[s] = atomicExch(&hhead[h], (uint32_t)(s + 1));
+        info[s] = (info[s] & 3u) | ((uint32_t)h << 2);
+    }
+}
+
+__global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
+    const large_desc& d = g.desc[blockIdx.y];
+    uint32_t* S = g.scratch;
+    if (S[d.o_cnt + 2]) return;
+    const uint32_t* tkey = S + d.o_tkey;
+    const uint32_t* info = S + d.o_info;
+    const uint32_t* nxt = S + d.o_nxt;
+    const uint32_t* hhead = S + d.o_hhead;
+    uint32_t* tb = S + d.o_tb;
+    uint32_t* within = S + d.o_within;
+    uint32_t* etot = S + d.o_etot;
+    unsigned long long* bmask = (unsigned long long*)w64(S, d.o_bmask);
+    uint32_t* bcnt = S + d.o_bcnt;
+    for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
+        const uint32_t t = tkey[s];
+        if (t == kInf) continue;
+        uint32_t q = hhead[info[s] >> 2], tmin = t, w = 0, E = 0;
+        while (q) {
+            const uint32_t s2 = q - 1;
+            const uint32_t t2 = tkey[s2];
+            const uint32_t e2 = __popc(info[s2] & 3u);
+            tmin = t2 < tmin ? t2 : tmin;
+            w += t2 > t ? e2 : 0u;
+            E += e2;
+            q = nxt[s2];
+        }
+        tb[s] = tmin;
+        within[s] = w;
+        if (tmin == t) {
+            etot[s] = E;
+            atomicOr(&bmask[t >> 6], 1ull << (t & 63u));
+            if (E) atomicAdd(&bcnt[t >> 6], E);
+        }
+    }
+}
+
+// One workgroup per pair: suffix exclusive scan of the block counts (emit offsets), the
+// total, the guard_budget decision and, for canonical pairs, canonical positions.
+__global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
+    __shared__ uint32_t part[kLBig / 64];
+    const large_desc& d = g.desc[blockIdx.x];
+    uint32_t* S = g.scratch;
+    uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const int tid = threadIdx.x;
+    uint32_t* bcnt = S + d.o_bcnt;
+    const uint32_t nblk = (uint32_t)d.nblk;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < nblk; r0 += kLBig) {   // reversed index r -> block nblk-1-r
+        const uint32_t r = r0 + tid;
+        const uint32_t b = nblk - 1 - r;
+        const uint32_t v = r < nblk ? bcnt[b] : 0u;
+        uint32_t tot;
+        const uint32_t ex = wg_exclusive_scan<kLBig>(v, part, tot);
+        if (r < nblk) bcnt[b] = carry + ex;
+        carry += tot;
+    }
+    const uint32_t total = carry;
+    const bool canonical = (g.flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > g.edge_budget;
+    if (tid == 0) {
+        cnt[3] = total;
+        cnt[4] = canonical;
+        g.C.e_cnt[d.pair] = total;
+        g.pair_status[d.pair] = canonical ? 1 : 0;
+    }
+    if (!canonical) return;
+    const uint32_t* tkey = S + d.o_tkey;
+    const uint32_t* info = S + d.o_info;
+    uint32_t* cpos = S + d.o_cpos;
+    carry = 0;
+    for (uint64_t s0 = 0; s0 < d.S; s0 += kLBig) {
+        const uint64_t s = s0 + tid;
+        const uint32_t v = (s < d.S && tkey[s] != kInf) ? (uint32_t)__popc(info[s] & 3u) : 0u;
+        uint32_t tot;
+        const uint32_t ex = wg_exclusive_scan<kLBig>(v, part, tot);
+        if (s < d.S) cpos[s] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
+    const large_desc& d = g.desc[blockIdx.y];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const bool canonical = cnt[4] != 0;
+    const uint32_t Bm = g.Bm, LB = d.LB, nB = d.nB;
+    const uint64_t pr = d.pair;
+    const uint64_t aeo = g.A.e_off[pr], beo = g.B.e_off[pr];
+    const uint32_t* tkey = S + d.o_tkey;
+    const uint32_t* info = S + d.o_info;
+    const uint32_t* tb = S + d.o_tb;
+    const uint32_t* within = S + d.o_within;
+    const uint32_t* etot = S + d.o_etot;
+    const unsigned long long* bmask = (const unsigned long long*)w64(S, d.o_bmask);
+    const uint32_t* bcnt = S + d.o_bcnt;
+    const uint32_t* cpos = S + d.o_cpos;
+    uint32_t* order = S + d.o_order;
+    uint32_t* hpos = S + d.o_hpos;
+    for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
+        if (tkey[s] == kInf) continue;
+        const uint32_t eb = info[s] & 3u;
+        if (!eb) continue;
+        const uint32_t t = tb[s], blk = t >> 6, bit = t & 63u;
+        uint32_t hp = bcnt[blk] + within[s];
+        uint64_t m = bmask[blk] & ~((2ull << bit) - 1ull);   // leaders later in this block
+        while (m) {
+            const uint32_t b2 = (uint32_t)__ffsll((long long)m) - 1u;
+            m &= m - 1ull;
+            const uint32_t t2 = (blk << 6) | b2;
+            const uint32_t i2 = t2 / nB, j2 = t2 - i2 * nB;
+            const uint64_t ma = g.A.meta[aeo + i2], mb = g.B.meta[beo + j2];
+            const uint64_t s2 = (uint64_t)(meta_layer(ma) * LB + meta_layer(mb)) * Bm +
+                                mod_small(meta_idx(ma) + meta_idx(mb), Bm);
+            hp += etot[s2];
+        }
+        const uint32_t p = canonical ? cpos[s] : hp;
+        const uint32_t s32 = (uint32_t)s;
+        if (eb & 1u) {
+            order[p] = s32 << 1;
+            if (canonical) hpos[p] = hp;
+        }
+        if (eb & 2u) {
+            const uint32_t o = eb & 1u;
+            order[p + o] = (s32 << 1) | 1u;
+            if (canonical) hpos[p + o] = hp + o;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kLB) void k_large_write(mul_large_args g) {
+    const large_desc& d = g.desc[blockIdx.y];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const uint32_t total = cnt[3];
+    const bool canonical = cnt[4] != 0;
+    const uint32_t Bm = g.Bm, base = d.LA + d.LB;
+    const uint64_t ceo = g.C.e_off[d.pair];
+    const uint32_t* order = S + d.o_order;
+    const uint32_t* hpos = S + d.o_hpos;
+    const uint32_t* remap = S + d.o_used;
+    const ulonglong2* sums = (const ulonglong2*)(S + d.o_sums);
+    for (uint32_t p = blockIdx.x * kLB + threadIdx.x; p < total; p += gridDim.x * kLB) {
+        const uint32_t e = order[p];
+        const uint32_t s = e >> 1, ch = e & 1u;
+        const uint32_t lp = s / Bm, r = s - lp * Bm;
+        const ulonglong2 w = sums[2 * (uint64_t)s + ch];
+        g.C.meta[ceo + p] = make_meta(remap[base + lp], r, ch);
+        g.C.w_lo[ceo + p] = w.x;
+        g.C.w_hi[ceo + p] = w.y;
+        if (g.salt_pos) g.salt_pos[ceo + p] = canonical ? hpos[p] : p;
+    }
+}
+
+unsigned grid_x(uint64_t work, uint64_t per_block, uint64_t cap) {
+    uint64_t b = (work + per_block - 1) / per_block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
+}  // namespace
+
+hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
+    if (!a.nl) return hipSuccess;
+    if (a.Bm > kBmax || a.max_lay > kLargeLayersMax) return hipErrorInvalidValue;
+    const unsigned nl = a.nl;
+    const size_t plds = prod_lds_bytes(a.Bm);
+    hipLaunchKernelGGL(k_large_init, dim3(grid_x(a.max_zero > a.max_S ? a.max_zero : a.max_S, kLB * 4, 4096), nl),
+                       dim3(kLB), 0, st, a);
+    hipLaunchKernelGGL(k_large_lists, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
+    hipLaunchKernelGGL(k_large_products, dim3((unsigned)a.max_tasks, nl), dim3(kLP), plds, st, a);
+    hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
+    const unsigned gs = grid_x(a.max_S, kLB * 2, 4096);
+    hipLaunchKernelGGL(k_large_link, dim3(gs, nl), dim3(kLB), 0, st, a);
+    hipLaunchKernelGGL(k_large_rank, dim3(gs, nl), dim3(kLB), 0, st, a);
+    hipLaunchKernelGGL(k_large_scan, dim3(nl), dim3(kLBig), 0, st, a);
+    hipLaunchKernelGGL(k_large_order, dim3(gs, nl), dim3(kLB), 0, st, a);
+    hipLaunchKernelGGL(k_large_write, dim3(grid_x(a.max_capE, kLB * 2, 4096), nl), dim3(kLB), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace pvhip

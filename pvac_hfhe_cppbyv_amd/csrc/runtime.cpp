@@ -20,9 +20,7 @@ using namespace pvhip;
 
 namespace {
 
-constexpr uint32_t kNbTableLen = 4097;      // bucket counts for |A.E||B.E| in [0, 4096]
-constexpr uint32_t kSmallProdMax = 4096;
-constexpr uint32_t kSmallKeysMax = 1536;
+constexpr uint32_t kNbTableLen = kFreshProdMax + 1;   // bucket counts for |A.E||B.E| in [0, 4096]
 
 struct timer_rec {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
@@ -41,9 +39,22 @@ struct pvac_hip_ctx {
     std::string err;
     // device tables / scratch
     uint32_t* nb_table = nullptr;
+    uint64_t* nb_magic = nullptr;
     uint8_t* pair_class = nullptr;
     uint32_t* pair_status = nullptr;
+    uint64_t* large_ids = nullptr;
+    uint64_t* large_info = nullptr;
     size_t pair_cap = 0;
+    // general ct_mul path: host descriptors of the last plan, device copies, scratch arena
+    std::vector<large_desc> large_host;
+    std::vector<large_desc> large_exec;
+    uint32_t plan_stamp = 0;
+    large_desc* desc_dev = nullptr;
+    size_t desc_cap = 0;
+    uint32_t* arena = nullptr;
+    size_t arena_words = 0;
+    uint32_t* salt_pos = nullptr;
+    size_t salt_cap = 0;
     uint64_t* scan_scratch = nullptr;
     size_t scan_cap = 0;
     plan_stats* stats = nullptr;
@@ -113,11 +124,17 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
     if (n > c->pair_cap) {
         hipFree(c->pair_class);
         hipFree(c->pair_status);
+        hipFree(c->large_ids);
+        hipFree(c->large_info);
         c->pair_class = nullptr;
         c->pair_status = nullptr;
+        c->large_ids = nullptr;
+        c->large_info = nullptr;
         size_t cap = std::max<size_t>(n, 1024);
         hipError_t e = hipMalloc(&c->pair_class, cap);
         if (e == hipSuccess) e = hipMalloc(&c->pair_status, cap * 4);
+        if (e == hipSuccess) e = hipMalloc(&c->large_ids, cap * 8);
+        if (e == hipSuccess) e = hipMalloc(&c->large_info, cap * 40);
         if (e != hipSuccess) { c->pair_cap = 0; return hip_fail(c, e, "alloc pair scratch"); }
         c->pair_cap = cap;
     }
@@ -134,6 +151,95 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
 
 bool batch_ok(const pvac_ct_batch* X) {
     return X && (X->n == 0 || (X->l_off && X->l_cnt && X->e_off && X->e_cnt));
+}
+
+template <typename T>
+int ensure_dev(pvac_hip_ctx* c, T*& p, size_t& cap, size_t n, const char* what) {
+    if (n <= cap) return PVAC_OK;
+    hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(n, 1024);
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e != hipSuccess) return hip_fail(c, e, what);
+    cap = want;
+    return PVAC_OK;
+}
+
+uint32_t ceil_log2(uint64_t x) {
+    uint32_t b = 0;
+    while ((1ull << b) < x) ++b;
+    return b;
+}
+
+// Scratch layout of one general-path pair (k_mul_large.hip), offsets relative to 0; the
+// executor rebases them into the arena. 64-bit arrays on even words, 16-byte arrays on
+// multiples of four.
+int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uint64_t nA, uint64_t nB, uint32_t Bm,
+                     std::string& why) {
+    d = large_desc{};
+    d.pair = pair;
+    d.n = nA * nB;
+    d.S = LA * LB * Bm;
+    d.Lc = LA + LB + LA * LB;
+    if (LA > 0xFFFFFFFFull || LB > 0xFFFFFFFFull || nA > 0xFFFFFFFFull || nB > 0xFFFFFFFFull ||
+        (nA && d.n / nA != nB) || d.n >= (1ull << 32)) {
+        why = "ct_mul: |A.E||B.E| >= 2^32 products in one pair";
+        return PVAC_ENOSYS;
+    }
+    if (d.Lc > kLargeLayersMax) {
+        why = "ct_mul: more than " + std::to_string(kLargeLayersMax) + " layers before compaction in one pair";
+        return PVAC_ENOSYS;
+    }
+    if (d.S >= (1ull << 31)) {
+        why = "ct_mul: key space |A.L||B.L|B >= 2^31";
+        return PVAC_ENOSYS;
+    }
+    d.LA = (uint32_t)LA; d.LB = (uint32_t)LB; d.nA = (uint32_t)nA; d.nB = (uint32_t)nB;
+    d.nblk = (d.n + 63) / 64;
+    const uint64_t keys = std::min(d.n, d.S);
+    d.capE = 2 * keys;
+    d.nbm = make_fastmod64(bucket_count_after_reserve(d.n));
+    d.hbits = std::max<uint32_t>(1, ceil_log2(2 * std::max<uint64_t>(keys, 1)));
+    const uint64_t hcap = 1ull << d.hbits;
+    uint64_t o = 0;
+    auto even = [&]() { o = (o + 1) & ~1ull; };
+    auto quad = [&]() { o = (o + 3) & ~3ull; };
+    quad();
+    d.o_zero = o;
+    d.o_cnt = o; o += 8;
+    d.o_hkey = o; o += 2 * hcap;
+    d.o_hhead = o; o += hcap;
+    even();
+    d.o_bmask = o; o += 2 * d.nblk;
+    d.o_bcnt = o; o += d.nblk + 1;
+    d.o_used = o; o += d.Lc;
+    d.zero_words = o - d.o_zero;
+    d.o_tkey = o; o += d.S;
+    d.o_lstA = o; o += 2 * LA + nA;
+    d.o_lstB = o; o += 2 * LB + nB;
+    d.o_neA = o; o += LA;
+    d.o_neB = o; o += LB;
+    d.o_info = o; o += d.S;
+    quad();
+    d.o_sums = o; o += 8 * d.S;
+    d.o_nxt = o; o += d.S;
+    d.o_tb = o; o += d.S;
+    d.o_within = o; o += d.S;
+    d.o_etot = o; o += d.S;
+    d.o_cpos = o; o += d.S;
+    d.o_order = o; o += d.capE;
+    d.o_hpos = o; o += d.capE;
+    quad();
+    d.words = o;
+    return PVAC_OK;
+}
+
+void rebase_desc(large_desc& d, uint64_t base) {
+    uint64_t* f[] = {&d.o_zero, &d.o_cnt, &d.o_hkey, &d.o_hhead, &d.o_bmask, &d.o_bcnt, &d.o_used, &d.o_tkey,
+                     &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
+                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos};
+    for (uint64_t* p : f) *p += base;
 }
 
 }  // namespace
@@ -160,9 +266,15 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
     if (e != hipSuccess) { delete c; return PVAC_EDEVICE; }
     c->own_stream = true;
     std::vector<uint32_t> nb(kNbTableLen);
-    for (uint32_t n = 0; n < kNbTableLen; ++n) nb[n] = (uint32_t)bucket_count_after_reserve(n);
+    std::vector<uint64_t> mg(kNbTableLen);
+    for (uint32_t n = 0; n < kNbTableLen; ++n) {
+        nb[n] = (uint32_t)bucket_count_after_reserve(n);
+        mg[n] = make_fastmod64(nb[n]).m;
+    }
     e = hipMalloc(&c->nb_table, nb.size() * 4);
     if (e == hipSuccess) e = hipMemcpy(c->nb_table, nb.data(), nb.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&c->nb_magic, mg.size() * 8);
+    if (e == hipSuccess) e = hipMemcpy(c->nb_magic, mg.data(), mg.size() * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(plan_stats));
     if (e == hipSuccess) e = hipMalloc(&c->totals, 2 * sizeof(unsigned long long));
     if (e != hipSuccess) { pvac_hip_ctx_destroy(c); return PVAC_ENOMEM; }
@@ -176,8 +288,14 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     flush_timers(c);
     hipFree(c->nb_table);
+    hipFree(c->nb_magic);
     hipFree(c->pair_class);
     hipFree(c->pair_status);
+    hipFree(c->large_ids);
+    hipFree(c->large_info);
+    hipFree(c->desc_dev);
+    hipFree(c->arena);
+    hipFree(c->salt_pos);
     hipFree(c->scan_scratch);
     hipFree(c->stats);
     hipFree(c->totals);
@@ -254,13 +372,15 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     plan->kind = 1;
     plan->n_pairs = A->n;
     C->n = A->n;
+    c->large_host.clear();
+    plan->reserved[0] = ++c->plan_stamp;
     if (!A->n) return PVAC_OK;
     int rc = ensure_pairs(c, A->n);
     if (rc) return rc;
     hipError_t e = hipMemsetAsync(c->stats, 0, sizeof(plan_stats), c->stream);
     if (e == hipSuccess)
-        e = launch_plan_mul(*A, *B, *C, c->pair_class, c->stats, c->nb_table, kNbTableLen, c->prm.B, kSmallKeysMax,
-                            kSmallProdMax, c->stream);
+        e = launch_plan_mul(*A, *B, *C, c->pair_class, c->large_ids, c->stats, c->nb_table, kNbTableLen, c->prm.B,
+                            c->stream);
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->l_off, A->n, c->scan_scratch, &c->totals[0], c->stream);
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->e_off, A->n, c->scan_scratch, &c->totals[1], c->stream);
     plan_stats st{};
@@ -279,8 +399,94 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     plan->max_nb = st.max_nb;
     plan->max_buckets = st.max_buckets;
     plan->max_layers = st.max_layers;
+    if (st.n_large) {
+        // shapes of the general-path pairs -> host descriptors (bucket counts from this libstdc++)
+        std::vector<uint64_t> info(5 * st.n_large);
+        e = launch_gather_large(*A, *B, c->large_ids, st.n_large, c->large_info, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(info.data(), c->large_info, info.size() * 8, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_plan (large)");
+        c->large_host.resize(st.n_large);
+        for (uint64_t k = 0; k < st.n_large; ++k) {
+            std::string why;
+            rc = build_large_desc(c->large_host[k], info[5 * k], info[5 * k + 1], info[5 * k + 2], info[5 * k + 3],
+                                  info[5 * k + 4], c->prm.B, why);
+            if (rc) {
+                c->large_host.clear();
+                return fail(c, rc, why);
+            }
+        }
+        // deterministic launch order (the plan kernel appends in arrival order)
+        std::sort(c->large_host.begin(), c->large_host.end(),
+                  [](const large_desc& x, const large_desc& y) { return x.pair < y.pair; });
+    }
     return PVAC_OK;
 }
+
+namespace {
+
+// Runs the general path over the plan's large pairs in sub-batches that fit the scratch budget.
+int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, const uint64_t* nonces,
+              pvac_ct_batch* C, uint32_t flags, uint32_t* salt_pos) {
+    const size_t nl = c->large_host.size();
+    int rc = ensure_dev(c, c->desc_dev, c->desc_cap, nl, "alloc large descriptors");
+    if (rc) return rc;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
+    uint64_t budget = std::max<uint64_t>((uint64_t)(free_b / 2) / 4 + c->arena_words, 1ull << 24);
+    budget = std::min<uint64_t>(budget, 16ull << 30);   // <= 64 GiB of scratch per sub-batch
+    c->large_exec = c->large_host;
+    size_t i = 0;
+    while (i < nl) {
+        uint64_t words = 0;
+        size_t j = i;
+        uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0;
+        while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
+            large_desc& d = c->large_exec[j];
+            const uint64_t w = d.words;
+            rebase_desc(d, words);
+            words += w;
+            mS = std::max(mS, d.S);
+            mZ = std::max(mZ, d.zero_words);
+            mT = std::max<uint64_t>(mT, (uint64_t)d.LA * d.LB);
+            mE = std::max(mE, d.capE);
+            mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
+            ++j;
+        }
+        if (words > c->arena_words) {
+            hipStreamSynchronize(c->stream);
+            hipFree(c->arena);
+            c->arena = nullptr;
+            c->arena_words = 0;
+            hipError_t e = hipMalloc(&c->arena, words * 4);
+            if (e != hipSuccess) return hip_fail(c, e, "alloc ct_mul scratch arena");
+            c->arena_words = words;
+        }
+        hipError_t e = hipMemcpyAsync(c->desc_dev + i, c->large_exec.data() + i, (j - i) * sizeof(large_desc),
+                                      hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "upload large descriptors");
+        mul_large_args a{};
+        a.A = *A; a.B = *B; a.C = *C;
+        a.nonces = nonces;
+        a.pair_status = c->pair_status;
+        a.desc = c->desc_dev + i;
+        a.scratch = c->arena;
+        a.nl = (uint32_t)(j - i);
+        a.Bm = c->prm.B;
+        a.canon_tag = c->prm.canon_tag;
+        a.edge_budget = c->prm.edge_budget;
+        a.flags = flags;
+        a.salt_pos = salt_pos;
+        a.max_S = mS; a.max_zero = mZ; a.max_tasks = mT; a.max_capE = mE; a.max_lay = mL;
+        e = launch_ct_mul_large(a, c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_large");
+        i = j;
+    }
+    return PVAC_OK;
+}
+
+}  // namespace
 
 int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_ct_batch* A, const pvac_ct_batch* B,
                          const uint64_t* nonces, const uint64_t* salts, pvac_ct_batch* C, uint32_t flags) {
@@ -288,39 +494,55 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         return fail(c, PVAC_EINVAL, "ct_mul_exec: bad arguments");
     if (A->n != plan->n_pairs || B->n != plan->n_pairs) return fail(c, PVAC_EINVAL, "ct_mul_exec: plan mismatch");
     if (!A->n) return PVAC_OK;
+    if (plan->reserved[0] != c->plan_stamp || plan->n_large != c->large_host.size())
+        return fail(c, PVAC_EINVAL, "ct_mul_exec: plan is not this context's latest ct_mul plan");
     if (!nonces) return fail(c, PVAC_EINVAL, "ct_mul_exec: nonces required");
     if (!C->layers || !C->meta || !C->w_lo || !C->w_hi) return fail(c, PVAC_EINVAL, "ct_mul_exec: output arrays");
-    if (plan->n_large)
-        return fail(c, PVAC_ENOSYS, "ct_mul_exec: pairs beyond the fresh-shape kernel need the layer-dense path");
     const bool with_sigma = (flags & PVAC_MUL_WITH_SIGMA) != 0;
     if (with_sigma && (!salts || !C->sigma || !c->H.ready))
         return fail(c, PVAC_EINVAL, "ct_mul_exec: WITH_SIGMA needs salts, C->sigma and H");
+    uint32_t* salt_pos = nullptr;
+    if (with_sigma) {
+        int rc = ensure_dev(c, c->salt_pos, c->salt_cap, plan->total_edge_slots, "alloc salt positions");
+        if (rc) return rc;
+        salt_pos = c->salt_pos;
+    }
     if (plan->n_small) {
-        mul_small_args a{};
+        mul_fresh_args a{};
         a.A = *A; a.B = *B; a.C = *C;
         a.nonces = nonces;
-        a.salt_pos = nullptr;
         a.pair_class = c->pair_class;
         a.pair_status = c->pair_status;
         a.nb_table = c->nb_table;
+        a.nb_magic = c->nb_magic;
+        a.salt_pos = salt_pos;
         a.canon_tag = c->prm.canon_tag;
         a.edge_budget = c->prm.edge_budget;
         a.Bm = c->prm.B;
         a.flags = flags;
-        a.ks_max = plan->max_keys;
+        a.ks_max = std::max<uint32_t>(plan->max_keys, 32u);   // LDS sizing floor (0-key batches)
         a.prod_max = plan->max_prod;
         a.na_max = plan->max_na;
         a.nb_max = plan->max_nb;
         a.buckets_max = plan->max_buckets;
         a.layers_max = plan->max_layers;
-        int blocks = 0;
-        scoped_timer t(c, "ct_mul_small");
-        hipError_t e = launch_ct_mul_small(a, c->num_cus, c->stream, &blocks);
-        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_small");
+        {
+            scoped_timer t(c, "mul_layers_fresh");
+            hipError_t e = launch_mul_layers_fresh(a, c->stream);
+            if (e != hipSuccess) return hip_fail(c, e, "mul_layers_fresh");
+        }
+        scoped_timer t(c, "ct_mul_fresh");
+        hipError_t e = launch_ct_mul_fresh(a, c->num_cus, c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_fresh");
+    }
+    if (plan->n_large) {
+        scoped_timer t(c, "ct_mul_large");
+        int rc = run_large(c, A, B, nonces, C, flags, salt_pos);
+        if (rc) return rc;
     }
     if (with_sigma) {
         scoped_timer t(c, "sigma");
-        hipError_t e = launch_sigma(c->H, c->prm, *C, salts, nullptr, c->num_cus, c->stream);
+        hipError_t e = launch_sigma(c->H, c->prm, *C, salts, salt_pos, c->num_cus, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "sigma");
     }
     return PVAC_OK;

@@ -1,0 +1,222 @@
+"""GPU parity of the general ct_mul path (k_mul_large.hip): chains c_k = c_{k-1} * x_k
+(reference tests/test_main.cpp:289-295), squares c <- c * c (tests/test_depth.cpp:46), pairs the
+fresh kernel cannot hold, mixed batches, duplicate edges, guard_budget ordering. Bit-exact
+against the reference's golden fixtures and the pinned CPU oracle."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from helpers import REF, Cipher, LAYER_DT, read_ct, read_layers_u64, read_u64, R_for
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev_batch(engine, ciphers, sigma=False):
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, HostCipher
+    hc = [HostCipher(c.layers, c.meta, c.w_lo, c.w_hi, c.sigma) for c in ciphers]
+    return DeviceBatch.from_host(hc, engine.device, sigma=sigma)
+
+
+def _i64(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64))
+
+
+def _layers_view(L):
+    L = L.copy()
+    prod = L["rule"] == 1
+    for f in ("ztag", "nonce_lo", "nonce_hi"):
+        L[f][prod] = 0
+    L["pa"][~prod] = 0
+    L["pb"][~prod] = 0
+    return L
+
+
+def _same(got, ref, view=True, sigma=False):
+    L = _layers_view(got.layers) if view else got.layers
+    for f in ("rule", "pa", "pb", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(L[f], ref.layers[f]), f
+    assert got.nE == ref.nE
+    assert np.array_equal(got.meta, ref.meta)
+    assert np.array_equal(got.w_lo, ref.w_lo) and np.array_equal(got.w_hi, ref.w_hi)
+    if sigma:
+        assert np.array_equal(got.sigma, ref.sigma)
+
+
+def _run_mul(eng, xs, ys, streams=None, seed=1, flags=0, with_salts=False):
+    """Batched ct_mul; per-pair reference streams (nonces, then salts) placed at their slots."""
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    loff = Cb.l_off.cpu().numpy().view(np.uint64)
+    eoff = Cb.e_off.cpu().numpy().view(np.uint64)
+    rng = np.random.default_rng(seed)
+    nonces = rng.integers(0, 2**63, 2 * max(plan.total_layer_slots, 1), dtype=np.uint64)
+    salts = np.zeros(max(plan.total_edge_slots, 1), np.uint64)
+    per = []
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        base = int(loff[p]) + x.nL + y.nL
+        nn = 2 * x.nL * y.nL
+        if streams is not None:
+            nonces[2 * base:2 * base + nn] = streams[p][:nn]
+            s = streams[p][nn:]
+            salts[int(eoff[p]):int(eoff[p]) + len(s)] = s
+        per.append(nonces[2 * base:2 * base + nn].copy())
+    kw = {}
+    if with_salts:
+        kw["salts"] = _i64(salts).to(eng.device)
+    out = eng.ct_mul(A, B, nonces=_i64(nonces).to(eng.device), C_=Cb, plan=plan, flags=flags, **kw)
+    return out.to_host(), plan, per
+
+
+def _sigdig(sig):
+    """Per-edge digest of the harness: first 8 bytes (LE) of SHA-256 over the LE sigma words."""
+    return np.array([int.from_bytes(hashlib.sha256(row.astype("<u8").tobytes()).digest()[:8], "little")
+                     for row in sig], np.uint64)
+
+
+# ------------------------------------------------------------------ reference golden chains
+@pytest.mark.parametrize("kind,steps", [("chain", 3), ("sq", 2)])
+def test_chain_and_square_golden_gpu(manifest, kind, steps):
+    """Each step as a batch of one through the engine: layers (incl. ztags), edge order and
+    weights identical to the reference's .ct; edges/layers/dec values from the manifest."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    from helpers import Oracle
+    orc = Oracle.load()
+    eng = Engine(device=0, canon_tag=manifest["canon_tag"])
+    c = read_ct(os.path.join(REF, f"{kind}0.ct"))[0]
+    Rin = [(c, read_u64(f"{kind}0_R.u64"))]
+    cur = c
+    for k in range(1, steps + 1):
+        if kind == "chain":
+            x = read_ct(os.path.join(REF, f"chain{k}_x.ct"))[0]
+            Rin.append((x, read_u64(f"chain{k}_x_R.u64")))
+        else:
+            x = cur
+        stream = read_u64(f"{kind}{k}_stream.u64")
+        out, plan, _ = _run_mul(eng, [cur], [x], [stream])
+        if k >= 2:
+            assert plan.n_large == 1, "step >= 2 must take the general path"
+        got = out[0]
+        _same(got, read_ct(os.path.join(REF, f"{kind}{k}.ct"))[0])
+        full = read_layers_u64(f"{kind}{k}_layers.u64")
+        assert np.array_equal(got.layers["ztag"], full["ztag"])
+        rec = manifest["chain" if kind == "chain" else "square"][k - 1]
+        assert got.nE == rec["edges"] and got.nL == rec["layers"]
+        gc = Cipher(got.layers, got.meta, got.w_lo, got.w_hi)
+        assert list(orc.dec(gc, read_u64("powg_B.u64"), R_for(gc, Rin))) == rec["dec"]
+        cur = Cipher(full, got.meta, got.w_lo, got.w_hi)
+
+
+def test_chain_sigma_golden_gpu(manifest):
+    """WITH_SIGMA on chain step 2 (general path): every output sigma's digest equals the
+    reference's (crypto/matrix.hpp:267-303 with the reference's salts)."""
+    from pvac_hfhe_cppbyv_amd import Engine, MUL_WITH_SIGMA
+    eng = Engine(device=0, canon_tag=manifest["canon_tag"])
+    assert eng.gen_H().hex() == manifest["H_digest"]
+    c1 = Cipher(read_layers_u64("chain1_layers.u64"), *[getattr(read_ct(os.path.join(REF, "chain1.ct"))[0], f)
+                                                         for f in ("meta", "w_lo", "w_hi")])
+    x = read_ct(os.path.join(REF, "chain2_x.ct"))[0]
+    out, plan, _ = _run_mul(eng, [c1], [x], [read_u64("chain2_stream.u64")], flags=MUL_WITH_SIGMA,
+                            with_salts=True)
+    assert plan.n_large == 1
+    assert np.array_equal(_sigdig(out[0].sigma), read_u64("chain2_sigdig.u64"))
+
+
+# ------------------------------------------------------------------ synthetic vs oracle
+def _mk(rng, nl, ne, dup_ok=True, B=337):
+    L = np.zeros(nl, LAYER_DT)
+    L["ztag"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+    L["nonce_lo"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+    if nl == 0:
+        ne = 0
+    if dup_ok:
+        lay = rng.integers(0, max(nl, 1), ne).astype(np.uint64)
+        idx = rng.integers(0, B, ne).astype(np.uint64)
+        ch = rng.integers(0, 2, ne).astype(np.uint64)
+    else:   # distinct (layer, idx, ch), shuffled
+        pick = rng.choice(max(nl, 1) * 2 * B, size=ne, replace=False).astype(np.uint64)
+        lay, rest = pick // np.uint64(2 * B), pick % np.uint64(2 * B)
+        idx, ch = rest >> np.uint64(1), rest & np.uint64(1)
+    meta = lay | (idx << np.uint64(32)) | (ch << np.uint64(48))
+    lo = rng.integers(0, 2**63, ne, dtype=np.uint64)
+    hi = rng.integers(0, 2**62, ne, dtype=np.uint64)
+    return Cipher(L, meta, lo, hi)
+
+
+def _check_vs_oracle(oracle, eng_kw, xs, ys, seed):
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, **eng_kw)
+    out, plan, per = _run_mul(eng, xs, ys, seed=seed)
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        ref = oracle.ct_mul(x, y, per[p], canon_tag=eng_kw.get("canon_tag", 0),
+                            edge_budget=eng_kw.get("edge_budget", 1200000))
+        _same(out[p], ref, view=False)
+    return plan
+
+
+def test_large_dense_chain_like_vs_oracle(oracle):
+    """Dense-owner mode: 3-6 layer ciphers with 200-674 distinct edges per layer times fresh-like
+    ciphers, plus their transposes (dense side = B)."""
+    rng = np.random.default_rng(5)
+    xs, ys = [], []
+    for k in range(12):
+        nl = 3 + k % 4
+        x = _mk(rng, nl, int(nl * rng.integers(200, 674)), dup_ok=False)
+        y = _mk(rng, 2, 40, dup_ok=False)
+        xs.append(x); ys.append(y)
+        xs.append(y); ys.append(x)
+    plan = _check_vs_oracle(oracle, {"canon_tag": 7}, xs, ys, 11)
+    assert plan.n_large == len(xs)
+
+
+def test_large_scatter_and_duplicates_vs_oracle(oracle):
+    """Scatter mode (sparse x sparse tasks) and duplicate (layer, idx, ch) edges in the dense side,
+    empty layers, empty ciphers, single edges."""
+    rng = np.random.default_rng(6)
+    shapes = [((5, 30), (4, 30)), ((3, 700), (3, 5)), ((8, 8), (8, 8)), ((2, 0), (9, 10)), ((0, 0), (7, 1)),
+              ((6, 1), (6, 1)), ((4, 400), (2, 60)), ((12, 90), (3, 40))]
+    xs = [_mk(rng, *a) for a, _ in shapes]
+    ys = [_mk(rng, *b) for _, b in shapes]
+    _check_vs_oracle(oracle, {"canon_tag": 8}, xs, ys, 12)
+
+
+def test_large_guard_budget_vs_oracle(oracle):
+    """guard_budget -> compact_edges order for pairs above edge_budget (encrypt.hpp:106-111)."""
+    rng = np.random.default_rng(7)
+    xs = [_mk(rng, 4, 600, dup_ok=False) for _ in range(3)]
+    ys = [_mk(rng, 2, 40, dup_ok=False) for _ in range(3)]
+    _check_vs_oracle(oracle, {"canon_tag": 9, "edge_budget": 2000}, xs, ys, 13)
+
+
+def test_mixed_batch_small_and_large_vs_oracle(oracle):
+    """Fresh-shape and general pairs interleaved in one batch share one output CSR."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    rng = np.random.default_rng(8)
+    xs, ys = [], []
+    for k in range(40):
+        if k % 3 == 0:
+            xs.append(_mk(rng, 4, 900, dup_ok=False)); ys.append(_mk(rng, 2, 40, dup_ok=False))
+        else:
+            xs.append(_mk(rng, 2, 40, dup_ok=False)); ys.append(_mk(rng, 2, 40, dup_ok=False))
+    plan = _check_vs_oracle(oracle, {"canon_tag": 10}, xs, ys, 14)
+    assert plan.n_small > 0 and plan.n_large > 0
+
+
+def test_engine_chain_depth5_vs_oracle(oracle):
+    """Engine-driven chains c_k = c_{k-1} * x_k for 16 inputs to depth 5, each step checked against
+    the oracle on the engine's own previous output (cfg-4 shape at reduced depth)."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0xC4)
+    n = 16
+    X = eng.gen_fresh(n, 0x4000, 20).to_host()
+    cur = [Cipher(c.layers, c.meta, c.w_lo, c.w_hi) for c in X]
+    for k in range(1, 6):
+        xk = [Cipher(c.layers, c.meta, c.w_lo, c.w_hi) for c in eng.gen_fresh(n, 0x4000 + k, 20).to_host()]
+        out, plan, per = _run_mul(eng, cur, xk, seed=100 + k)
+        for p in range(n):
+            ref = oracle.ct_mul(cur[p], xk[p], per[p], canon_tag=0xC4)
+            _same(out[p], ref, view=False)
+        cur = [Cipher(o.layers, o.meta, o.w_lo, o.w_hi) for o in out]
+    assert cur[0].nE > 10000

@@ -1,0 +1,35 @@
+#!/bin/bash
+# PMC passes over bench.py's dominant kernel (one counter group per rocprofv3 run, as the
+# MI355X guide prescribes: FETCH_SIZE and WRITE_SIZE cannot share a pass).
+# Usage (GPU box): tools/prof_pmc.sh [kernel-regex] [extra bench args...]
+# Output: gpurun_out/pmc/<pass>/... (CSV) + gpurun_out/pmc/summary.json
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+export TMPDIR=/tmp
+KRE="${1:-k_ct_mul}"
+shift || true
+OUT="$ROOT/gpurun_out/pmc"
+mkdir -p "$OUT"
+BENCH=(python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu --no-extras "$@")
+passes=(
+  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY"
+  "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+  "GRBM_GUI_ACTIVE GRBM_COUNT"
+)
+i=0
+for p in "${passes[@]}"; do
+  i=$((i + 1))
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $p --kernel-include-regex "$KRE" -d "$OUT/p$i" -o run \
+      --output-format csv -- "${BENCH[@]}" > "$OUT/p$i.log" 2>&1)
+  rc=$?
+  echo "pass $i ($p): rc=$rc"
+  if [ $rc -ne 0 ]; then
+    tail -5 "$OUT/p$i.log"
+    # counter-name errors are harmless (nothing ran on the GPU); anything else stops the script
+    if ! grep -qi "counter\|not found\|invalid\|unsupported" "$OUT/p$i.log"; then exit $rc; fi
+  fi
+done
+python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.json" && cat "$OUT/summary.json"
