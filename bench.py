@@ -34,6 +34,11 @@ def parse():
     ap.add_argument("--cpu-pairs", type=int, default=1 << 17)
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--sigma-pairs", type=int, default=1 << 12)
+    ap.add_argument("--chain-inputs", type=int, default=1 << 12, help="cfg 4 chain inputs timed (per chunk run)")
+    ap.add_argument("--chain-chunk", type=int, default=1 << 10)
+    ap.add_argument("--chain-depth", type=int, default=8)
+    ap.add_argument("--only", choices=["chain", "sigma", "fp"], default=None,
+                    help="run one side measurement alone (profiling) and print its JSON")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     return ap.parse_args()
@@ -55,24 +60,29 @@ def main():
 
     eng = Engine(device=local, canon_tag=0x5EED0003)
     dev = eng.device
+    if args.only == "chain":
+        print(json.dumps(chain_bench(eng, args)), flush=True)
+        return
+    from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks
     n = args.pairs
-    seed = 0x5EED0003 + 0x1000 * rank
-    A = eng.gen_fresh(n, seed, args.epl)
-    B = eng.gen_fresh(n, seed + 1, args.epl)
+    # weak scaling: rank r owns global pairs [r*n, (r+1)*n); inputs and nonces are keyed by the
+    # global pair index, so the N-GPU result is the 1-GPU result of the same global batch, sharded
+    first = rank * n
+    seed = 0x5EED0003
+    A = eng.gen_fresh(n, seed, args.epl, first_index=first)
+    B = eng.gen_fresh(n, seed + 1, args.epl, first_index=first)
     nonces = None
-    totals = torch.zeros(world, dtype=torch.int64, device=dev)
-    mine = torch.zeros(1, dtype=torch.int64, device=dev)
+    placement = {}
 
     def step():
         nonlocal nonces
         Cb, plan = eng.ct_mul_plan(A, B)
         if nonces is None or nonces.numel() < 2 * plan.total_layer_slots:
-            nonces = torch.empty(2 * plan.total_layer_slots, dtype=torch.int64, device=dev)
-            eng.fill_random(nonces, seed + 2)
+            nonces = eng.fill_nonces(A, B, Cb, plan, seed + 2, first_index=first)
         out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
-        if world > 1:   # gather-only: per-rank output totals -> global offsets of the sharded result
-            mine.copy_(out.e_cnt[:n].sum().view(1))
-            dist.all_gather_into_tensor(totals, mine)
+        # gather-only (cfg 5): per-rank output totals -> this shard's offset in the global edge CSR
+        off, total, _ = global_edge_offsets(plan.total_edge_slots, device=dev)
+        placement.update(offset=off, total_edge_slots=total)
         return out, plan
 
     for _ in range(args.warmup):
@@ -95,10 +105,7 @@ def main():
     eng.timing(False)
     kern_ms, kern_launches = eng.timing_get("ct_mul_fresh")
     lay_ms, lay_launches = eng.timing_get("mul_layers_fresh")
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device=dev)
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * n / (elapsed / args.steps)
 
@@ -139,6 +146,8 @@ def main():
             "global_pairs": world * n,
             "output_edges_per_pair": out_edges / n,
             "parallelism": f"dp{world} (independent pair shards, gather of totals over RCCL)",
+            "shard": {"first_pair": first, "edge_slot_offset": placement.get("offset"),
+                      "global_edge_slots": placement.get("total_edge_slots")},
         },
         "roofline": {
             "bound": "hbm",
@@ -316,7 +325,43 @@ def extras(eng, args, with_cpu):
     if with_cpu:
         full["cpu_baseline"] = _ref_full_baseline()
     res["ct_mul_with_sigma"] = full
+    res["cfg4_chain"] = chain_bench(eng, args)
     return res
+
+
+def chain_bench(eng, args):
+    """cfg 4 (SURVEY 8(d) restatement of test_depth): c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) to depth
+    8 over fresh-shaped x_i, in chunks; every step is plan + exec on the general path."""
+    import torch
+    dev = eng.device
+    n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
+    step_ms = [0.0] * depth
+    step_edges = [0.0] * depth
+    products = 0.0
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for c0 in range(0, n, chunk):
+        k = min(chunk, n - c0)
+        X = eng.gen_fresh(k, 0x5EED0004 + c0, args.epl)
+        cur = X
+        for d in range(depth):
+            ts = time.perf_counter()
+            Cb, plan = eng.ct_mul_plan(cur, X)
+            nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=dev)
+            eng.fill_random(nonces, 0x5EED0040 + 97 * c0 + d)
+            out = eng.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
+            torch.cuda.synchronize(dev)
+            step_ms[d] += 1000.0 * (time.perf_counter() - ts)
+            products += float((cur.e_cnt[:k].to(torch.float64) * X.e_cnt[:k].to(torch.float64)).sum().item())
+            step_edges[d] += float(out.e_cnt[:k].sum().item())
+            del Cb, nonces
+            cur = out
+        del cur, X
+        torch.cuda.empty_cache()
+    el = time.perf_counter() - t0
+    return {"inputs": n, "depth": depth, "chunk": chunk, "seconds": el, "chains_per_s": n / el,
+            "ct_mul_per_s": n * depth / el, "products": products, "Gfp_mul_per_s": products / el / 1e9,
+            "edges_per_input_by_step": [e / n for e in step_edges], "ms_by_step": step_ms}
 
 
 def _ref_full_baseline():

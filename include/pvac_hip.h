@@ -178,6 +178,15 @@ int pvac_hip_sigma_batch(pvac_hip_ctx* ctx, pvac_ct_batch* X, const uint64_t* sa
  * nonzero canonical weights, edges grouped by layer and Fisher-Yates shuffled within a layer.
  * Writes a dense CSR batch whose arrays the caller allocated for n*2 layers, n*2*epl edges. */
 int pvac_hip_gen_fresh_batch(pvac_hip_ctx* ctx, uint64_t seed, uint32_t edges_per_layer, pvac_ct_batch* X);
+/* Same generator keyed by GLOBAL cipher index first_index + i, so a shard reproduces the
+ * corresponding slice of a single-GPU batch (multi-GPU acceptance: N-GPU output == 1-GPU). */
+int pvac_hip_gen_fresh_batch_at(pvac_hip_ctx* ctx, uint64_t seed, uint64_t first_index, uint32_t edges_per_layer,
+                                pvac_ct_batch* X);
+/* Product-layer nonces for a planned ct_mul (C->l_off from pvac_hip_ct_mul_plan), keyed by
+ * (seed, GLOBAL pair index first_index + i, product layer): replaces make_nonce128's draws
+ * (core/types.hpp:77-79) for synthetic, shard-invariant batches. out: 2 words per C layer slot. */
+int pvac_hip_fill_nonces(pvac_hip_ctx* ctx, uint64_t seed, uint64_t first_index, const pvac_ct_batch* A,
+                         const pvac_ct_batch* B, const pvac_ct_batch* C, uint64_t* out);
 /* splitmix64 stream fill (device): out[i] = splitmix64(seed + (i+1)*golden). */
 int pvac_hip_fill_random(pvac_hip_ctx* ctx, uint64_t seed, uint64_t* out, size_t n);
 /* Host-only: the bucket count std::unordered_map::reserve(n) picks on this libstdc++ (the

@@ -1,0 +1,438 @@
+// pvac_hip.hpp — header-only C++17 adapter: the pvac-hfhe 0.1.0 by-value ciphertext API on top of
+// the MI355X C ABI (pvac_hip.h / libpvac_hip.so).
+//
+// It is templated on the REFERENCE'S OWN types (include/pvac/core/types.hpp:72-139): any Cipher
+// with `L` (Layer{rule, seed{ztag, nonce{lo, hi}}, pa, pb}) and `E` (Edge{layer_id, idx, ch,
+// w{lo, hi}, s{nbits, w}}) vectors and any PubKey with `prm{B, m_bits, n_bits, h_col_wt,
+// x_col_wt, err_wt, edge_budget}`, `canon_tag` and `H` (vector of BitVec columns). Nothing of
+// the reference is copied; a maintainer routes the reference's functions here:
+//
+//   pvac::ct_mul(pk, A, B)  (ops/arithmetic.hpp:47)  -> pvac_hip::ct_mul(pk, A, B)
+//   pvac::ct_add(pk, A, B)  (ops/arithmetic.hpp:12)  -> pvac_hip::ct_add(pk, A, B)
+//   pvac::ct_sub(pk, A, B)  (ops/arithmetic.hpp:43)  -> pvac_hip::ct_sub(pk, A, B)
+//   pvac::ct_scale(pk, A,s) (ops/arithmetic.hpp:33)  -> pvac_hip::ct_scale(pk, A, s)
+// plus batched forms (std::vector of pairs in, std::vector out) that keep one launch per batch.
+//
+// Randomness: like the reference (core/random.hpp:40-110), nonces (2 words per new product
+// layer, (la, lb) row-major, lo then hi) and salts (1 word per emitted edge, in emit order) come
+// from getrandom(2) one 8-byte draw at a time, in the reference's order for a single ct_mul. A
+// caller-supplied source (any callable returning uint64_t) replaces it for reproducible runs.
+// Errors: C ABI status codes become pvac_hip::Error (the reference has no error codes and lets
+// std::bad_alloc escape, arithmetic.hpp:76).
+//
+// Build: g++/hipcc -std=c++17 -I<repo>/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__
+//        ... -L<repo>/pvac_hfhe_cppbyv_amd/lib -lpvac_hip -L/opt/rocm/lib -lamdhip64
+#ifndef PVAC_HIP_HPP
+#define PVAC_HIP_HPP
+
+#include <hip/hip_runtime_api.h>
+#include <sys/random.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "pvac_hip.h"
+
+namespace pvac_hip {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+using RandomSource = std::function<uint64_t()>;
+
+// One 8-byte getrandom per word, as csprng_u64 does (core/random.hpp:106-110).
+inline uint64_t os_random_u64() {
+    uint64_t v = 0;
+    size_t got = 0;
+    while (got < sizeof v) {
+        const ssize_t r = getrandom(reinterpret_cast<uint8_t*>(&v) + got, sizeof v - got, 0);
+        if (r <= 0) throw Error(PVAC_EDEVICE, "getrandom failed");
+        got += (size_t)r;
+    }
+    return v;
+}
+
+namespace detail {
+
+inline void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw Error(PVAC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// RAII device array of T
+template <class T>
+struct dev_array {
+    T* p = nullptr;
+    size_t n = 0;
+    dev_array() = default;
+    explicit dev_array(size_t count) { alloc(count); }
+    dev_array(const dev_array&) = delete;
+    dev_array& operator=(const dev_array&) = delete;
+    dev_array(dev_array&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    ~dev_array() { if (p) (void)hipFree(p); }
+    void alloc(size_t count) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = count;
+        hip_ok(hipMalloc(&p, (count ? count : 1) * sizeof(T)), "hipMalloc");
+    }
+    void upload(const T* h, size_t count, hipStream_t s) {
+        if (count) hip_ok(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s), "H2D");
+    }
+    void download(T* h, size_t count, hipStream_t s) const {
+        if (count) hip_ok(hipMemcpyAsync(h, p, count * sizeof(T), hipMemcpyDeviceToHost, s), "D2H");
+    }
+};
+
+// Host SoA image of a batch of reference Ciphers + its device copy.
+struct batch {
+    std::vector<uint64_t> l_off, l_cnt, e_off, e_cnt, meta, w_lo, w_hi, sigma;
+    std::vector<pvac_layer> layers;
+    dev_array<uint64_t> d_l_off, d_l_cnt, d_e_off, d_e_cnt, d_meta, d_w_lo, d_w_hi, d_sigma;
+    dev_array<pvac_layer> d_layers;
+    uint32_t sigma_words = 0;
+
+    pvac_ct_batch view(bool with_sigma) {
+        pvac_ct_batch b{};
+        b.n = l_cnt.size();
+        b.l_off = d_l_off.p; b.l_cnt = d_l_cnt.p; b.layers = d_layers.p;
+        b.e_off = d_e_off.p; b.e_cnt = d_e_cnt.p;
+        b.meta = d_meta.p; b.w_lo = d_w_lo.p; b.w_hi = d_w_hi.p;
+        b.sigma = with_sigma ? d_sigma.p : nullptr;
+        b.sigma_words = sigma_words;
+        return b;
+    }
+};
+
+template <class CipherT>
+void to_host(const std::vector<const CipherT*>& cs, uint32_t sigma_words, bool with_sigma, batch& b) {
+    const size_t n = cs.size();
+    b.sigma_words = sigma_words;
+    b.l_off.resize(n); b.l_cnt.resize(n); b.e_off.resize(n); b.e_cnt.resize(n);
+    uint64_t lo = 0, eo = 0;
+    for (size_t i = 0; i < n; ++i) {
+        b.l_off[i] = lo; b.l_cnt[i] = cs[i]->L.size(); lo += cs[i]->L.size();
+        b.e_off[i] = eo; b.e_cnt[i] = cs[i]->E.size(); eo += cs[i]->E.size();
+    }
+    b.layers.resize(lo);
+    b.meta.resize(eo); b.w_lo.resize(eo); b.w_hi.resize(eo);
+    if (with_sigma) b.sigma.assign(eo * sigma_words, 0);
+    size_t l = 0, e = 0;
+    for (const CipherT* c : cs) {
+        for (const auto& L : c->L) {
+            pvac_layer& y = b.layers[l++];
+            y.rule = (uint32_t)L.rule; y.pa = L.pa; y.pb = L.pb; y.pad = 0;
+            y.ztag = L.seed.ztag; y.nonce_lo = L.seed.nonce.lo; y.nonce_hi = L.seed.nonce.hi;
+        }
+        for (const auto& E : c->E) {
+            b.meta[e] = (uint64_t)E.layer_id | ((uint64_t)E.idx << 32) | ((uint64_t)E.ch << 48);
+            b.w_lo[e] = E.w.lo; b.w_hi[e] = E.w.hi;
+            if (with_sigma) {
+                const size_t k = std::min<size_t>(E.s.w.size(), sigma_words);
+                if (k) std::memcpy(&b.sigma[e * sigma_words], E.s.w.data(), k * 8);
+            }
+            ++e;
+        }
+    }
+}
+
+inline void upload(batch& b, hipStream_t s, bool with_sigma) {
+    b.d_l_off.alloc(b.l_off.size()); b.d_l_off.upload(b.l_off.data(), b.l_off.size(), s);
+    b.d_l_cnt.alloc(b.l_cnt.size()); b.d_l_cnt.upload(b.l_cnt.data(), b.l_cnt.size(), s);
+    b.d_e_off.alloc(b.e_off.size()); b.d_e_off.upload(b.e_off.data(), b.e_off.size(), s);
+    b.d_e_cnt.alloc(b.e_cnt.size()); b.d_e_cnt.upload(b.e_cnt.data(), b.e_cnt.size(), s);
+    b.d_layers.alloc(b.layers.size()); b.d_layers.upload(b.layers.data(), b.layers.size(), s);
+    b.d_meta.alloc(b.meta.size()); b.d_meta.upload(b.meta.data(), b.meta.size(), s);
+    b.d_w_lo.alloc(b.w_lo.size()); b.d_w_lo.upload(b.w_lo.data(), b.w_lo.size(), s);
+    b.d_w_hi.alloc(b.w_hi.size()); b.d_w_hi.upload(b.w_hi.data(), b.w_hi.size(), s);
+    if (with_sigma) { b.d_sigma.alloc(b.sigma.size()); b.d_sigma.upload(b.sigma.data(), b.sigma.size(), s); }
+}
+
+// Output records of capacity layer/edge slots; the per-cipher offset/count arrays were
+// allocated before the plan (which writes the offsets) and are kept.
+inline void alloc_out(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t sigma_words, bool with_sigma) {
+    c.sigma_words = sigma_words;
+    c.d_layers.alloc(lslots);
+    c.d_meta.alloc(eslots); c.d_w_lo.alloc(eslots); c.d_w_hi.alloc(eslots);
+    if (with_sigma) c.d_sigma.alloc(eslots * sigma_words);
+    c.l_cnt.resize(n);
+}
+
+template <class CipherT>
+std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t m_bits,
+                                 bool with_sigma, hipStream_t s) {
+    c.l_off.resize(n); c.l_cnt.resize(n); c.e_off.resize(n); c.e_cnt.resize(n);
+    c.layers.resize(lslots); c.meta.resize(eslots); c.w_lo.resize(eslots); c.w_hi.resize(eslots);
+    c.d_l_off.download(c.l_off.data(), n, s); c.d_l_cnt.download(c.l_cnt.data(), n, s);
+    c.d_e_off.download(c.e_off.data(), n, s); c.d_e_cnt.download(c.e_cnt.data(), n, s);
+    c.d_layers.download(c.layers.data(), lslots, s);
+    c.d_meta.download(c.meta.data(), eslots, s);
+    c.d_w_lo.download(c.w_lo.data(), eslots, s); c.d_w_hi.download(c.w_hi.data(), eslots, s);
+    if (with_sigma) {
+        c.sigma.resize(eslots * c.sigma_words);
+        c.d_sigma.download(c.sigma.data(), c.sigma.size(), s);
+    }
+    hip_ok(hipStreamSynchronize(s), "sync");
+    std::vector<CipherT> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        CipherT& C = out[i];
+        C.L.resize(c.l_cnt[i]);
+        for (size_t l = 0; l < c.l_cnt[i]; ++l) {
+            const pvac_layer& y = c.layers[c.l_off[i] + l];
+            auto& L = C.L[l];
+            L.rule = static_cast<decltype(L.rule)>(y.rule);
+            L.pa = y.pa; L.pb = y.pb;
+            L.seed.ztag = y.ztag; L.seed.nonce.lo = y.nonce_lo; L.seed.nonce.hi = y.nonce_hi;
+        }
+        C.E.resize(c.e_cnt[i]);
+        for (size_t k = 0; k < c.e_cnt[i]; ++k) {
+            const size_t e = c.e_off[i] + k;
+            auto& E = C.E[k];
+            E.layer_id = (uint32_t)c.meta[e];
+            E.idx = (uint16_t)(c.meta[e] >> 32);
+            E.ch = (uint8_t)(c.meta[e] >> 48);
+            E.w.lo = c.w_lo[e]; E.w.hi = c.w_hi[e];
+            E.s.nbits = m_bits;
+            if (with_sigma) E.s.w.assign(&c.sigma[e * c.sigma_words], &c.sigma[e * c.sigma_words] + c.sigma_words);
+            else E.s.w.assign(c.sigma_words, 0);
+        }
+    }
+    return out;
+}
+
+}  // namespace detail
+
+// One device context per (device, canon_tag); owns the device copy of pk.H for sigma.
+class Engine {
+public:
+    Engine(int device, const pvac_hip_params& prm) : prm_(prm) {
+        const int rc = pvac_hip_ctx_create(device, &prm, &ctx_);
+        if (rc) throw Error(rc, "pvac_hip_ctx_create failed (no MI355X / HIP runtime?)");
+        stream_ = (hipStream_t)pvac_hip_ctx_stream(ctx_);
+    }
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+    ~Engine() { pvac_hip_ctx_destroy(ctx_); }
+
+    template <class PubKeyT>
+    static pvac_hip_params params_of(const PubKeyT& pk) {
+        pvac_hip_params p{};
+        p.B = (uint32_t)pk.prm.B; p.m_bits = (uint32_t)pk.prm.m_bits; p.n_bits = (uint32_t)pk.prm.n_bits;
+        p.h_col_wt = (uint32_t)pk.prm.h_col_wt; p.x_col_wt = (uint32_t)pk.prm.x_col_wt;
+        p.err_wt = (uint32_t)pk.prm.err_wt; p.edge_budget = (uint64_t)pk.prm.edge_budget;
+        p.canon_tag = pk.canon_tag;
+        return p;
+    }
+
+    pvac_hip_ctx* ctx() const { return ctx_; }
+    uint32_t sigma_words() const { return (prm_.m_bits + 63) / 64; }
+
+    // H regenerated on the device from canon_tag (gen_H, crypto/matrix.hpp:191-251); returns the
+    // H_digest for comparison with pk.H_digest.
+    std::vector<uint8_t> gen_H() {
+        std::vector<uint8_t> d(32);
+        check(pvac_hip_ctx_gen_H(ctx_, d.data()));
+        h_ready_ = true;
+        return d;
+    }
+
+    // pk.H (dense BitVec columns) -> device sparse columns, once; an empty pk.H (e.g. a key
+    // loaded without H) is regenerated on the device from canon_tag.
+    template <class PubKeyT>
+    void ensure_H(const PubKeyT& pk) {
+        if (h_ready_) return;
+        if (pk.H.empty()) {
+            (void)gen_H();
+            return;
+        }
+        const uint32_t wpc = sigma_words();
+        std::vector<uint64_t> dense((size_t)pk.H.size() * wpc, 0);
+        for (size_t c = 0; c < pk.H.size(); ++c)
+            std::memcpy(&dense[c * wpc], pk.H[c].w.data(), std::min<size_t>(pk.H[c].w.size(), wpc) * 8);
+        check(pvac_hip_ctx_set_H(ctx_, dense.data(), (uint32_t)pk.H.size(), wpc));
+        h_ready_ = true;
+    }
+
+    // Batched ct_mul (ops/arithmetic.hpp:47-106) over pairs (A[i], B[i]). with_sigma needs pk.H.
+    template <class PubKeyT, class CipherT>
+    std::vector<CipherT> ct_mul(const PubKeyT& pk, const std::vector<const CipherT*>& A,
+                                const std::vector<const CipherT*>& B, bool with_sigma, const RandomSource& rnd) {
+        if (A.size() != B.size()) throw Error(PVAC_EINVAL, "ct_mul: |A| != |B|");
+        const size_t n = A.size();
+        if (!n) return {};
+        if (with_sigma) ensure_H(pk);
+        detail::batch a, b, c;
+        detail::to_host(A, sigma_words(), false, a);
+        detail::to_host(B, sigma_words(), false, b);
+        detail::upload(a, stream_, false);
+        detail::upload(b, stream_, false);
+        pvac_ct_batch va = a.view(false), vb = b.view(false);
+        c.d_l_off.alloc(n); c.d_l_cnt.alloc(n); c.d_e_off.alloc(n); c.d_e_cnt.alloc(n);
+        pvac_ct_batch vc{};
+        vc.l_off = c.d_l_off.p; vc.l_cnt = c.d_l_cnt.p; vc.e_off = c.d_e_off.p; vc.e_cnt = c.d_e_cnt.p;
+        pvac_hip_plan plan{};
+        check(pvac_hip_ct_mul_plan(ctx_, &va, &vb, &vc, &plan));
+        // nonces per pair in the reference's draw order: (la, lb) row-major, lo then hi
+        std::vector<uint64_t> loff(n);
+        c.d_l_off.download(loff.data(), n, stream_);
+        detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+        std::vector<uint64_t> nonces(2 * (plan.total_layer_slots ? plan.total_layer_slots : 1), 0);
+        for (size_t i = 0; i < n; ++i) {
+            const uint64_t LA = A[i]->L.size(), LB = B[i]->L.size();
+            const uint64_t s0 = loff[i] + LA + LB;
+            for (uint64_t k = 0; k < LA * LB; ++k) {
+                nonces[2 * (s0 + k)] = rnd();
+                nonces[2 * (s0 + k) + 1] = rnd();
+            }
+        }
+        detail::dev_array<uint64_t> d_nonces(nonces.size());
+        d_nonces.upload(nonces.data(), nonces.size(), stream_);
+        detail::alloc_out(c, n, plan.total_layer_slots, plan.total_edge_slots, sigma_words(), with_sigma);
+        vc = c.view(false);
+        vc.n = n;
+        check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, nullptr, &vc, 0));
+        if (with_sigma) {
+            // one salt per emitted edge, drawn after the weights are known (arithmetic.hpp:90-94);
+            // the second exec reproduces the same edges and consumes the salts in hash order
+            std::vector<uint64_t> ecnt(n), eoff(n);
+            c.d_e_cnt.download(ecnt.data(), n, stream_);
+            c.d_e_off.download(eoff.data(), n, stream_);
+            detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+            std::vector<uint64_t> salts(plan.total_edge_slots ? plan.total_edge_slots : 1, 0);
+            for (size_t i = 0; i < n; ++i)
+                for (uint64_t k = 0; k < ecnt[i]; ++k) salts[eoff[i] + k] = rnd();
+            detail::dev_array<uint64_t> d_salts(salts.size());
+            d_salts.upload(salts.data(), salts.size(), stream_);
+            check(pvac_hip_ct_mul_plan(ctx_, &va, &vb, &vc, &plan));
+            vc = c.view(true);
+            vc.n = n;
+            check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, d_salts.p, &vc, PVAC_MUL_WITH_SIGMA));
+            return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits,
+                                                true, stream_);
+        }
+        return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits, false,
+                                            stream_);
+    }
+
+    // Batched ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45); sigmas carried through.
+    template <class CipherT>
+    std::vector<CipherT> ct_add(const std::vector<const CipherT*>& A, const std::vector<const CipherT*>& B, bool negate_b) {
+        if (A.size() != B.size()) throw Error(PVAC_EINVAL, "ct_add: |A| != |B|");
+        const size_t n = A.size();
+        if (!n) return {};
+        detail::batch a, b, c;
+        detail::to_host(A, sigma_words(), true, a);
+        detail::to_host(B, sigma_words(), true, b);
+        detail::upload(a, stream_, true);
+        detail::upload(b, stream_, true);
+        pvac_ct_batch va = a.view(true), vb = b.view(true);
+        c.d_l_off.alloc(n); c.d_l_cnt.alloc(n); c.d_e_off.alloc(n); c.d_e_cnt.alloc(n);
+        pvac_ct_batch vc{};
+        vc.l_off = c.d_l_off.p; vc.l_cnt = c.d_l_cnt.p; vc.e_off = c.d_e_off.p; vc.e_cnt = c.d_e_cnt.p;
+        pvac_hip_plan plan{};
+        check(pvac_hip_ct_add_plan(ctx_, &va, &vb, &vc, &plan));
+        detail::alloc_out(c, n, plan.total_layer_slots, plan.total_edge_slots, sigma_words(), true);
+        vc = c.view(true);
+        vc.n = n;
+        check(pvac_hip_ct_add_exec(ctx_, &plan, &va, &vb, negate_b ? 1 : 0, &vc));
+        return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits, true,
+                                            stream_);
+    }
+
+    // Element-wise Fp over host arrays (core/field.hpp:50-71, 209-213), one launch.
+    void fp_binop(int op, const uint64_t* a_lo, const uint64_t* a_hi, const uint64_t* b_lo, const uint64_t* b_hi,
+                  uint64_t* c_lo, uint64_t* c_hi, size_t n) {
+        if (!n) return;
+        detail::dev_array<uint64_t> d[6];
+        for (auto& x : d) x.alloc(n);
+        d[0].upload(a_lo, n, stream_); d[1].upload(a_hi, n, stream_);
+        const size_t nb = op == PVAC_FP_SCALE ? 1 : n;
+        if (op != PVAC_FP_NEG) { d[2].upload(b_lo, nb, stream_); d[3].upload(b_hi, nb, stream_); }
+        check(pvac_hip_fp_binop(ctx_, op, d[0].p, d[1].p, d[2].p, d[3].p, d[4].p, d[5].p, n));
+        d[4].download(c_lo, n, stream_); d[5].download(c_hi, n, stream_);
+        detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+    }
+
+private:
+    void check(int rc) {
+        if (rc) throw Error(rc, std::string("pvac_hip: ") + pvac_hip_last_error(ctx_));
+    }
+    pvac_hip_params prm_;
+    pvac_hip_ctx* ctx_ = nullptr;
+    hipStream_t stream_ = nullptr;
+    bool h_ready_ = false;
+};
+
+// Process-wide engines keyed by canon_tag (one public key = one context), device 0 unless
+// PVAC_HIP_DEVICE is set. Contexts are not shared between threads (C ABI contract).
+template <class PubKeyT>
+Engine& engine_for(const PubKeyT& pk) {
+    thread_local std::map<uint64_t, std::unique_ptr<Engine>> engines;
+    auto it = engines.find(pk.canon_tag);
+    if (it == engines.end()) {
+        const char* d = std::getenv("PVAC_HIP_DEVICE");
+        it = engines.emplace(pk.canon_tag, std::make_unique<Engine>(d ? std::atoi(d) : 0, Engine::params_of(pk))).first;
+    }
+    return *it->second;
+}
+
+// ---- drop-in single-op forms (ops/arithmetic.hpp signatures) ------------------------------
+template <class PubKeyT, class CipherT>
+CipherT ct_mul(const PubKeyT& pk, const CipherT& A, const CipherT& B, const RandomSource& rnd = os_random_u64) {
+    return engine_for(pk).ct_mul(pk, std::vector<const CipherT*>{&A}, std::vector<const CipherT*>{&B}, true, rnd)[0];
+}
+
+template <class PubKeyT, class CipherT>
+CipherT ct_add(const PubKeyT& pk, const CipherT& A, const CipherT& B) {
+    return engine_for(pk).ct_add(std::vector<const CipherT*>{&A}, std::vector<const CipherT*>{&B}, false)[0];
+}
+
+template <class PubKeyT, class CipherT>
+CipherT ct_sub(const PubKeyT& pk, const CipherT& A, const CipherT& B) {
+    return engine_for(pk).ct_add(std::vector<const CipherT*>{&A}, std::vector<const CipherT*>{&B}, true)[0];
+}
+
+// ct_scale (ops/arithmetic.hpp:33-37): every edge weight times s.
+template <class PubKeyT, class CipherT, class FpT>
+CipherT ct_scale(const PubKeyT& pk, const CipherT& A, const FpT& s) {
+    CipherT C = A;
+    const size_t n = C.E.size();
+    std::vector<uint64_t> lo(n), hi(n), slo{s.lo}, shi{s.hi};
+    for (size_t i = 0; i < n; ++i) { lo[i] = C.E[i].w.lo; hi[i] = C.E[i].w.hi; }
+    engine_for(pk).fp_binop(PVAC_FP_SCALE, lo.data(), hi.data(), slo.data(), shi.data(), lo.data(), hi.data(), n);
+    for (size_t i = 0; i < n; ++i) { C.E[i].w.lo = lo[i]; C.E[i].w.hi = hi[i]; }
+    return C;
+}
+
+// ---- batched forms ------------------------------------------------------------------------
+template <class PubKeyT, class CipherT>
+std::vector<CipherT> ct_mul_batch(const PubKeyT& pk, const std::vector<CipherT>& A, const std::vector<CipherT>& B,
+                                  bool with_sigma = true, const RandomSource& rnd = os_random_u64) {
+    std::vector<const CipherT*> a, b;
+    for (auto& x : A) a.push_back(&x);
+    for (auto& x : B) b.push_back(&x);
+    return engine_for(pk).ct_mul(pk, a, b, with_sigma, rnd);
+}
+
+template <class PubKeyT, class CipherT>
+std::vector<CipherT> ct_add_batch(const PubKeyT& pk, const std::vector<CipherT>& A, const std::vector<CipherT>& B,
+                                  bool negate_b = false) {
+    std::vector<const CipherT*> a, b;
+    for (auto& x : A) a.push_back(&x);
+    for (auto& x : B) b.push_back(&x);
+    return engine_for(pk).ct_add(a, b, negate_b);
+}
+
+}  // namespace pvac_hip
+
+#endif  // PVAC_HIP_HPP

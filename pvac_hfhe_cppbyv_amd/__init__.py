@@ -84,6 +84,8 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_ct_scale": ([vp, C.POINTER(CtBatch), u64, u64], i32),
         "pvac_hip_sigma_batch": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_gen_fresh_batch": ([vp, u64, u32, C.POINTER(CtBatch)], i32),
+        "pvac_hip_gen_fresh_batch_at": ([vp, u64, u64, u32, C.POINTER(CtBatch)], i32),
+        "pvac_hip_fill_nonces": ([vp, u64, u64, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch), vp], i32),
         "pvac_hip_fill_random": ([vp, u64, vp, C.c_size_t], i32),
         "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_bucket_count": ([u64], u64),
@@ -308,11 +310,20 @@ class Engine:
         self._check(self.lib.pvac_hip_fill_random(self.ctx, seed, C.c_void_p(t.data_ptr()), t.numel()))
         return t
 
-    def gen_fresh(self, n, seed, edges_per_layer=20):
+    def gen_fresh(self, n, seed, edges_per_layer=20, first_index=0):
+        """cfg-3 synthetic fresh-shaped ciphers; cipher i is keyed by global index first_index + i."""
         X = DeviceBatch.empty(n, 2 * n, 2 * edges_per_layer * n, self.device)
         sx = X.struct()
-        self._check(self.lib.pvac_hip_gen_fresh_batch(self.ctx, seed, edges_per_layer, C.byref(sx)))
+        self._check(self.lib.pvac_hip_gen_fresh_batch_at(self.ctx, seed, first_index, edges_per_layer, C.byref(sx)))
         return X
+
+    def fill_nonces(self, A, B, C_, plan, seed, first_index=0):
+        """Product-layer nonces keyed by (seed, global pair index, product layer) for a planned ct_mul."""
+        out = self.torch.zeros(2 * max(plan.total_layer_slots, 1), dtype=self.torch.int64, device=self.device)
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        self._check(self.lib.pvac_hip_fill_nonces(self.ctx, seed, first_index, C.byref(sa), C.byref(sb), C.byref(sc),
+                                                  C.c_void_p(out.data_ptr())))
+        return out
 
     def digest(self, X: DeviceBatch):
         out = self.torch.empty(max(X.n, 1), dtype=self.torch.int64, device=self.device)

@@ -53,7 +53,10 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* p
 hipError_t launch_fp_binop(int op, const uint64_t* alo, const uint64_t* ahi, const uint64_t* blo,
                            const uint64_t* bhi, uint64_t* clo, uint64_t* chi, size_t n, hipStream_t st);
 hipError_t launch_fill_random(uint64_t seed, uint64_t* out, size_t n, hipStream_t st);
-hipError_t launch_gen_fresh(uint64_t seed, uint32_t epl, uint32_t B, const pvac_ct_batch& X, hipStream_t st);
+hipError_t launch_gen_fresh(uint64_t seed, uint64_t first, uint32_t epl, uint32_t B, const pvac_ct_batch& X,
+                            hipStream_t st);
+hipError_t launch_fill_nonces(uint64_t seed, uint64_t first, const pvac_ct_batch& A, const pvac_ct_batch& B,
+                              const uint64_t* c_l_off, uint64_t* out, hipStream_t st);
 hipError_t launch_batch_digest(const pvac_ct_batch& X, uint64_t* out, hipStream_t st);
 hipError_t launch_ct_scale(const pvac_ct_batch& X, uint64_t slo, uint64_t shi, hipStream_t st);
 

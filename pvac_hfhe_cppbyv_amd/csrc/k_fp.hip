@@ -118,14 +118,15 @@ __global__ void k_fill_random(uint64_t seed, uint64_t* out, size_t n) {
 // Distinct (idx, ch) per layer drawn by rejection against an LDS bitmap, weights uniform
 // nonzero canonical, edges grouped by layer and Fisher-Yates shuffled within each layer.
 constexpr int kGenBlock = 64;
-__global__ __launch_bounds__(kGenBlock) void k_gen_fresh(uint64_t seed, uint32_t epl, uint32_t B,
+__global__ __launch_bounds__(kGenBlock) void k_gen_fresh(uint64_t seed, uint64_t first, uint32_t epl, uint32_t B,
                                                          pvac_ct_batch X) {
     extern __shared__ __attribute__((aligned(16))) uint64_t gen_lds[];
     const uint32_t words = (2 * B + 63) / 64;
     uint64_t* used = gen_lds + (size_t)threadIdx.x * words;
     const uint64_t i = (uint64_t)blockIdx.x * kGenBlock + threadIdx.x;
     if (i >= X.n) return;
-    uint64_t s = seed ^ (i * 0xD1B54A32D192ED03ULL);
+    // keyed by the GLOBAL cipher index: a shard [first, first + n) reproduces a 1-GPU batch
+    uint64_t s = seed ^ ((first + i) * 0xD1B54A32D192ED03ULL);
     (void)splitmix64(s);
     const uint64_t loff = 2 * i, eoff = 2ull * epl * i;
     X.l_off[i] = loff;
@@ -157,6 +158,21 @@ __global__ __launch_bounds__(kGenBlock) void k_gen_fresh(uint64_t seed, uint32_t
             X.meta[e0 + k] = X.meta[e0 + j]; X.w_lo[e0 + k] = X.w_lo[e0 + j]; X.w_hi[e0 + k] = X.w_hi[e0 + j];
             X.meta[e0 + j] = m; X.w_lo[e0 + j] = a; X.w_hi[e0 + j] = b;
         }
+    }
+}
+
+// Product-layer nonces keyed by (seed, GLOBAL pair index, product layer): word 2k/2k+1 of the
+// product layer (la, lb) of pair i sits at its output layer slot (ABI nonce convention).
+__global__ void k_fill_nonces(uint64_t seed, uint64_t first, pvac_ct_batch A, pvac_ct_batch B, const uint64_t* c_l_off,
+                              uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint64_t LA = A.l_cnt[i], LB = B.l_cnt[i];
+    const uint64_t s0 = c_l_off[i] + LA + LB;
+    for (uint64_t k = 0; k < LA * LB; ++k) {
+        uint64_t s = seed ^ ((first + i) * 0xD1B54A32D192ED03ULL) ^ (k * 0x8CB92BA72F3D8DD7ULL);
+        out[2 * (s0 + k)] = splitmix64(s);
+        out[2 * (s0 + k) + 1] = splitmix64(s);
     }
 }
 
@@ -214,13 +230,22 @@ hipError_t launch_fill_random(uint64_t seed, uint64_t* out, size_t n, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_gen_fresh(uint64_t seed, uint32_t epl, uint32_t B, const pvac_ct_batch& X, hipStream_t st) {
+hipError_t launch_fill_nonces(uint64_t seed, uint64_t first, const pvac_ct_batch& A, const pvac_ct_batch& B,
+                              const uint64_t* c_l_off, uint64_t* out, hipStream_t st) {
+    if (!A.n) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_nonces, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, st, seed, first, A, B,
+                       c_l_off, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_fresh(uint64_t seed, uint64_t first, uint32_t epl, uint32_t B, const pvac_ct_batch& X,
+                            hipStream_t st) {
     if (!X.n) return hipSuccess;
     if (epl == 0 || epl > 2 * B) return hipErrorInvalidValue;
     const size_t words = (2 * B + 63) / 64;
     const size_t lds = words * 8 * kGenBlock;
     const size_t blocks = (X.n + kGenBlock - 1) / kGenBlock;
-    hipLaunchKernelGGL(k_gen_fresh, dim3((unsigned)blocks), dim3(kGenBlock), lds, st, seed, epl, B, X);
+    hipLaunchKernelGGL(k_gen_fresh, dim3((unsigned)blocks), dim3(kGenBlock), lds, st, seed, first, epl, B, X);
     return hipGetLastError();
 }
 

@@ -626,8 +626,19 @@ int pvac_hip_sigma_batch(pvac_hip_ctx* c, pvac_ct_batch* X, const uint64_t* salt
 
 // ---------------------------------------------------------------- synthetic / checks
 int pvac_hip_gen_fresh_batch(pvac_hip_ctx* c, uint64_t seed, uint32_t epl, pvac_ct_batch* X) {
+    return pvac_hip_gen_fresh_batch_at(c, seed, 0, epl, X);
+}
+
+int pvac_hip_gen_fresh_batch_at(pvac_hip_ctx* c, uint64_t seed, uint64_t first_index, uint32_t epl,
+                                pvac_ct_batch* X) {
     if (!c || !batch_ok(X) || !X->layers || !X->meta || !X->w_lo || !X->w_hi) return PVAC_EINVAL;
-    return hip_fail(c, launch_gen_fresh(seed, epl, c->prm.B, *X, c->stream), "gen_fresh");
+    return hip_fail(c, launch_gen_fresh(seed, first_index, epl, c->prm.B, *X, c->stream), "gen_fresh");
+}
+
+int pvac_hip_fill_nonces(pvac_hip_ctx* c, uint64_t seed, uint64_t first_index, const pvac_ct_batch* A,
+                         const pvac_ct_batch* B, const pvac_ct_batch* C, uint64_t* out) {
+    if (!c || !batch_ok(A) || !batch_ok(B) || !C || !C->l_off || (A->n && !out) || A->n != B->n) return PVAC_EINVAL;
+    return hip_fail(c, launch_fill_nonces(seed, first_index, *A, *B, C->l_off, out, c->stream), "fill_nonces");
 }
 
 int pvac_hip_fill_random(pvac_hip_ctx* c, uint64_t seed, uint64_t* out, size_t n) {

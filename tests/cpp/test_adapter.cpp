@@ -1,0 +1,282 @@
+// test_adapter.cpp — the C++ drop-in adapter (include/pvac_hip.hpp) driven the way reference code
+// calls the by-value API (tests/test_main.cpp:172-313 style), on types that mirror the reference's
+// field layout (include/pvac/core/types.hpp:72-139), checked against the golden fixtures minted by
+// the unmodified reference (tests/golden/ref, tests/golden/bounty). Runs on the GPU box:
+//   test_adapter <golden_dir> <canon_tag> <H_digest_hex>
+// Exit 0 = every check passed; failures abort with a message (like the reference's must()).
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "pvac_hip.hpp"
+
+namespace mirror {   // same member names/types as pvac:: (core/types.hpp, core/field.hpp, core/bitvec.hpp)
+struct Fp { uint64_t lo, hi; };
+struct BitVec { size_t nbits = 0; std::vector<uint64_t> w; };
+struct Nonce128 { uint64_t lo, hi; };
+struct RSeed { uint64_t ztag; Nonce128 nonce; };
+enum class RRule : uint8_t { BASE = 0, PROD = 1 };
+struct Layer { RRule rule; RSeed seed; uint32_t pa; uint32_t pb; };
+struct Edge { uint32_t layer_id; uint16_t idx; uint8_t ch; Fp w; BitVec s; };
+struct Cipher { std::vector<Layer> L; std::vector<Edge> E; };
+struct Params {
+    int B = 337, m_bits = 8192, n_bits = 16384, h_col_wt = 192, x_col_wt = 128, err_wt = 128;
+    size_t edge_budget = 1200000;
+};
+struct PubKey { Params prm; uint64_t canon_tag = 0; std::vector<BitVec> H; };
+}  // namespace mirror
+
+using mirror::Cipher;
+
+static int g_checks = 0;
+#define MUST(cond, ...)                                                        \
+    do {                                                                       \
+        ++g_checks;                                                            \
+        if (!(cond)) {                                                         \
+            std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);          \
+            std::fprintf(stderr, __VA_ARGS__);                                 \
+            std::fprintf(stderr, "\n");                                        \
+            std::exit(1);                                                      \
+        }                                                                      \
+    } while (0)
+
+// ---- .ct codec (format of the reference's tests/add.cpp:22-155; our own reader/writer)
+static std::vector<uint8_t> slurp(const std::string& p) {
+    std::ifstream f(p, std::ios::binary);
+    MUST(f.good(), "open %s", p.c_str());
+    return std::vector<uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+struct reader {
+    const std::vector<uint8_t>& b;
+    size_t o = 0;
+    template <class T> T get() {
+        T v;
+        MUST(o + sizeof(T) <= b.size(), "truncated .ct");
+        std::memcpy(&v, &b[o], sizeof(T));
+        o += sizeof(T);
+        return v;
+    }
+};
+
+static std::vector<Cipher> read_ct(const std::string& path) {
+    const auto buf = slurp(path);
+    reader r{buf};
+    MUST(r.get<uint32_t>() == 0x66699666u && r.get<uint32_t>() == 1u, "bad .ct header %s", path.c_str());
+    const uint64_t n = r.get<uint64_t>();
+    std::vector<Cipher> out(n);
+    for (auto& c : out) {
+        const uint32_t nL = r.get<uint32_t>(), nE = r.get<uint32_t>();
+        c.L.resize(nL);
+        for (auto& L : c.L) {
+            L = mirror::Layer{};
+            L.rule = (mirror::RRule)r.get<uint8_t>();
+            if (L.rule == mirror::RRule::BASE) {
+                L.seed.ztag = r.get<uint64_t>();
+                L.seed.nonce.lo = r.get<uint64_t>();
+                L.seed.nonce.hi = r.get<uint64_t>();
+            } else if (L.rule == mirror::RRule::PROD) {
+                L.pa = r.get<uint32_t>();
+                L.pb = r.get<uint32_t>();
+            } else {
+                r.o += 24;
+            }
+        }
+        c.E.resize(nE);
+        for (auto& E : c.E) {
+            E.layer_id = r.get<uint32_t>();
+            E.idx = r.get<uint16_t>();
+            E.ch = r.get<uint8_t>();
+            (void)r.get<uint8_t>();
+            E.w.lo = r.get<uint64_t>();
+            E.w.hi = r.get<uint64_t>();
+            E.s.nbits = r.get<uint32_t>();
+            E.s.w.resize((E.s.nbits + 63) / 64);
+            for (auto& w : E.s.w) w = r.get<uint64_t>();
+        }
+    }
+    MUST(r.o == buf.size(), "trailing bytes in %s", path.c_str());
+    return out;
+}
+
+template <class T>
+static void put(std::vector<uint8_t>& o, T v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    o.insert(o.end(), p, p + sizeof(T));
+}
+
+static std::vector<uint8_t> write_ct(const std::vector<Cipher>& cs) {
+    std::vector<uint8_t> o;
+    put<uint32_t>(o, 0x66699666u);
+    put<uint32_t>(o, 1u);
+    put<uint64_t>(o, cs.size());
+    for (const auto& c : cs) {
+        put<uint32_t>(o, (uint32_t)c.L.size());
+        put<uint32_t>(o, (uint32_t)c.E.size());
+        for (const auto& L : c.L) {
+            put<uint8_t>(o, (uint8_t)L.rule);
+            if (L.rule == mirror::RRule::BASE) {
+                put(o, L.seed.ztag); put(o, L.seed.nonce.lo); put(o, L.seed.nonce.hi);
+            } else {
+                put(o, L.pa); put(o, L.pb);
+            }
+        }
+        for (const auto& E : c.E) {
+            put(o, E.layer_id); put(o, E.idx); put(o, E.ch); put<uint8_t>(o, 0);
+            put(o, E.w.lo); put(o, E.w.hi);
+            put<uint32_t>(o, (uint32_t)E.s.nbits);
+            for (uint64_t w : E.s.w) put(o, w);
+        }
+    }
+    return o;
+}
+
+static std::vector<uint64_t> read_u64(const std::string& p) {
+    const auto b = slurp(p);
+    std::vector<uint64_t> v(b.size() / 8);
+    std::memcpy(v.data(), b.data(), v.size() * 8);
+    return v;
+}
+
+// A .ct keeps BASE seeds and PROD parents only: project a full cipher the same way.
+static Cipher ct_view(Cipher c) {
+    for (auto& L : c.L) {
+        if (L.rule == mirror::RRule::PROD) L.seed = mirror::RSeed{};
+        else { L.pa = 0; L.pb = 0; }
+    }
+    return c;
+}
+
+static bool same_edges(const Cipher& a, const Cipher& b, bool sigma) {
+    if (a.E.size() != b.E.size()) return false;
+    for (size_t i = 0; i < a.E.size(); ++i) {
+        const auto &x = a.E[i], &y = b.E[i];
+        if (x.layer_id != y.layer_id || x.idx != y.idx || x.ch != y.ch || x.w.lo != y.w.lo || x.w.hi != y.w.hi)
+            return false;
+        if (sigma && x.s.w != y.s.w) return false;
+    }
+    return true;
+}
+
+static bool same_layers(const Cipher& a, const Cipher& b) {
+    if (a.L.size() != b.L.size()) return false;
+    for (size_t i = 0; i < a.L.size(); ++i) {
+        const auto &x = a.L[i], &y = b.L[i];
+        if (x.rule != y.rule || x.pa != y.pa || x.pb != y.pb || x.seed.ztag != y.seed.ztag ||
+            x.seed.nonce.lo != y.seed.nonce.lo || x.seed.nonce.hi != y.seed.nonce.hi)
+            return false;
+    }
+    return true;
+}
+
+// replays a reference random stream (nonces, then salts) like the harness' getrandom log
+struct replay {
+    std::vector<uint64_t> s;
+    size_t k = 0;
+    uint64_t operator()() {
+        MUST(k < s.size(), "random stream exhausted");
+        return s[k++];
+    }
+};
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        std::fprintf(stderr, "usage: %s <golden_dir> <canon_tag> <H_digest_hex>\n", argv[0]);
+        return 2;
+    }
+    const std::string gold = argv[1], ref = gold + "/ref", bounty = gold + "/bounty";
+    mirror::PubKey pk;
+    pk.canon_tag = std::strtoull(argv[2], nullptr, 10);
+    const std::string hdig = argv[3];
+
+    // H regenerated on the device from canon_tag matches the reference key's H_digest
+    auto& eng = pvac_hip::engine_for(pk);
+    const auto d = eng.gen_H();
+    char hex[65];
+    for (int i = 0; i < 32; ++i) std::snprintf(hex + 2 * i, 3, "%02x", d[i]);
+    MUST(hdig == hex, "H_digest %s != %s", hex, hdig.c_str());
+
+    // ct_add / ct_sub (ops/arithmetic.hpp:12-45) on the 8 golden pairs, sigmas carried
+    for (int p = 0; p < 8; ++p) {
+        const Cipher x = read_ct(ref + "/pair" + std::to_string(p) + "_x.ct")[0];
+        const Cipher y = read_ct(ref + "/pair" + std::to_string(p) + "_y.ct")[0];
+        const Cipher s = pvac_hip::ct_add(pk, x, y);
+        const Cipher r_add = read_ct(ref + "/pair" + std::to_string(p) + "_add.ct")[0];
+        MUST(same_layers(ct_view(s), r_add) && same_edges(s, r_add, true), "ct_add pair %d", p);
+        const Cipher dlt = pvac_hip::ct_sub(pk, x, y);
+        const Cipher r_sub = read_ct(ref + "/pair" + std::to_string(p) + "_sub.ct")[0];
+        MUST(same_layers(ct_view(dlt), r_sub) && same_edges(dlt, r_sub, true), "ct_sub pair %d", p);
+        // ct_scale by p-1 (= ct_neg, arithmetic.hpp:39-41) gives the B half of ct_sub
+        const Cipher ny = pvac_hip::ct_scale(pk, y, mirror::Fp{~0ull - 1, 0x7FFFFFFFFFFFFFFFull});
+        for (size_t e = 0; e < ny.E.size(); ++e) {
+            const auto& want = r_sub.E[x.E.size() + e].w;
+            MUST(ny.E[e].w.lo == want.lo && ny.E[e].w.hi == want.hi, "ct_scale pair %d edge %zu", p, e);
+        }
+    }
+
+    // bounty2_data: sum.ct == combine(a.ct, b.ct) byte for byte through the adapter
+    {
+        const Cipher a = read_ct(bounty + "/a.ct")[0], b = read_ct(bounty + "/b.ct")[0];
+        const Cipher s = pvac_hip::ct_add(pk, a, b);
+        MUST(write_ct({ct_view(s)}) == slurp(bounty + "/sum.ct"), "bounty2 sum.ct bytes");
+    }
+
+    // full ct_mul with sigma (ops/arithmetic.hpp:47-106): pair 0 byte-identical to the reference
+    {
+        const Cipher x = read_ct(ref + "/pair0_x.ct")[0], y = read_ct(ref + "/pair0_y.ct")[0];
+        replay rs{read_u64(ref + "/pair0_mul_stream.u64")};
+        const Cipher m = pvac_hip::ct_mul(pk, x, y, std::ref(rs));
+        const Cipher r = read_ct(ref + "/pair0_mul.ct")[0];
+        MUST(rs.k == rs.s.size(), "ct_mul consumed %zu of %zu random words", rs.k, rs.s.size());
+        MUST(same_layers(ct_view(m), r) && same_edges(m, r, true), "ct_mul pair 0 (with sigma)");
+        MUST(write_ct({ct_view(m)}) == slurp(ref + "/pair0_mul.ct"), "ct_mul pair 0 .ct bytes");
+    }
+
+    // chain c_k = c_{k-1} * x_k (tests/test_main.cpp:289-295), weights and order, steps 1..3
+    {
+        const auto lay = [&](int k) {
+            const auto v = read_u64(ref + "/chain" + std::to_string(k) + "_layers.u64");
+            std::vector<mirror::Layer> L(v.size() / 6);
+            for (size_t i = 0; i < L.size(); ++i) {
+                L[i].rule = (mirror::RRule)v[6 * i];
+                L[i].pa = (uint32_t)v[6 * i + 1]; L[i].pb = (uint32_t)v[6 * i + 2];
+                L[i].seed.ztag = v[6 * i + 3]; L[i].seed.nonce.lo = v[6 * i + 4]; L[i].seed.nonce.hi = v[6 * i + 5];
+            }
+            return L;
+        };
+        Cipher cur = read_ct(ref + "/chain0.ct")[0];
+        for (int k = 1; k <= 3; ++k) {
+            const Cipher x = read_ct(ref + "/chain" + std::to_string(k) + "_x.ct")[0];
+            replay rs{read_u64(ref + "/chain" + std::to_string(k) + "_stream.u64")};
+            std::vector<Cipher> A{cur}, B{x};
+            const Cipher c = pvac_hip::ct_mul_batch(pk, A, B, false, std::ref(rs))[0];
+            const Cipher r = read_ct(ref + "/chain" + std::to_string(k) + ".ct")[0];
+            MUST(same_layers(ct_view(c), r) && same_edges(c, r, false), "chain step %d", k);
+            const auto full = lay(k);
+            MUST(c.L.size() == full.size(), "chain step %d layers", k);
+            for (size_t l = 0; l < full.size(); ++l) MUST(c.L[l].seed.ztag == full[l].seed.ztag, "ztag %zu", l);
+            cur = c;
+        }
+    }
+
+    // fp_binop through the adapter on the golden vectors (core/field.hpp:50-213)
+    {
+        const auto alo = read_u64(ref + "/fp_a_lo.u64"), ahi = read_u64(ref + "/fp_a_hi.u64");
+        const auto blo = read_u64(ref + "/fp_b_lo.u64"), bhi = read_u64(ref + "/fp_b_hi.u64");
+        const size_t n = alo.size();
+        std::vector<uint64_t> lo(n), hi(n);
+        const std::pair<int, const char*> ops[] = {{PVAC_FP_ADD, "add"}, {PVAC_FP_SUB, "sub"}, {PVAC_FP_MUL, "mul"}};
+        for (const auto& op : ops) {
+            eng.fp_binop(op.first, alo.data(), ahi.data(), blo.data(), bhi.data(), lo.data(), hi.data(), n);
+            MUST(lo == read_u64(ref + "/fp_" + op.second + "_lo.u64") && hi == read_u64(ref + "/fp_" + op.second + "_hi.u64"),
+                 "fp_%s", op.second);
+        }
+    }
+
+    std::printf("test_adapter: %d checks passed\n", g_checks);
+    return 0;
+}

@@ -1,0 +1,68 @@
+"""Multi-process sharding logic (pvac_hfhe_cppbyv_amd/shard.py) on world size 2 with gloo, CPU only.
+The GPU path uses the same code over RCCL (bench.py); shard invariance of the engine's results is
+checked on the GPU in tests/test_gpu_shard.py."""
+import os
+import socket
+
+import pytest
+
+from pvac_hfhe_cppbyv_amd.shard import exclusive_offsets, shard_range
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 1000, 1 << 20):
+        for w in (1, 2, 3, 8):
+            got = [shard_range(n, w, r) for r in range(w)]
+            assert sum(c for _, c in got) == n
+            pos = 0
+            for s, c in got:
+                assert s == pos
+                pos += c
+            assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_total, q):
+    import torch
+    import torch.distributed as dist
+    from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    start, count = shard_range(n_total, world, rank)
+    # stand-in per-pair output sizes keyed by the global pair index (what the engine returns)
+    sizes = [1190 + (g * 7919) % 53 for g in range(start, start + count)]
+    off, total, per = global_edge_offsets(sum(sizes))
+    slow = max_over_ranks(0.5 + rank)
+    q.put((rank, start, count, off, total, per, slow))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_global_offsets():
+    import torch.multiprocessing as mp
+    n_total = 1001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = [1190 + (g * 7919) % 53 for g in range(n_total)]
+    offs, total = exclusive_offsets([sum(full[s:s + c]) for _, s, c, *_ in res])
+    for (rank, s, c, off, tot, per, slow), want in zip(res, offs):
+        assert off == want                 # this shard's place in the global edge CSR
+        assert tot == total == sum(full)   # grand total agrees on every rank
+        assert slow == 1.5                 # max over ranks
+    assert res[0][1] == 0 and res[1][1] == res[0][2]
