@@ -24,16 +24,38 @@ __device__ __forceinline__ uint64_t make_meta(uint32_t layer, uint32_t idx, uint
     return (uint64_t)layer | ((uint64_t)(idx & 0xFFFFu) << 32) | ((uint64_t)(ch & 0xFFu) << 48);
 }
 
+// Wave64 inclusive prefix sum with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast
+// 15/31 across rows): six VALU ops, no LDS round trips (unlike __shfl_up's ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// OR over the 64 lanes of a wave (same DPP network; lane 63 ends with the total), uniform result
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t x) {
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+    return (uint64_t)wave_or_u32((uint32_t)v) | ((uint64_t)wave_or_u32((uint32_t)(v >> 32)) << 32);
+}
+
 // Workgroup-wide exclusive scan of one u32 per thread. `part` is LDS scratch of BS/64 words.
 template <int BS>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* part, uint32_t& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
+    const uint32_t x = wave_incl_scan_u32(v);
     if (lane == 63) part[wave] = x;
     __syncthreads();
     uint32_t base = 0, tot = 0;
@@ -101,6 +123,7 @@ constexpr uint32_t kFreshKeysMax = 1536;    // |A.L||B.L|B key slots
 constexpr uint32_t kFreshProdMax = 4096;    // |A.E||B.E| products
 constexpr uint32_t kFreshEdgesMax = 256;    // |A.E|, |B.E|
 constexpr uint32_t kFreshLayersMax = 64;    // |C.L| before compaction
+constexpr uint32_t kFreshThreads = 512;     // workgroup of the fresh kernel
 
 struct mul_fresh_args {
     pvac_ct_batch A, B, C;
@@ -118,7 +141,8 @@ struct mul_fresh_args {
     uint32_t ks_max, prod_max, na_max, nb_max, buckets_max, layers_max;
 };
 hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st);
-hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, int num_cus, hipStream_t st);
+// args_dev: device copy of `a` (the kernel reads its arguments from memory, see k_mul_fresh.hip)
+hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* args_dev, int num_cus, hipStream_t st);
 
 // ---- ct_mul, general path (k_mul_large.hip): multi-kernel, global scratch, one workgroup
 // per (A-layer, B-layer) product task. The host prepares one descriptor per large pair with

@@ -93,6 +93,58 @@ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
 
 __device__ __forceinline__ bool fp_nonzero(const fp& a) { return (a.lo | a.hi) != 0; }
 
+// ---- lazy products for sums ------------------------------------------------------------
+// For CANONICAL a, b (< 2^127) the first Mersenne fold of the 254-bit product already gives a
+// 128-bit x with x == a*b (mod p): z < 2^254, so (z mod 2^127) + (z >> 127) < 2^128. Sums of
+// such x are reduced once (fp_fold3_lazy), which skips the second fold and fp_from_words per
+// product. Equal mod p to the reference's fp_add chain of fp_mul results (field.hpp:50-56,
+// 209-213), which computes the exact sum mod p for canonical addends.
+__device__ __forceinline__ void fp_mul_fold1(const fp& a, const fp& b, uint64_t& x0, uint64_t& x1) {
+    uint64_t p00l, p00h, p01l, p01h, p10l, p10h, p11l, p11h;
+    mul_64x64(a.lo, b.lo, p00l, p00h);
+    mul_64x64(a.lo, b.hi, p01l, p01h);
+    mul_64x64(a.hi, b.lo, p10l, p10h);
+    mul_64x64(a.hi, b.hi, p11l, p11h);
+    uint64_t c1, c2;
+    uint64_t z1 = add_co(p00h, p01l, c1);
+    z1 = add_co(z1, p10l, c2);
+    const uint64_t k1 = c1 + c2;
+    uint64_t c3, c4, c5;
+    uint64_t z2 = add_co(p01h, p10h, c3);
+    z2 = add_co(z2, p11l, c4);
+    z2 = add_co(z2, k1, c5);
+    const uint64_t z3 = p11h + c3 + c4 + c5;   // < 2^62 for canonical inputs
+    const uint64_t h0 = (z1 >> 63) | (z2 << 1);
+    const uint64_t h1 = (z2 >> 63) | (z3 << 1);
+    uint64_t d0;
+    x0 = add_co(p00l, h0, d0);
+    x1 = (z1 & kM63) + h1 + d0;                // no carry out: x < 2^128
+}
+
+// 128-bit x -> 43/43/42-bit limbs; up to 2^21 of them sum in u64 limbs without overflow
+__device__ __forceinline__ void fp_split3_128(uint64_t x0, uint64_t x1, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
+    l0 = x0 & ((1ULL << 43) - 1);
+    l1 = ((x0 >> 43) | (x1 << 21)) & ((1ULL << 43) - 1);
+    l2 = x1 >> 22;
+}
+
+// (l0 + l1 * 2^43 + l2 * 2^86) mod p, canonical, for limb sums l < 2^64
+__device__ __forceinline__ fp fp_fold3_lazy(uint64_t l0, uint64_t l1, uint64_t l2) {
+    uint64_t c0, c1, c2;
+    const uint64_t w0 = add_co(l0, l1 << 43, c0);
+    uint64_t w1 = add_co(l1 >> 21, l2 << 22, c1);
+    w1 = add_co(w1, c0, c2);
+    const uint64_t w2 = (l2 >> 42) + c1 + c2;   // V < 2^151
+    const uint64_t top = (w1 >> 63) | (w2 << 1);
+    uint64_t d;
+    const uint64_t lo = add_co(w0, top, d);
+    const uint64_t hi = (w1 & kM63) + d;
+    return fp_from_words(lo, hi);
+}
+
+// canonical representative of any 128-bit word pair (fp_from_words, field.hpp:26-48)
+__device__ __forceinline__ fp fp_canon(uint64_t lo, uint64_t hi) { return fp_from_words(lo, hi); }
+
 // ---- exact multi-product accumulation for LDS atomics ----------------------------------
 // A canonical value v < 2^127 splits into three limbs of 43/42/42 bits. Up to 2^21 such
 // values summed limb-wise in u64 accumulators cannot overflow; fold_limbs recombines and

@@ -43,7 +43,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
         C.l_off[i] = capL;   // scanned in place afterwards
         C.e_off[i] = capE;
         small = keys <= kFreshKeysMax && prod <= kFreshProdMax && prod < nb_len && nA <= kFreshEdgesMax &&
-                nB <= kFreshEdgesMax && capL <= kFreshLayersMax;
+                nB <= kFreshEdgesMax && capL <= kFreshLayersMax &&
+                nb_table[prod < nb_len ? prod : 0] + prod + 3 <= 3 * keys;   // chains + key sums fit in LDS
         pair_class[i] = small ? PAIR_SMALL : PAIR_LARGE;
         if (small) {
             mk = (uint32_t)keys; mp = (uint32_t)prod; ma = (uint32_t)nA; mb = (uint32_t)nB;

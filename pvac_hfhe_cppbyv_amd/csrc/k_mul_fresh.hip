@@ -23,12 +23,29 @@
 //                        independent, no overflow below 2^21 addends). compact_layers is a
 //                        wave-wide bitmask closure over LDS-resident parent masks; edges are
 //                        staged in LDS at their emit positions and written out coalesced.
-#include <cstdlib>
-
 #include "common.hpp"
 #include "sha256.hpp"
 
 namespace pvhip {
+
+// Diagnostic build only (make diag -> lib/libpvac_hip_diag.so): wave 0 of every workgroup
+// accumulates s_memtime deltas per phase into a debug array; never touches kernel outputs.
+#ifdef PVAC_PHASE_STAMPS
+constexpr int kStampPhases = 12;
+__device__ unsigned long long g_fresh_stamps[4096 * kStampPhases];
+#define PHASE_STAMP(ph)                                                  \
+    do {                                                                 \
+        if (threadIdx.x == 0) {                                          \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+            st_acc_[ph] += now_ - st_last_;                              \
+            st_last_ = now_;                                             \
+        }                                                                \
+    } while (0)
+#else
+#define PHASE_STAMP(ph) \
+    do {                \
+    } while (0)
+#endif
 
 namespace {
 
@@ -67,7 +84,7 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
 // ---------------------------------------------------------------- aggregation + emit
 struct fresh_layout {
     // byte offsets into dynamic LDS
-    uint32_t acc, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
+    uint32_t acc, tkey, klist, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
@@ -77,6 +94,7 @@ __host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint
     uint32_t o = 0;
     L.acc = o;   o = align16(o + ks * 48u);           // 2 channels x 3 u64 limbs per key slot
     L.tkey = o;  o = align16(o + ks * 4u);
+    L.klist = o; o = align16(o + ks * 4u);            // compact list of existing keys
     L.a_w = o;   o = align16(o + na * 16u);
     L.a_inf = o; o = align16(o + na * 4u);
     L.b_w = o;   o = align16(o + nb * 16u);
@@ -92,15 +110,18 @@ __host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint
 enum : int { MF_PART = 0 /* <= 8 scan partials */, MF_INVALID = 8, MF_TOTAL = 9, MF_IDENT = 10,
              MF_KEEP = 12 /* u64 */, MF_WAVELP = 16 /* 8 x u64 */ };
 
-__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t lo = __shfl_xor((uint32_t)v, d, 64);
-        const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
-        v |= (uint64_t)lo | ((uint64_t)hi << 32);
-    }
-    return v;
+// Kernel arguments read through the constant address space: scalar loads (lgkmcnt only), so an
+// argument read never waits on outstanding vector-memory loads.
+using argp = const __attribute__((address_space(4))) mul_fresh_args*;
+
+__device__ __forceinline__ argp launder(uint64_t v) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return (argp)(((uint64_t)hi << 32) | lo);
 }
+__device__ __forceinline__ argp launder(argp p) { return launder((uint64_t)p); }
+
 
 // Per-pair header (workgroup-uniform). pr == kNoPair ends the persistent loop.
 constexpr uint64_t kNoPair = ~0ull;
@@ -108,52 +129,74 @@ struct fresh_hdr {
     uint64_t pr;
     uint32_t LA, LB, nA, nB;
     uint64_t aeo, beo, alo, blo, clo, ceo;
+    uint32_t nbk;        // libstdc++ bucket count after reserve(|A.E||B.E|)
+    uint64_t nb_magic;   // its fastmod64 multiplier
 };
 
-__device__ __forceinline__ uint64_t next_small(const mul_fresh_args& g, uint64_t from) {
-    for (uint64_t q = from; q < g.A.n; q += gridDim.x)
-        if (g.pair_class[q] == PAIR_SMALL) return q;
+// read-only tables seen through the constant address space: uniform-index reads become scalar
+// loads (lgkmcnt), which never wait behind the vector-memory prefetch of the next pair
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const T* p) {
+    return (const __attribute__((address_space(4))) T*)p;
+}
+
+__device__ __forceinline__ uint64_t next_small(argp g, uint64_t from) {
+    for (uint64_t q = from; q < g->A.n; q += gridDim.x)
+        if (cst(g->pair_class)[q] == PAIR_SMALL) return q;
     return kNoPair;
 }
 
-__device__ __forceinline__ fresh_hdr load_hdr(const mul_fresh_args& g, uint64_t pr) {
+__device__ __forceinline__ fresh_hdr load_hdr(argp g, uint64_t pr) {
     fresh_hdr h{};
     h.pr = pr;
     if (pr != kNoPair) {
-        h.LA = (uint32_t)g.A.l_cnt[pr]; h.LB = (uint32_t)g.B.l_cnt[pr];
-        h.nA = (uint32_t)g.A.e_cnt[pr]; h.nB = (uint32_t)g.B.e_cnt[pr];
-        h.aeo = g.A.e_off[pr]; h.beo = g.B.e_off[pr];
-        h.alo = g.A.l_off[pr]; h.blo = g.B.l_off[pr];
-        h.clo = g.C.l_off[pr]; h.ceo = g.C.e_off[pr];
+        h.LA = (uint32_t)cst(g->A.l_cnt)[pr]; h.LB = (uint32_t)cst(g->B.l_cnt)[pr];
+        h.nA = (uint32_t)cst(g->A.e_cnt)[pr]; h.nB = (uint32_t)cst(g->B.e_cnt)[pr];
+        h.aeo = cst(g->A.e_off)[pr]; h.beo = cst(g->B.e_off)[pr];
+        h.alo = cst(g->A.l_off)[pr]; h.blo = cst(g->B.l_off)[pr];
+        h.clo = cst(g->C.l_off)[pr]; h.ceo = cst(g->C.e_off)[pr];
+        const uint32_t n = h.nA * h.nB;
+        h.nbk = cst(g->nb_table)[n];
+        h.nb_magic = cst(g->nb_magic)[n];
     }
     return h;
 }
 
-// Next pair's inputs held in registers while the current pair is ordered and written:
-// thread t owns A edge t, B edge t and C layer t (nA, nB <= 256 <= BS, Lc <= 64).
+// The next pair's raw inputs ride in registers while the current pair is ordered and written:
+// thread t holds A edge t, B edge t and words 0..2 (rule, pa, pb) of input layer t. Nothing is
+// computed from them until stage_pair, so no wait is placed on the loads before then.
 struct fresh_pref {
-    uint64_t am, awl, awh, bm, bwl, bwh, pmv;
+    uint64_t am, al, ah, bm, bl, bh;
+    uint32_t rule, pa, pb;
 };
 
-template <int BS>
-__device__ __forceinline__ fresh_pref prefetch_pair(const mul_fresh_args& g, const fresh_hdr& h) {
+__device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h) {
+    // branch-free: every lane loads a clamped (valid) index, so no divergent block ends in a
+    // wait; lanes past the counts simply ignore what they loaded
     fresh_pref f{};
     const uint32_t t = threadIdx.x;
     if (h.pr == kNoPair) return f;
-    if (t < h.nA) { f.am = g.A.meta[h.aeo + t]; f.awl = g.A.w_lo[h.aeo + t]; f.awh = g.A.w_hi[h.aeo + t]; }
-    if (t < h.nB) { f.bm = g.B.meta[h.beo + t]; f.bwl = g.B.w_lo[h.beo + t]; f.bwh = g.B.w_hi[h.beo + t]; }
-    const uint32_t base = h.LA + h.LB, Lc = base + h.LA * h.LB;
-    if (t < base) {   // rule/pa/pb of the input layers (compact_layers parents)
-        const pvac_layer& x = t < h.LA ? g.A.layers[h.alo + t] : g.B.layers[h.blo + (t - h.LA)];
-        f.pmv = ((uint64_t)x.rule << 63) | ((uint64_t)x.pb << 32) | x.pa;
-    } else if (t < Lc) {
-        f.pmv = 0;
+    if (h.nA) {
+        const uint64_t e = h.aeo + min(t, h.nA - 1);
+        f.am = g->A.meta[e]; f.al = g->A.w_lo[e]; f.ah = g->A.w_hi[e];
+    }
+    if (h.nB) {
+        const uint64_t e = h.beo + min(t, h.nB - 1);
+        f.bm = g->B.meta[e]; f.bl = g->B.w_lo[e]; f.bh = g->B.w_hi[e];
+    }
+    const uint32_t nl = h.LA + h.LB;
+    if (nl) {
+        const uint32_t l = min(t, nl - 1);
+        const pvac_layer* rec = l < h.LA ? g->A.layers + h.alo + l : g->B.layers + h.blo + (l - h.LA);
+        const uint3 w3 = *(const uint3*)rec;
+        f.rule = w3.x; f.pa = w3.y; f.pb = w3.z;
     }
     return f;
 }
 
-// registers -> LDS staging of one pair; flags invalid references in misc[MF_INVALID]
-template <int BS>
+// registers -> staged operands: validated, canonical weights (products depend only on w mod p;
+// canonical operands let the lazy product skip a fold), packed (idx, layer, ch), and the
+// compact_layers parent mask of every C layer. Flags invalid references in misc[MF_INVALID].
 __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr& h, uint32_t Bm, ulonglong2* a_w,
                                            uint32_t* a_inf, ulonglong2* b_w, uint32_t* b_inf, uint64_t* pm,
                                            uint32_t* misc) {
@@ -162,41 +205,51 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
     if (t < h.nA) {
         const uint32_t la = meta_layer(f.am), idx = meta_idx(f.am), ch = meta_ch(f.am);
         if (la >= h.LA || idx >= Bm || ch > 1) misc[MF_INVALID] = 1;
-        a_w[t] = make_ulonglong2(f.awl, f.awh);
+        const fp w = fp_canon(f.al, f.ah);
+        a_w[t] = make_ulonglong2(w.lo, w.hi);
         a_inf[t] = idx | ((la & 0x7FFFu) << 16) | (ch << 31);
     }
     if (t < h.nB) {
         const uint32_t lb = meta_layer(f.bm), idx = meta_idx(f.bm), ch = meta_ch(f.bm);
         if (lb >= h.LB || idx >= Bm || ch > 1) misc[MF_INVALID] = 1;
-        b_w[t] = make_ulonglong2(f.bwl, f.bwh);
+        const fp w = fp_canon(f.bl, f.bh);
+        b_w[t] = make_ulonglong2(w.lo, w.hi);
         b_inf[t] = idx | ((lb & 0x7FFFu) << 16) | (ch << 31);
     }
     const uint32_t base = h.LA + h.LB, Lc = base + h.LA * h.LB;
+    uint32_t rule = f.rule;
+    asm volatile("" : "+v"(rule));   // keep the compare here: hoisted, it waits on the prefetch
     if (t < Lc) {
         uint64_t m = 0;
         if (t < base) {
-            if (f.pmv >> 63) {   // PROD: parents, B's shifted by |A.L| (arithmetic.hpp:54-57)
+            if (rule == 1u) {   // PROD: parents, B's shifted by |A.L| (arithmetic.hpp:54-57)
                 const uint32_t off = t < h.LA ? 0u : h.LA;
-                const uint32_t pa = (uint32_t)f.pmv + off, pb = (uint32_t)(f.pmv >> 32) + off;
+                const uint32_t pa = f.pa + off, pb = f.pb + off;
                 m = (pa < Lc ? 1ull << pa : 0ull) | (pb < Lc ? 1ull << pb : 0ull);
             }
         } else {
-            const uint32_t lp = t - base;
-            m = (1ull << (lp / h.LB)) | (1ull << (h.LA + lp % h.LB));
+            const uint32_t lp = t - base;   // < 64: float quotient is exact after floor
+            const uint32_t la = (uint32_t)__float2uint_rd(((float)lp + 0.5f) / (float)h.LB);
+            m = (1ull << la) | (1ull << (h.LA + lp - la * h.LB));
         }
         pm[t] = m;
     }
 }
 
 template <int BS, int MINW>
-__global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(mul_fresh_args g, fresh_layout Ls) {
-    constexpr int FS = kFreshKeysMax / BS;               // key slots owned per thread
+__global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args* __restrict__ gp, fresh_layout Ls) {
+    constexpr int KI = kFreshKeysMax / BS;               // compact keys owned per thread (3)
     constexpr int NW = BS / 64;
-    static_assert(FS * BS == (int)kFreshKeysMax && BS >= (int)kFreshEdgesMax && NW <= 8, "fresh geometry");
+    static_assert(BS == (int)kFreshThreads && BS >= (int)kFreshEdgesMax && NW <= 8, "fresh geometry");
+    // Arguments live in a device buffer; the pointer is laundered after every barrier so the
+    // compiler re-reads fields from the scalar cache on use instead of pinning ~60 SGPRs of
+    // pointers for the whole loop (which spilled into VGPRs and scratch).
+    argp gq = launder((uint64_t)gp);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     unsigned long long* acc = (unsigned long long*)(lds + Ls.acc);
-    uint32_t* accw = (uint32_t*)(lds + Ls.acc);           // u32 view: heads | G | nxt, then staging
+    uint32_t* accw = (uint32_t*)(lds + Ls.acc);           // u32 view: heads | G | nxt | key sums
     uint32_t* tkey = (uint32_t*)(lds + Ls.tkey);
+    uint32_t* klist = (uint32_t*)(lds + Ls.klist);
     ulonglong2* a_w = (ulonglong2*)(lds + Ls.a_w);
     uint32_t* a_inf = (uint32_t*)(lds + Ls.a_inf);
     ulonglong2* b_w = (ulonglong2*)(lds + Ls.b_w);
@@ -208,46 +261,52 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(mul_fresh_args g, fre
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const uint32_t Bm = g.Bm;
-    const uint32_t acc_vec = g.ks_max * 3u;               // 16-byte vectors in the accumulator region
+    const uint32_t Bm = gq->Bm;
+    const float inv_b = 1.0f / (float)Bm;
 
     // one-time clear: accumulators 0, first-insert times INF
-    for (uint32_t w = tid; w < acc_vec; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
-    for (uint32_t s = tid; s < g.ks_max; s += BS) tkey[s] = kTInf;
+    for (uint32_t w = tid; w < gq->ks_max * 3u; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
+    for (uint32_t s = tid; s < gq->ks_max; s += BS) tkey[s] = kTInf;
     if (tid < 32) misc[tid] = 0;
     __syncthreads();
 
-    fresh_hdr cur = load_hdr(g, next_small(g, blockIdx.x));
-    stage_pair<BS>(prefetch_pair<BS>(g, cur), cur, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+#ifdef PVAC_PHASE_STAMPS
+    unsigned long long st_acc_[kStampPhases] = {};
+    unsigned long long st_last_ = __builtin_amdgcn_s_memtime();
+#endif
+    fresh_hdr cur = load_hdr(gq, next_small(gq, blockIdx.x));
+    stage_pair(prefetch_pair(gq, cur), cur, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
     __syncthreads();
+    PHASE_STAMP(0);
 
     while (cur.pr != kNoPair) {
-        const fresh_hdr nxt = load_hdr(g, next_small(g, cur.pr + gridDim.x));
+        gq = launder(gq);
+        const fresh_hdr nxt = load_hdr(gq, next_small(gq, cur.pr + gridDim.x));
         const uint64_t pr = cur.pr;
         const uint32_t LA = cur.LA, LB = cur.LB, nA = cur.nA, nB = cur.nB;
         const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
         const uint32_t base = LA + LB, Lc = base + LP;
-        const uint32_t nbk = g.nb_table[n];
-        const fastmod64 fm{nbk, g.nb_magic[n]};
-        const uint64_t clo = cur.clo, ceo = cur.ceo;
+        const uint32_t nbk = cur.nbk;
+        const uint32_t chain_words = nbk + n + KS;               // heads | G | nxt
+        const uint32_t sum_base = (chain_words + 3u) & ~3u;      // key sums: 8 words per key
 
         if (misc[MF_INVALID]) {   // invalid references: reject the pair (reference behaviour is UB)
             __syncthreads();
             if (tid == 0) {
-                g.pair_status[pr] = 2;
-                g.C.l_cnt[pr] = 0;
-                g.C.e_cnt[pr] = 0;
+                gq->pair_status[pr] = 2;
+                gq->C.l_cnt[pr] = 0;
+                gq->C.e_cnt[pr] = 0;
                 misc[MF_INVALID] = 0;
             }
             __syncthreads();
-            stage_pair<BS>(prefetch_pair<BS>(g, nxt), nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+            stage_pair(prefetch_pair(gq, nxt), nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
             __syncthreads();
             cur = nxt;
             continue;
         }
 
         // ---- S1: all |A.E||B.E| products into LDS limb accumulators + first-insert times.
-        //      Thread (j, g0) keeps B edge j in registers and walks A edges g0, g0 + G, ...
+        //      Thread (j, g0) keeps B edge j in registers and walks A edges g0 + k*groups.
         if (n) {
             const uint32_t groups = BS / nB;
             const uint32_t j = (uint32_t)tid % nB, g0 = (uint32_t)tid / nB;
@@ -259,14 +318,14 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(mul_fresh_args g, fre
                 for (uint32_t i = g0; i < nA; i += groups) {
                     const uint32_t ai = a_inf[i];
                     const ulonglong2 x = a_w[i];
-                    const uint32_t la = (ai >> 16) & 0x7FFFu;
+                    const uint32_t lp = ((ai >> 16) & 0x7FFFu) * LB + lb;
                     uint32_t r = (ai & 0xFFFFu) + ib;
                     r = r >= Bm ? r - Bm : r;
-                    const uint32_t s = (la * LB + lb) * Bm + r;
+                    const uint32_t s = lp * Bm + r;
                     const uint32_t chn = (ai ^ bj) >> 31;   // 0 = P (same sign), 1 = M
-                    const fp prod = fp_mul(fp{x.x, x.y}, yb);
-                    uint64_t l0, l1, l2;
-                    fp_split3(prod, l0, l1, l2);
+                    uint64_t x0, x1, l0, l1, l2;
+                    fp_mul_fold1(fp{x.x, x.y}, yb, x0, x1);
+                    fp_split3_128(x0, x1, l0, l1, l2);
                     unsigned long long* q = acc + (size_t)(s * 2 + chn) * 3;
                     atomicAdd(q + 0, (unsigned long long)l0);
                     atomicAdd(q + 1, (unsigned long long)l1);
@@ -276,76 +335,101 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(mul_fresh_args g, fre
             }
         }
         __syncthreads();
-        // next pair's inputs: loads in flight across S2a..S5, staged after the copy-out
-        const fresh_pref pf = prefetch_pair<BS>(g, nxt);
+        gq = launder(gq);
+        PHASE_STAMP(1);
+        // next pair's raw inputs: loads in flight until stage_pair at the end of this iteration
+        const fresh_pref pf = prefetch_pair(gq, nxt);
 
-        // ---- S2a: fold owned slots into registers, clear their limbs, bucket of each key
-        fp sumP[FS], sumM[FS];
-        uint32_t tk[FS], eb[FS], bk[FS];
+        // ---- S2: compact the existing keys (slot order) into a dense list, so every thread owns
+        //      <= KI keys with no divergence on key existence
+        uint32_t nkeys;
+        {
+            constexpr uint32_t SPT = kFreshKeysMax / BS;             // slots per thread (3)
+            const uint32_t s0 = (uint32_t)tid * SPT;
+            uint32_t cnt = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < SPT; ++u) cnt += (s0 + u < KS && tkey[s0 + u] != kTInf) ? 1u : 0u;
+            uint32_t at = block_exclusive_scan<BS>(cnt, misc + MF_PART, nkeys);
+#pragma unroll
+            for (uint32_t u = 0; u < SPT; ++u)
+                if (s0 + u < KS && tkey[s0 + u] != kTInf) klist[at++] = s0 + u;
+        }
+        __syncthreads();
+
+        // ---- S2a: fold each key's limbs, clear them, hash the key to its libstdc++ bucket
+        const fastmod64 fm{nbk, cur.nb_magic};
+        fp sumP[KI], sumM[KI];
+        uint32_t ks[KI], kt[KI], eb[KI], bk[KI];
         uint64_t myor = 0;
 #pragma unroll
-        for (int k = 0; k < FS; ++k) {
-            const uint32_t s = tid + k * BS;
-            tk[k] = kTInf;
-            eb[k] = 0;
-            bk[k] = 0;
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t q_i = tid + (uint32_t)k * BS;
+            ks[k] = 0; kt[k] = 0; eb[k] = 0; bk[k] = 0;
             sumP[k] = fp{0, 0};
             sumM[k] = fp{0, 0};
-            if (s < KS) {
-                tk[k] = tkey[s];
-                if (tk[k] != kTInf) {
-                    unsigned long long* q = acc + (size_t)s * 6;
-                    sumP[k] = fp_fold3(q[0], q[1], q[2]);
-                    sumM[k] = fp_fold3(q[3], q[4], q[5]);
-                    eb[k] = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
-                    q[0] = 0; q[1] = 0; q[2] = 0; q[3] = 0; q[4] = 0; q[5] = 0;
-                    const uint32_t lp = s / Bm, idx = s - lp * Bm;
-                    const uint64_t key = ((uint64_t)lp << 32) | idx;
-                    bk[k] = (uint32_t)fmod64(key * kGolden, fm);   // std::hash -> bucket
-                    if (eb[k]) myor |= 1ull << lp;
-                }
+            if (q_i < nkeys) {
+                const uint32_t s = klist[q_i];
+                ks[k] = s;
+                kt[k] = tkey[s];
+                // s / B for s < 1536: the float quotient of s + 1/2 is exact after floor
+                const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), r = s - lp * Bm;
+                unsigned long long* q = acc + (size_t)s * 6;
+                sumP[k] = fp_fold3_lazy(q[0], q[1], q[2]);
+                sumM[k] = fp_fold3_lazy(q[3], q[4], q[5]);
+                q[0] = 0; q[1] = 0; q[2] = 0; q[3] = 0; q[4] = 0; q[5] = 0;
+                eb[k] = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
+                const uint64_t key = ((uint64_t)lp << 32) | r;
+                bk[k] = (uint32_t)fmod64(key * kGolden, fm);   // std::hash -> bucket
+                if (eb[k]) myor |= 1ull << lp;
             }
         }
         myor = wave_or_u64(myor);
         if (lane == 0) wave_lp[wave] = myor;
-        __syncthreads();
+        __syncthreads();   // every limb is read and zeroed: chains and key sums may use the region
+        gq = launder(gq);
+        PHASE_STAMP(2);
 
-        // ---- S2b: bucket chains over the (now all-zero) accumulator region
+        // ---- S2b: key sums to LDS (compact, beside the chains), bucket chains
         uint32_t* heads = accw;
         uint32_t* G = heads + nbk;
         uint32_t* nxtl = G + n;
+        ulonglong2* ksum = (ulonglong2*)(accw + sum_base);   // [2 q] = P, [2 q + 1] = M
 #pragma unroll
-        for (int k = 0; k < FS; ++k) {
-            if (tk[k] != kTInf) {
-                const uint32_t s = tid + k * BS;
-                const uint32_t prev = atomicExch(&heads[bk[k]], s + 1);
-                nxtl[s] = prev | (eb[k] << 30);
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t q_i = tid + (uint32_t)k * BS;
+            if (q_i < nkeys) {
+                ksum[2 * q_i] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
+                ksum[2 * q_i + 1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
+                const uint32_t prev = atomicExch(&heads[bk[k]], ks[k] + 1);
+                nxtl[ks[k]] = prev | (eb[k] << 30);
             }
         }
         __syncthreads();
+        gq = launder(gq);
+        PHASE_STAMP(3);
 
         // ---- S2c: walk chains -> bucket first-insert time, rank inside the bucket, group sizes;
         //      wave 0 then runs compact_layers (encrypt.hpp:73-104) as a bitmask closure
-        uint32_t tb[FS], within[FS];
+        uint32_t tb[KI], within[KI];
 #pragma unroll
-        for (int k = 0; k < FS; ++k) {
+        for (int k = 0; k < KI; ++k) {
             tb[k] = 0;
             within[k] = 0;
-            if (tk[k] != kTInf) {
-                uint32_t q = heads[bk[k]], tmin = tk[k], w = 0, E = 0;
+            if (tid + (uint32_t)k * BS < nkeys) {
+                uint32_t q = heads[bk[k]], tmin = kt[k], w = 0, E = 0;
                 while (q) {
                     const uint32_t s2 = q - 1;
                     const uint32_t t2 = tkey[s2];
                     const uint32_t nx = nxtl[s2];
                     const uint32_t e2 = __popc(nx >> 30);
                     tmin = t2 < tmin ? t2 : tmin;
-                    w += t2 > tk[k] ? e2 : 0u;
+                    w += t2 > kt[k] ? e2 : 0u;
                     E += e2;
                     q = nx & 0x3FFFFFFFu;
                 }
                 tb[k] = tmin;
                 within[k] = w;
-                if (tmin == tk[k]) G[tmin] = E;
+                if (tmin == kt[k]) G[tmin] = E;
             }
         }
         if (wave == 0) {
@@ -369,6 +453,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(mul_fresh_args g, fre
             }
         }
         __syncthreads();
+        gq = launder(gq);
+        PHASE_STAMP(4);
 
         // ---- S3: exclusive SUFFIX scan of G over t in [0, n): emit offset of each bucket group
         {
@@ -387,100 +473,99 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(mul_fresh_args g, fre
             if (tid == 0) misc[MF_TOTAL] = total;
         }
         __syncthreads();
+        gq = launder(gq);
+        PHASE_STAMP(5);
 
-        // ---- S4: emit positions into registers; reset first-insert times
+        // ---- S4: emit positions; write every key's edges straight to its output slots
         const uint32_t total = misc[MF_TOTAL];
         // guard_budget (encrypt.hpp:106-111): above edge_budget the reference runs compact_edges,
         // whose output is (layer, idx, P before M) order; product edges are already unique per
         // (layer, idx, ch) and nonzero, so it only re-orders them.
-        const bool canonical = (g.flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > g.edge_budget;
-        uint32_t pos[FS], hpos[FS];
+        const bool canonical = (gq->flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > gq->edge_budget;
+        const uint64_t ceo = cur.ceo;
         uint32_t rowbase = 0;
 #pragma unroll
-        for (int k = 0; k < FS; ++k) {
-            hpos[k] = G[tb[k]] + within[k];
-            if (canonical) {   // workgroup-uniform: slot order s = tid + k*BS
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t q_i = tid + (uint32_t)k * BS;
+            const bool own = q_i < nkeys;
+            const uint32_t hp = own ? G[tb[k]] + within[k] : 0u;
+            uint32_t p = hp;
+            if (canonical) {   // workgroup-uniform: compact keys are in slot order, row k = keys k*BS..
                 uint32_t rowtot;
-                pos[k] = rowbase + block_exclusive_scan<BS>(__popc(eb[k]), misc + MF_PART, rowtot);
+                p = rowbase + block_exclusive_scan<BS>(__popc(eb[k]), misc + MF_PART, rowtot);
                 rowbase += rowtot;
-            } else {
-                pos[k] = hpos[k];
             }
-            if (tk[k] != kTInf) tkey[tid + k * BS] = kTInf;
-        }
-        __syncthreads();
-
-        // ---- S4b: stage edge records at their emit positions (over heads/G/nxt, now dead)
-        uint64_t* st_meta = (uint64_t*)accw;
-        uint64_t* st_lo = st_meta + total;
-        uint64_t* st_hi = st_lo + total;
-#pragma unroll
-        for (int k = 0; k < FS; ++k) {
+            if (own) tkey[ks[k]] = kTInf;
             if (eb[k]) {
-                const uint32_t s = tid + k * BS;
-                const uint32_t lp = s / Bm, idx = s - lp * Bm;
+                const uint32_t s = ks[k];
+                const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), idx = s - lp * Bm;
                 const uint32_t lid = remap[base + lp];
-                uint32_t p = pos[k];
-                if (canonical && g.salt_pos) {   // salts are drawn in hash order (arithmetic.hpp:90-101)
-                    g.salt_pos[ceo + p] = hpos[k];
-                    if (eb[k] == 3u) g.salt_pos[ceo + p + 1] = hpos[k] + 1;
-                }
+                uint32_t* sp = gq->salt_pos;
                 if (eb[k] & 1u) {
-                    st_meta[p] = make_meta(lid, idx, 0);
-                    st_lo[p] = sumP[k].lo;
-                    st_hi[p] = sumP[k].hi;
+                    const ulonglong2 w = ksum[2 * q_i];
+                    gq->C.meta[ceo + p] = make_meta(lid, idx, 0);
+                    gq->C.w_lo[ceo + p] = w.x;
+                    gq->C.w_hi[ceo + p] = w.y;
+                    if (sp) sp[ceo + p] = hp;   // salts are drawn in hash order (arithmetic.hpp:90-101)
                     ++p;
                 }
                 if (eb[k] & 2u) {
-                    st_meta[p] = make_meta(lid, idx, 1);
-                    st_lo[p] = sumM[k].lo;
-                    st_hi[p] = sumM[k].hi;
+                    const ulonglong2 w = ksum[2 * q_i + 1];
+                    gq->C.meta[ceo + p] = make_meta(lid, idx, 1);
+                    gq->C.w_lo[ceo + p] = w.x;
+                    gq->C.w_hi[ceo + p] = w.y;
+                    if (sp) sp[ceo + p] = hp + (eb[k] & 1u);
                 }
             }
-        }
-        __syncthreads();
-
-        // ---- S5: coalesced copy-out, layer compaction fix-up, counts
-        for (uint32_t t = tid; t < total; t += BS) {
-            g.C.meta[ceo + t] = st_meta[t];
-            g.C.w_lo[ceo + t] = st_lo[t];
-            g.C.w_hi[ceo + t] = st_hi[t];
-            if (g.salt_pos && !canonical) g.salt_pos[ceo + t] = t;
         }
         const uint64_t keep = *(const uint64_t*)(misc + MF_KEEP);
         if (!misc[MF_IDENT] && wave == 1) {
             // k_mul_layers_fresh wrote identity placement; compact in place (remap[l] <= l, and
             // every lane of this wave loads before any lane stores)
             const uint32_t l = lane;
+            const uint64_t clo = cur.clo;
             pvac_layer y{};
-            if (l < Lc) y = g.C.layers[clo + l];
+            if (l < Lc) y = gq->C.layers[clo + l];
             if (l < Lc && ((keep >> l) & 1ull)) {
                 if (y.rule == 1) {
                     y.pa = y.pa < Lc ? remap[y.pa] : kTInf;
                     y.pb = y.pb < Lc ? remap[y.pb] : kTInf;
                 }
-                g.C.layers[clo + remap[l]] = y;
+                gq->C.layers[clo + remap[l]] = y;
             }
         }
         if (tid == 0) {
-            g.C.e_cnt[pr] = total;
-            g.C.l_cnt[pr] = (uint64_t)__popcll(keep);
-            g.pair_status[pr] = canonical ? 1 : 0;
+            gq->C.e_cnt[pr] = total;
+            gq->C.l_cnt[pr] = (uint64_t)__popcll(keep);
+            gq->pair_status[pr] = canonical ? 1 : 0;
         }
         __syncthreads();
-        // ---- clear what this pair dirtied (staging / chains), stage the next pair
+        gq = launder(gq);
+        PHASE_STAMP(6);
+        // ---- clear chains and key sums for the next pair, stage the next pair
         {
-            const uint32_t words = max(6u * total, nbk + n + KS);
-            const uint32_t vecs = (words + 3u) >> 2;
+            const uint32_t vecs = (sum_base + 8u * nkeys + 3u) >> 2;
             for (uint32_t w = tid; w < vecs; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
         }
-        stage_pair<BS>(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
         __syncthreads();
+        PHASE_STAMP(9);
         cur = nxt;
     }
+#ifdef PVAC_PHASE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 4096)
+        for (int p = 0; p < kStampPhases; ++p) g_fresh_stamps[blockIdx.x * kStampPhases + p] = st_acc_[p];
+#endif
 }
 
 }  // namespace
+
+#ifdef PVAC_PHASE_STAMPS
+extern "C" int pvac_hip_diag_fresh_stamps(unsigned long long* host, size_t n) {
+    if (n > sizeof(g_fresh_stamps) / 8) n = sizeof(g_fresh_stamps) / 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fresh_stamps), n * 8) == hipSuccess ? 0 : -5;
+}
+#endif
 
 hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st) {
     if (!a.A.n) return hipSuccess;
@@ -489,26 +574,22 @@ hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, int num_cus, hipStream_t st) {
+hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* args_dev, int num_cus, hipStream_t st) {
     if (!a.A.n) return hipSuccess;
     if (a.ks_max > kFreshKeysMax || a.layers_max > kFreshLayersMax || a.na_max > kFreshEdgesMax ||
         a.nb_max > kFreshEdgesMax)
         return hipErrorInvalidValue;
     const fresh_layout L = fresh_lds(a.ks_max, a.na_max, a.nb_max);
-    // chains (heads | G | nxt) and the staged edges must fit inside the accumulator region
-    if ((uint64_t)(a.buckets_max + a.prod_max + a.ks_max) > (uint64_t)a.ks_max * 12u) return hipErrorInvalidValue;
+    // chains (heads | G | nxt) and the key sums (8 words per key) share the accumulator region
+    // (the plan routes pairs that would not fit to the general path)
+    if ((uint64_t)(a.buckets_max + a.prod_max + a.ks_max + 3u) + 8ull * a.ks_max > (uint64_t)a.ks_max * 12u)
+        return hipErrorInvalidValue;
     if (L.total > 160u * 1024u) return hipErrorInvalidValue;
     const int per_cu = L.total <= 80u * 1024u ? 2 : 1;
     uint64_t blocks = (uint64_t)num_cus * per_cu;
     if (blocks > a.A.n) blocks = a.A.n;
-    static const int threads = [] {
-        const char* e = std::getenv("PVAC_FRESH_THREADS");   // tuning knob; results are identical
-        return e && std::atoi(e) == 256 ? 256 : 512;
-    }();
-    if (threads == 256)
-        hipLaunchKernelGGL((k_ct_mul_fresh<256, 2>), dim3((unsigned)blocks), dim3(256), L.total, st, a, L);
-    else
-        hipLaunchKernelGGL((k_ct_mul_fresh<512, 4>), dim3((unsigned)blocks), dim3(512), L.total, st, a, L);
+    hipLaunchKernelGGL((k_ct_mul_fresh<kFreshThreads, 4>), dim3((unsigned)blocks), dim3(kFreshThreads), L.total, st,
+                       args_dev, L);
     return hipGetLastError();
 }
 

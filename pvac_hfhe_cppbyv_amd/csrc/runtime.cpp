@@ -55,6 +55,8 @@ struct pvac_hip_ctx {
     size_t arena_words = 0;
     uint32_t* salt_pos = nullptr;
     size_t salt_cap = 0;
+    mul_fresh_args* fresh_args = nullptr;   // device copy of the fresh kernel's arguments
+    mul_fresh_args fresh_args_host{};
     uint64_t* scan_scratch = nullptr;
     size_t scan_cap = 0;
     plan_stats* stats = nullptr;
@@ -296,6 +298,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->desc_dev);
     hipFree(c->arena);
     hipFree(c->salt_pos);
+    hipFree(c->fresh_args);
     hipFree(c->scan_scratch);
     hipFree(c->stats);
     hipFree(c->totals);
@@ -531,8 +534,16 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
             hipError_t e = launch_mul_layers_fresh(a, c->stream);
             if (e != hipSuccess) return hip_fail(c, e, "mul_layers_fresh");
         }
+        if (!c->fresh_args) {
+            hipError_t ea = hipMalloc(&c->fresh_args, sizeof(mul_fresh_args));
+            if (ea != hipSuccess) return hip_fail(c, ea, "alloc fresh args");
+        }
+        // stream-ordered copy from the ctx's host mirror (kept alive until the next exec)
+        c->fresh_args_host = a;
+        hipError_t e = hipMemcpyAsync(c->fresh_args, &c->fresh_args_host, sizeof a, hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "upload fresh args");
         scoped_timer t(c, "ct_mul_fresh");
-        hipError_t e = launch_ct_mul_fresh(a, c->num_cus, c->stream);
+        e = launch_ct_mul_fresh(a, c->fresh_args, c->num_cus, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "ct_mul_fresh");
     }
     if (plan->n_large) {

@@ -33,3 +33,17 @@ for p in "${passes[@]}"; do
   fi
 done
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.json" && cat "$OUT/summary.json"
+# traffic record for bench.py's roofline.traffic (same pairs / edges-per-layer as the bench run)
+python3 - "$OUT/summary.json" "$OUT/pmc_ct_mul_fresh.json" "$@" <<'PY'
+import json, sys
+summ = json.load(open(sys.argv[1]))
+k = summ.get("k_ct_mul_fresh")
+args = sys.argv[3:]
+pairs = int(args[args.index("--pairs") + 1]) if "--pairs" in args else 1 << 20
+epl = int(args[args.index("--epl") + 1]) if "--epl" in args else 20
+if k and "hbm_bytes_per_launch" in k:
+    json.dump({"pairs": pairs, "epl": epl, "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
+               "hbm_read_bytes": k["hbm_read_bytes_corrected"], "hbm_write_bytes": k["hbm_write_bytes"],
+               "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) / WRITE_SIZE, "
+                         "mean per dispatch; tools/prof_pmc.sh"}, open(sys.argv[2], "w"), indent=1)
+PY
