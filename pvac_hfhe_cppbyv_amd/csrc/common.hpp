@@ -125,8 +125,21 @@ constexpr uint32_t kFreshEdgesMax = 256;    // |A.E|, |B.E|
 constexpr uint32_t kFreshLayersMax = 64;    // |C.L| before compaction
 constexpr uint32_t kFreshThreads = 512;     // workgroup of the fresh kernel
 
+// One 64-byte header record per pair (written by k_mul_layers_fresh, read by k_ct_mul_fresh with
+// a single scalar load): every per-pair field the aggregation kernel needs, in one cache line.
+struct __attribute__((aligned(64))) fresh_rec {
+    uint64_t aeo, beo, ceo;      // edge offsets of A, B, C
+    uint64_t alo, blo, clo;      // layer offsets
+    uint64_t nb_magic;           // fastmod64 multiplier of nbk
+    uint32_t shape;              // nA | nB << 16   (each <= kFreshEdgesMax)
+    uint16_t nbk;                // libstdc++ bucket count after reserve(nA nB); 0 = not a fresh pair
+    uint8_t LA, LB;
+};
+static_assert(sizeof(fresh_rec) == 64, "fresh_rec is one cache line");
+
 struct mul_fresh_args {
     pvac_ct_batch A, B, C;
+    fresh_rec* recs;             // per pair, filled by k_mul_layers_fresh
     const uint64_t* nonces;
     const uint8_t* pair_class;
     uint32_t* pair_status;       // 0 = reference order, 1 = canonical order, 2 = rejected (bad refs)

@@ -57,9 +57,24 @@ constexpr int kLayBlock = 128;
 
 __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g) {
     const uint64_t pr = (uint64_t)blockIdx.x * kLayBlock + threadIdx.x;
-    if (pr >= g.A.n || g.pair_class[pr] != PAIR_SMALL) return;
+    if (pr >= g.A.n) return;
+    fresh_rec rec{};
+    if (g.pair_class[pr] != PAIR_SMALL) {   // nbk = 0: the aggregation kernel skips the pair
+        g.recs[pr] = rec;
+        return;
+    }
     const uint32_t LA = (uint32_t)g.A.l_cnt[pr], LB = (uint32_t)g.B.l_cnt[pr];
     const uint64_t alo = g.A.l_off[pr], blo = g.B.l_off[pr], clo = g.C.l_off[pr];
+    {
+        const uint32_t nA = (uint32_t)g.A.e_cnt[pr], nB = (uint32_t)g.B.e_cnt[pr];
+        rec.aeo = g.A.e_off[pr]; rec.beo = g.B.e_off[pr]; rec.ceo = g.C.e_off[pr];
+        rec.alo = alo; rec.blo = blo; rec.clo = clo;
+        rec.nb_magic = g.nb_magic[nA * nB];
+        rec.shape = nA | (nB << 16);
+        rec.nbk = (uint16_t)g.nb_table[nA * nB];
+        rec.LA = (uint8_t)LA; rec.LB = (uint8_t)LB;
+        g.recs[pr] = rec;
+    }
     for (uint32_t l = 0; l < LA; ++l) g.C.layers[clo + l] = g.A.layers[alo + l];
     for (uint32_t l = 0; l < LB; ++l) {
         pvac_layer y = g.B.layers[blo + l];
@@ -133,16 +148,14 @@ struct fresh_hdr {
     uint64_t nb_magic;   // its fastmod64 multiplier
 };
 
-// read-only tables seen through the constant address space: uniform-index reads become scalar
-// loads (lgkmcnt), which never wait behind the vector-memory prefetch of the next pair
-template <class T>
-__device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const T* p) {
-    return (const __attribute__((address_space(4))) T*)p;
-}
+// Header records are read through the constant address space: uniform-index reads become scalar
+// loads (lgkmcnt), which never wait behind the vector-memory prefetch of the next pair.
+using recp = const __attribute__((address_space(4))) fresh_rec*;
 
 __device__ __forceinline__ uint64_t next_small(argp g, uint64_t from) {
+    const recp R = (recp)g->recs;
     for (uint64_t q = from; q < g->A.n; q += gridDim.x)
-        if (cst(g->pair_class)[q] == PAIR_SMALL) return q;
+        if (R[q].nbk) return q;
     return kNoPair;
 }
 
@@ -150,14 +163,13 @@ __device__ __forceinline__ fresh_hdr load_hdr(argp g, uint64_t pr) {
     fresh_hdr h{};
     h.pr = pr;
     if (pr != kNoPair) {
-        h.LA = (uint32_t)cst(g->A.l_cnt)[pr]; h.LB = (uint32_t)cst(g->B.l_cnt)[pr];
-        h.nA = (uint32_t)cst(g->A.e_cnt)[pr]; h.nB = (uint32_t)cst(g->B.e_cnt)[pr];
-        h.aeo = cst(g->A.e_off)[pr]; h.beo = cst(g->B.e_off)[pr];
-        h.alo = cst(g->A.l_off)[pr]; h.blo = cst(g->B.l_off)[pr];
-        h.clo = cst(g->C.l_off)[pr]; h.ceo = cst(g->C.e_off)[pr];
-        const uint32_t n = h.nA * h.nB;
-        h.nbk = cst(g->nb_table)[n];
-        h.nb_magic = cst(g->nb_magic)[n];
+        const recp r = (recp)g->recs + pr;
+        h.LA = r->LA; h.LB = r->LB;
+        h.nA = r->shape & 0xFFFFu; h.nB = r->shape >> 16;
+        h.aeo = r->aeo; h.beo = r->beo; h.ceo = r->ceo;
+        h.alo = r->alo; h.blo = r->blo; h.clo = r->clo;
+        h.nbk = r->nbk;
+        h.nb_magic = r->nb_magic;
     }
     return h;
 }
@@ -282,6 +294,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     while (cur.pr != kNoPair) {
         gq = launder(gq);
         const fresh_hdr nxt = load_hdr(gq, next_small(gq, cur.pr + gridDim.x));
+#ifdef PVAC_PHASE_STAMPS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // diag: header latency as its own phase
+        PHASE_STAMP(10);
+#endif
         const uint64_t pr = cur.pr;
         const uint32_t LA = cur.LA, LB = cur.LB, nA = cur.nA, nB = cur.nB;
         const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
@@ -355,6 +371,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 if (s0 + u < KS && tkey[s0 + u] != kTInf) klist[at++] = s0 + u;
         }
         __syncthreads();
+        PHASE_STAMP(8);
 
         // ---- S2a: fold each key's limbs, clear them, hash the key to its libstdc++ bucket
         const fastmod64 fm{nbk, cur.nb_magic};
@@ -542,13 +559,20 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(6);
-        // ---- clear chains and key sums for the next pair, stage the next pair
+        // ---- clear chains and key sums for the next pair, stage the next pair.
+        //      The record of the pair after next is touched here (scalar cache warm-up); its value
+        //      is consumed only after the barrier, whose wait it shares, so the load's latency runs
+        //      under the clear and the next iteration's header loads hit.
+        uint32_t touch = 0;
+        if (nxt.pr != kNoPair && nxt.pr + gridDim.x < gq->A.n) touch = ((recp)gq->recs)[nxt.pr + gridDim.x].nbk;
         {
             const uint32_t vecs = (sum_base + 8u * nkeys + 3u) >> 2;
             for (uint32_t w = tid; w < vecs; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
         }
+        PHASE_STAMP(7);
         stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
         __syncthreads();
+        asm volatile("" ::"s"(touch));
         PHASE_STAMP(9);
         cur = nxt;
     }

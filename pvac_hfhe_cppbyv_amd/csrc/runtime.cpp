@@ -42,6 +42,7 @@ struct pvac_hip_ctx {
     uint64_t* nb_magic = nullptr;
     uint8_t* pair_class = nullptr;
     uint32_t* pair_status = nullptr;
+    fresh_rec* fresh_recs = nullptr;   // per-pair header records of the fresh ct_mul path
     uint64_t* large_ids = nullptr;
     uint64_t* large_info = nullptr;
     size_t pair_cap = 0;
@@ -128,6 +129,8 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
         hipFree(c->pair_status);
         hipFree(c->large_ids);
         hipFree(c->large_info);
+        hipFree(c->fresh_recs);
+        c->fresh_recs = nullptr;
         c->pair_class = nullptr;
         c->pair_status = nullptr;
         c->large_ids = nullptr;
@@ -137,6 +140,7 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
         if (e == hipSuccess) e = hipMalloc(&c->pair_status, cap * 4);
         if (e == hipSuccess) e = hipMalloc(&c->large_ids, cap * 8);
         if (e == hipSuccess) e = hipMalloc(&c->large_info, cap * 40);
+        if (e == hipSuccess) e = hipMalloc(&c->fresh_recs, cap * sizeof(fresh_rec));
         if (e != hipSuccess) { c->pair_cap = 0; return hip_fail(c, e, "alloc pair scratch"); }
         c->pair_cap = cap;
     }
@@ -272,6 +276,7 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
     for (uint32_t n = 0; n < kNbTableLen; ++n) {
         nb[n] = (uint32_t)bucket_count_after_reserve(n);
         mg[n] = make_fastmod64(nb[n]).m;
+        if (nb[n] == 0 || nb[n] > 0xFFFFu) { delete c; return PVAC_ERANGE; }   // fresh_rec.nbk is u16
     }
     e = hipMalloc(&c->nb_table, nb.size() * 4);
     if (e == hipSuccess) e = hipMemcpy(c->nb_table, nb.data(), nb.size() * 4, hipMemcpyHostToDevice);
@@ -293,6 +298,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->nb_magic);
     hipFree(c->pair_class);
     hipFree(c->pair_status);
+    hipFree(c->fresh_recs);
     hipFree(c->large_ids);
     hipFree(c->large_info);
     hipFree(c->desc_dev);
@@ -513,6 +519,7 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
     if (plan->n_small) {
         mul_fresh_args a{};
         a.A = *A; a.B = *B; a.C = *C;
+        a.recs = c->fresh_recs;
         a.nonces = nonces;
         a.pair_class = c->pair_class;
         a.pair_status = c->pair_status;

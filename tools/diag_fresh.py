@@ -14,8 +14,8 @@ import torch  # noqa: E402
 
 from pvac_hfhe_cppbyv_amd import Engine, load_library  # noqa: E402
 
-PHASES = ["prologue", "S1 products", "S2a fold+bucket", "S2b link", "S2c walk+closure", "S3 scan",
-          "S4 positions", "S4b staging", "S5 copy-out", "clear+stage next"]
+PHASES = ["prologue", "S1 products", "S2a fold+bucket (after compact)", "S2b link", "S2c walk+closure", "S3 scan",
+          "S4 positions", "clear", "S2 compact", "stage next (prefetch wait)", "next header wait"]
 
 
 def main():

@@ -18,7 +18,7 @@ def main(root):
         with open(path) as f:
             for row in csv.DictReader(f):
                 k = row.get("Kernel_Name", "?")
-                short = k.replace("(anonymous namespace)", "anon").split("(")[0].split("::")[-1]
+                short = k.replace("(anonymous namespace)", "anon").split("(")[0].split("<")[0].split("::")[-1]
                 name = row.get("Counter_Name")
                 try:
                     v = float(row.get("Counter_Value", "nan"))
