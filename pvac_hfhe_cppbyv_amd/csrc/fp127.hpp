@@ -16,10 +16,17 @@ struct fp { uint64_t lo, hi; };
 constexpr uint64_t kM63 = 0x7FFFFFFFFFFFFFFFULL;
 constexpr uint64_t kAll = ~0ULL;
 
-// 64x64 -> 128
+// 64x64 -> 128 as four v_mad_u64_u32 (32x32 + 64 -> 64). `a*b` plus `__umul64hi(a, b)` would
+// compute the partial products twice (~9 multiplies); here each partial product is formed once
+// and carried through the accumulate operand. No step overflows: (2^32-1)^2 + 2(2^32-1) = 2^64-1.
 __device__ __forceinline__ void mul_64x64(uint64_t a, uint64_t b, uint64_t& lo, uint64_t& hi) {
-    lo = a * b;
-    hi = __umul64hi(a, b);
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p0 = (uint64_t)a0 * b0;
+    const uint64_t p1 = (uint64_t)a0 * b1 + (p0 >> 32);
+    const uint64_t p2 = (uint64_t)a1 * b0 + (uint32_t)p1;
+    hi = (uint64_t)a1 * b1 + (p1 >> 32) + (p2 >> 32);
+    lo = (p2 << 32) | (uint32_t)p0;
 }
 
 // add with carry-out

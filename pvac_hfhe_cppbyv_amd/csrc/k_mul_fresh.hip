@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
 // ---------------------------------------------------------------- aggregation + emit
 struct fresh_layout {
     // byte offsets into dynamic LDS
-    uint32_t acc, tkey, klist, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
+    uint32_t acc, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
@@ -109,7 +109,6 @@ __host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint
     uint32_t o = 0;
     L.acc = o;   o = align16(o + ks * 48u);           // 2 channels x 3 u64 limbs per key slot
     L.tkey = o;  o = align16(o + ks * 4u);
-    L.klist = o; o = align16(o + ks * 4u);            // compact list of existing keys
     L.a_w = o;   o = align16(o + na * 16u);
     L.a_inf = o; o = align16(o + na * 4u);
     L.b_w = o;   o = align16(o + nb * 16u);
@@ -250,8 +249,9 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
 
 template <int BS, int MINW>
 __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args* __restrict__ gp, fresh_layout Ls) {
-    constexpr int KI = kFreshKeysMax / BS;               // compact keys owned per thread (3)
+    constexpr int KI = kFreshKeysMax / BS;               // key slots owned per thread (3): s = tid + k*BS
     constexpr int NW = BS / 64;
+    constexpr int U = 4;                                 // products in flight per thread in S1
     static_assert(BS == (int)kFreshThreads && BS >= (int)kFreshEdgesMax && NW <= 8, "fresh geometry");
     // Arguments live in a device buffer; the pointer is laundered after every barrier so the
     // compiler re-reads fields from the scalar cache on use instead of pinning ~60 SGPRs of
@@ -259,9 +259,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     argp gq = launder((uint64_t)gp);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     unsigned long long* acc = (unsigned long long*)(lds + Ls.acc);
-    uint32_t* accw = (uint32_t*)(lds + Ls.acc);           // u32 view: heads | G | nxt | key sums
+    uint32_t* accw = (uint32_t*)(lds + Ls.acc);           // u32 view: heads | G | nxt | key sums | inv
+    const uint32_t acc_words = (Ls.tkey - Ls.acc) / 4u;
     uint32_t* tkey = (uint32_t*)(lds + Ls.tkey);
-    uint32_t* klist = (uint32_t*)(lds + Ls.klist);
     ulonglong2* a_w = (ulonglong2*)(lds + Ls.a_w);
     uint32_t* a_inf = (uint32_t*)(lds + Ls.a_inf);
     ulonglong2* b_w = (ulonglong2*)(lds + Ls.b_w);
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     const float inv_b = 1.0f / (float)Bm;
 
     // one-time clear: accumulators 0, first-insert times INF
-    for (uint32_t w = tid; w < gq->ks_max * 3u; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
+    for (uint32_t w = tid; w < acc_words / 4u; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
     for (uint32_t s = tid; s < gq->ks_max; s += BS) tkey[s] = kTInf;
     if (tid < 32) misc[tid] = 0;
     __syncthreads();
@@ -303,8 +303,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
         const uint32_t base = LA + LB, Lc = base + LP;
         const uint32_t nbk = cur.nbk;
-        const uint32_t chain_words = nbk + n + KS;               // heads | G | nxt
-        const uint32_t sum_base = (chain_words + 3u) & ~3u;      // key sums: 8 words per key
+        // acc region reuse after S2a (u32 words): heads[nbk] | G u16[n] | nxt u16[KS] | key sums
+        // (8 words per slot) | inv[total]
+        const uint32_t sum_base = (nbk + (n + 1u) / 2u + (KS + 1u) / 2u + 3u) & ~3u;
+        const uint32_t inv_base = sum_base + 8u * KS;
 
         if (misc[MF_INVALID]) {   // invalid references: reject the pair (reference behaviour is UB)
             __syncthreads();
@@ -322,7 +324,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         }
 
         // ---- S1: all |A.E||B.E| products into LDS limb accumulators + first-insert times.
-        //      Thread (j, g0) keeps B edge j in registers and walks A edges g0 + k*groups.
+        //      Thread (j, g0) keeps B edge j and reads its <= U A edges g0 + u*groups up front, so
+        //      the U products and their atomics issue back to back.
         if (n) {
             const uint32_t groups = BS / nB;
             const uint32_t j = (uint32_t)tid % nB, g0 = (uint32_t)tid / nB;
@@ -331,22 +334,34 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 const ulonglong2 y = b_w[j];
                 const fp yb{y.x, y.y};
                 const uint32_t lb = (bj >> 16) & 0x7FFFu, ib = bj & 0xFFFFu;
-                for (uint32_t i = g0; i < nA; i += groups) {
-                    const uint32_t ai = a_inf[i];
-                    const ulonglong2 x = a_w[i];
-                    const uint32_t lp = ((ai >> 16) & 0x7FFFu) * LB + lb;
-                    uint32_t r = (ai & 0xFFFFu) + ib;
-                    r = r >= Bm ? r - Bm : r;
-                    const uint32_t s = lp * Bm + r;
-                    const uint32_t chn = (ai ^ bj) >> 31;   // 0 = P (same sign), 1 = M
-                    uint64_t x0, x1, l0, l1, l2;
-                    fp_mul_fold1(fp{x.x, x.y}, yb, x0, x1);
-                    fp_split3_128(x0, x1, l0, l1, l2);
-                    unsigned long long* q = acc + (size_t)(s * 2 + chn) * 3;
-                    atomicAdd(q + 0, (unsigned long long)l0);
-                    atomicAdd(q + 1, (unsigned long long)l1);
-                    atomicAdd(q + 2, (unsigned long long)l2);
-                    atomicMin(&tkey[s], i * nB + j);
+                for (uint32_t i0 = g0; i0 < nA; i0 += U * groups) {
+                    uint32_t ai[U];
+                    ulonglong2 x[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = min(i0 + (uint32_t)u * groups, nA - 1u);
+                        ai[u] = a_inf[i];
+                        x[u] = a_w[i];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = i0 + (uint32_t)u * groups;
+                        if (i < nA) {
+                            const uint32_t lp = ((ai[u] >> 16) & 0x7FFFu) * LB + lb;
+                            uint32_t r = (ai[u] & 0xFFFFu) + ib;
+                            r = r >= Bm ? r - Bm : r;
+                            const uint32_t s = lp * Bm + r;
+                            const uint32_t chn = (ai[u] ^ bj) >> 31;   // 0 = P (same sign), 1 = M
+                            uint64_t x0, x1, l0, l1, l2;
+                            fp_mul_fold1(fp{x[u].x, x[u].y}, yb, x0, x1);
+                            fp_split3_128(x0, x1, l0, l1, l2);
+                            unsigned long long* q = acc + (size_t)(s * 2 + chn) * 3;
+                            atomicAdd(q + 0, (unsigned long long)l0);
+                            atomicAdd(q + 1, (unsigned long long)l1);
+                            atomicAdd(q + 2, (unsigned long long)l2);
+                            atomicMin(&tkey[s], i * nB + j);
+                        }
+                    }
                 }
             }
         }
@@ -356,38 +371,20 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         // next pair's raw inputs: loads in flight until stage_pair at the end of this iteration
         const fresh_pref pf = prefetch_pair(gq, nxt);
 
-        // ---- S2: compact the existing keys (slot order) into a dense list, so every thread owns
-        //      <= KI keys with no divergence on key existence
-        uint32_t nkeys;
-        {
-            constexpr uint32_t SPT = kFreshKeysMax / BS;             // slots per thread (3)
-            const uint32_t s0 = (uint32_t)tid * SPT;
-            uint32_t cnt = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < SPT; ++u) cnt += (s0 + u < KS && tkey[s0 + u] != kTInf) ? 1u : 0u;
-            uint32_t at = block_exclusive_scan<BS>(cnt, misc + MF_PART, nkeys);
-#pragma unroll
-            for (uint32_t u = 0; u < SPT; ++u)
-                if (s0 + u < KS && tkey[s0 + u] != kTInf) klist[at++] = s0 + u;
-        }
-        __syncthreads();
-        PHASE_STAMP(8);
-
-        // ---- S2a: fold each key's limbs, clear them, hash the key to its libstdc++ bucket
+        // ---- S2a: every thread owns key slots s = tid + k*BS: fold the limbs, clear them, hash
+        //      the key to its libstdc++ bucket
         const fastmod64 fm{nbk, cur.nb_magic};
         fp sumP[KI], sumM[KI];
-        uint32_t ks[KI], kt[KI], eb[KI], bk[KI];
+        uint32_t kt[KI], eb[KI], bk[KI];
         uint64_t myor = 0;
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            const uint32_t q_i = tid + (uint32_t)k * BS;
-            ks[k] = 0; kt[k] = 0; eb[k] = 0; bk[k] = 0;
+            const uint32_t s = tid + (uint32_t)k * BS;
+            kt[k] = kTInf; eb[k] = 0; bk[k] = 0;
             sumP[k] = fp{0, 0};
             sumM[k] = fp{0, 0};
-            if (q_i < nkeys) {
-                const uint32_t s = klist[q_i];
-                ks[k] = s;
-                kt[k] = tkey[s];
+            if (s < KS) kt[k] = tkey[s];
+            if (kt[k] != kTInf) {
                 // s / B for s < 1536: the float quotient of s + 1/2 is exact after floor
                 const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), r = s - lp * Bm;
                 unsigned long long* q = acc + (size_t)s * 6;
@@ -406,19 +403,19 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         gq = launder(gq);
         PHASE_STAMP(2);
 
-        // ---- S2b: key sums to LDS (compact, beside the chains), bucket chains
+        // ---- S2b: key sums to LDS (by slot, beside the chains), bucket chains
         uint32_t* heads = accw;
-        uint32_t* G = heads + nbk;
-        uint32_t* nxtl = G + n;
-        ulonglong2* ksum = (ulonglong2*)(accw + sum_base);   // [2 q] = P, [2 q + 1] = M
+        uint16_t* G = (uint16_t*)(heads + nbk);
+        uint16_t* nxtl = G + n;
+        ulonglong2* ksum = (ulonglong2*)(accw + sum_base);   // [2 s] = P, [2 s + 1] = M
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            const uint32_t q_i = tid + (uint32_t)k * BS;
-            if (q_i < nkeys) {
-                ksum[2 * q_i] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
-                ksum[2 * q_i + 1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
-                const uint32_t prev = atomicExch(&heads[bk[k]], ks[k] + 1);
-                nxtl[ks[k]] = prev | (eb[k] << 30);
+            const uint32_t s = tid + (uint32_t)k * BS;
+            if (kt[k] != kTInf) {
+                ksum[2 * s] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
+                ksum[2 * s + 1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
+                const uint32_t prev = atomicExch(&heads[bk[k]], s + 1);
+                nxtl[s] = (uint16_t)(prev | (eb[k] << 14));
             }
         }
         __syncthreads();
@@ -432,21 +429,21 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         for (int k = 0; k < KI; ++k) {
             tb[k] = 0;
             within[k] = 0;
-            if (tid + (uint32_t)k * BS < nkeys) {
+            if (kt[k] != kTInf) {
                 uint32_t q = heads[bk[k]], tmin = kt[k], w = 0, E = 0;
                 while (q) {
                     const uint32_t s2 = q - 1;
                     const uint32_t t2 = tkey[s2];
                     const uint32_t nx = nxtl[s2];
-                    const uint32_t e2 = __popc(nx >> 30);
+                    const uint32_t e2 = __popc(nx >> 14);
                     tmin = t2 < tmin ? t2 : tmin;
                     w += t2 > kt[k] ? e2 : 0u;
                     E += e2;
-                    q = nx & 0x3FFFFFFFu;
+                    q = nx & 0x3FFFu;
                 }
                 tb[k] = tmin;
                 within[k] = w;
-                if (tmin == kt[k]) G[tmin] = E;
+                if (tmin == kt[k]) G[tmin] = (uint16_t)E;
             }
         }
         if (wave == 0) {
@@ -484,7 +481,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             for (uint32_t r = r0; r < r0 + per && r < n; ++r) {
                 const uint32_t t = n - 1 - r;
                 const uint32_t v = G[t];
-                G[t] = run;
+                G[t] = (uint16_t)run;
                 run += v;
             }
             if (tid == 0) misc[MF_TOTAL] = total;
@@ -493,45 +490,72 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         gq = launder(gq);
         PHASE_STAMP(5);
 
-        // ---- S4: emit positions; write every key's edges straight to its output slots
+        // ---- S4: emit positions
         const uint32_t total = misc[MF_TOTAL];
         // guard_budget (encrypt.hpp:106-111): above edge_budget the reference runs compact_edges,
         // whose output is (layer, idx, P before M) order; product edges are already unique per
         // (layer, idx, ch) and nonzero, so it only re-orders them.
         const bool canonical = (gq->flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > gq->edge_budget;
+        // reference (hash) order: owners publish their edges' positions (inv[p] = slot, channel) and
+        // a writer pass stores positions p = tid, tid + BS, ... contiguously. Canonical order, or a
+        // pair whose inverse map does not fit beside the key sums, stores from the owners instead.
+        const bool gather = !canonical && inv_base + total <= acc_words;
         const uint64_t ceo = cur.ceo;
-        uint32_t rowbase = 0;
+        uint32_t* inv = accw + inv_base;
+        if (gather) {
 #pragma unroll
-        for (int k = 0; k < KI; ++k) {
-            const uint32_t q_i = tid + (uint32_t)k * BS;
-            const bool own = q_i < nkeys;
-            const uint32_t hp = own ? G[tb[k]] + within[k] : 0u;
-            uint32_t p = hp;
-            if (canonical) {   // workgroup-uniform: compact keys are in slot order, row k = keys k*BS..
-                uint32_t rowtot;
-                p = rowbase + block_exclusive_scan<BS>(__popc(eb[k]), misc + MF_PART, rowtot);
-                rowbase += rowtot;
-            }
-            if (own) tkey[ks[k]] = kTInf;
-            if (eb[k]) {
-                const uint32_t s = ks[k];
-                const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), idx = s - lp * Bm;
-                const uint32_t lid = remap[base + lp];
-                uint32_t* sp = gq->salt_pos;
-                if (eb[k] & 1u) {
-                    const ulonglong2 w = ksum[2 * q_i];
-                    gq->C.meta[ceo + p] = make_meta(lid, idx, 0);
-                    gq->C.w_lo[ceo + p] = w.x;
-                    gq->C.w_hi[ceo + p] = w.y;
-                    if (sp) sp[ceo + p] = hp;   // salts are drawn in hash order (arithmetic.hpp:90-101)
-                    ++p;
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                if (kt[k] != kTInf) {
+                    tkey[s] = kTInf;
+                    nxtl[s] = 0;
+                    uint32_t p = G[tb[k]] + within[k];
+                    if (eb[k] & 1u) inv[p++] = s << 1;
+                    if (eb[k] & 2u) inv[p] = (s << 1) | 1u;
+                    if (!(eb[k] & 1u)) ksum[2 * s] = make_ulonglong2(0, 0);       // never read by a writer
+                    if (!(eb[k] & 2u)) ksum[2 * s + 1] = make_ulonglong2(0, 0);
                 }
-                if (eb[k] & 2u) {
-                    const ulonglong2 w = ksum[2 * q_i + 1];
-                    gq->C.meta[ceo + p] = make_meta(lid, idx, 1);
-                    gq->C.w_lo[ceo + p] = w.x;
-                    gq->C.w_hi[ceo + p] = w.y;
-                    if (sp) sp[ceo + p] = hp + (eb[k] & 1u);
+            }
+        } else {
+            uint32_t rowbase = 0;
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                const bool own = kt[k] != kTInf;
+                const uint32_t hp = own ? G[tb[k]] + within[k] : 0u;
+                uint32_t p = hp;
+                if (canonical) {   // workgroup-uniform: row k = slots k*BS.., i.e. slot order
+                    uint32_t rowtot;
+                    p = rowbase + block_exclusive_scan<BS>(__popc(eb[k]), misc + MF_PART, rowtot);
+                    rowbase += rowtot;
+                }
+                if (own) {
+                    tkey[s] = kTInf;
+                    nxtl[s] = 0;
+                }
+                if (eb[k]) {
+                    const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), idx = s - lp * Bm;
+                    const uint32_t lid = remap[base + lp];
+                    uint32_t* sp = gq->salt_pos;
+                    if (eb[k] & 1u) {
+                        const ulonglong2 w = ksum[2 * s];
+                        gq->C.meta[ceo + p] = make_meta(lid, idx, 0);
+                        gq->C.w_lo[ceo + p] = w.x;
+                        gq->C.w_hi[ceo + p] = w.y;
+                        if (sp) sp[ceo + p] = hp;   // salts are drawn in hash order (arithmetic.hpp:90-101)
+                        ++p;
+                    }
+                    if (eb[k] & 2u) {
+                        const ulonglong2 w = ksum[2 * s + 1];
+                        gq->C.meta[ceo + p] = make_meta(lid, idx, 1);
+                        gq->C.w_lo[ceo + p] = w.x;
+                        gq->C.w_hi[ceo + p] = w.y;
+                        if (sp) sp[ceo + p] = hp + (eb[k] & 1u);
+                    }
+                }
+                if (own) {
+                    ksum[2 * s] = make_ulonglong2(0, 0);
+                    ksum[2 * s + 1] = make_ulonglong2(0, 0);
                 }
             }
         }
@@ -559,15 +583,34 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(6);
-        // ---- clear chains and key sums for the next pair, stage the next pair.
-        //      The record of the pair after next is touched here (scalar cache warm-up); its value
-        //      is consumed only after the barrier, whose wait it shares, so the load's latency runs
-        //      under the clear and the next iteration's header loads hit.
+
+        // ---- S5 (reference order): coalesced writer over emit positions; clears what it read
+        if (gather) {
+            uint32_t* sp = gq->salt_pos;
+            for (uint32_t p = tid; p < total; p += BS) {
+                const uint32_t e = inv[p];
+                const uint32_t s = e >> 1, ch = e & 1u;
+                const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), idx = s - lp * Bm;
+                const uint32_t lid = remap[base + lp];
+                const ulonglong2 w = ksum[2 * s + ch];
+                inv[p] = 0;
+                ksum[2 * s + ch] = make_ulonglong2(0, 0);
+                gq->C.meta[ceo + p] = make_meta(lid, idx, ch);
+                gq->C.w_lo[ceo + p] = w.x;
+                gq->C.w_hi[ceo + p] = w.y;
+                if (sp) sp[ceo + p] = p;   // hash order == emit order here
+            }
+        }
+        PHASE_STAMP(8);
+
+        // ---- clear bucket heads and G for the next pair (the rest was cleared by its readers),
+        //      stage the next pair. The record of the pair after next is touched here (scalar-
+        //      cache warm-up); its value is consumed only after the barrier, whose wait it shares.
         uint32_t touch = 0;
         if (nxt.pr != kNoPair && nxt.pr + gridDim.x < gq->A.n) touch = ((recp)gq->recs)[nxt.pr + gridDim.x].nbk;
         {
-            const uint32_t vecs = (sum_base + 8u * nkeys + 3u) >> 2;
-            for (uint32_t w = tid; w < vecs; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
+            const uint32_t words = nbk + (n + 1u) / 2u;
+            for (uint32_t w = tid; w < words; w += BS) accw[w] = 0;
         }
         PHASE_STAMP(7);
         stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
