@@ -106,47 +106,96 @@ __device__ __forceinline__ bool fp_nonzero(const fp& a) { return (a.lo | a.hi) !
 // such x are reduced once (fp_fold3_lazy), which skips the second fold and fp_from_words per
 // product. Equal mod p to the reference's fp_add chain of fp_mul results (field.hpp:50-56,
 // 209-213), which computes the exact sum mod p for canonical addends.
+//
+// These helpers work on 32-bit words: products are v_mad_u64_u32 chains and every multi-word
+// sum is a v_add_co_u32 / v_addc_co_u32 carry chain (__builtin_addc), instead of 64-bit adds
+// with compare-and-select carries.
+__device__ __forceinline__ uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint64_t join32(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+// (hi:lo) >> sh for 0 < sh < 32 (v_alignbit_b32)
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+    unsigned co;
+    const uint32_t r = __builtin_addc(a, b, cin, &co);
+    cout = co;
+    return r;
+}
+
 __device__ __forceinline__ void fp_mul_fold1(const fp& a, const fp& b, uint64_t& x0, uint64_t& x1) {
-    uint64_t p00l, p00h, p01l, p01h, p10l, p10h, p11l, p11h;
-    mul_64x64(a.lo, b.lo, p00l, p00h);
-    mul_64x64(a.lo, b.hi, p01l, p01h);
-    mul_64x64(a.hi, b.lo, p10l, p10h);
-    mul_64x64(a.hi, b.hi, p11l, p11h);
-    uint64_t c1, c2;
-    uint64_t z1 = add_co(p00h, p01l, c1);
-    z1 = add_co(z1, p10l, c2);
-    const uint64_t k1 = c1 + c2;
-    uint64_t c3, c4, c5;
-    uint64_t z2 = add_co(p01h, p10h, c3);
-    z2 = add_co(z2, p11l, c4);
-    z2 = add_co(z2, k1, c5);
-    const uint64_t z3 = p11h + c3 + c4 + c5;   // < 2^62 for canonical inputs
-    const uint64_t h0 = (z1 >> 63) | (z2 << 1);
-    const uint64_t h1 = (z2 >> 63) | (z3 << 1);
-    uint64_t d0;
-    x0 = add_co(p00l, h0, d0);
-    x1 = (z1 & kM63) + h1 + d0;                // no carry out: x < 2^128
+    const uint32_t A[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
+    const uint32_t B[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
+    uint32_t z[8];
+    {   // row 0: one mad chain
+        uint64_t t = (uint64_t)A[0] * B[0];
+        z[0] = lo32(t);
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+            t = (uint64_t)A[0] * B[j] + (t >> 32);
+            z[j] = lo32(t);
+        }
+        z[4] = hi32(t);
+    }
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {   // rows 1..3: mad chain into r, then z[i..i+4] += r
+        uint32_t r[5];
+        uint64_t t = (uint64_t)A[i] * B[0];
+        r[0] = lo32(t);
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+            t = (uint64_t)A[i] * B[j] + (t >> 32);
+            r[j] = lo32(t);
+        }
+        r[4] = hi32(t);
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[i + j] = addc(z[i + j], r[j], c, c);
+        z[i + 4] = r[4] + c;   // the partial product fits in i + 5 words: no carry out
+    }
+    // x = (z mod 2^127) + (z >> 127); z < 2^254 so the high part has < 2^127 and x < 2^128
+    uint32_t c = 0;
+    const uint32_t w0 = addc(z[0], funnel(z[4], z[3], 31), 0u, c);
+    const uint32_t w1 = addc(z[1], funnel(z[5], z[4], 31), c, c);
+    const uint32_t w2 = addc(z[2], funnel(z[6], z[5], 31), c, c);
+    const uint32_t w3 = (z[3] & 0x7FFFFFFFu) + funnel(z[7], z[6], 31) + c;
+    x0 = join32(w0, w1);
+    x1 = join32(w2, w3);
 }
 
 // 128-bit x -> 43/43/42-bit limbs; up to 2^21 of them sum in u64 limbs without overflow
 __device__ __forceinline__ void fp_split3_128(uint64_t x0, uint64_t x1, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
-    l0 = x0 & ((1ULL << 43) - 1);
-    l1 = ((x0 >> 43) | (x1 << 21)) & ((1ULL << 43) - 1);
-    l2 = x1 >> 22;
+    const uint32_t w0 = lo32(x0), w1 = hi32(x0), w2 = lo32(x1), w3 = hi32(x1);
+    l0 = join32(w0, w1 & 0x7FFu);                                 // bits 0..42
+    l1 = join32(funnel(w2, w1, 11), (w2 >> 11) & 0x7FFu);        // bits 43..85
+    l2 = join32(funnel(w3, w2, 22), w3 >> 22);                    // bits 86..127
 }
 
 // (l0 + l1 * 2^43 + l2 * 2^86) mod p, canonical, for limb sums l < 2^64
 __device__ __forceinline__ fp fp_fold3_lazy(uint64_t l0, uint64_t l1, uint64_t l2) {
-    uint64_t c0, c1, c2;
-    const uint64_t w0 = add_co(l0, l1 << 43, c0);
-    uint64_t w1 = add_co(l1 >> 21, l2 << 22, c1);
-    w1 = add_co(w1, c0, c2);
-    const uint64_t w2 = (l2 >> 42) + c1 + c2;   // V < 2^151
-    const uint64_t top = (w1 >> 63) | (w2 << 1);
-    uint64_t d;
-    const uint64_t lo = add_co(w0, top, d);
-    const uint64_t hi = (w1 & kM63) + d;
-    return fp_from_words(lo, hi);
+    // V as five words (V < 2^151): l0 + (l1 << 43), then + (l2 << 86)
+    uint32_t c = 0;
+    const uint32_t v0 = lo32(l0);
+    const uint32_t v1 = addc(hi32(l0), lo32(l1) << 11, 0u, c);
+    uint32_t v2 = addc(funnel(hi32(l1), lo32(l1), 21), 0u, c, c);
+    uint32_t v3 = (hi32(l1) >> 21) + c;
+    v2 = addc(v2, lo32(l2) << 22, 0u, c);
+    v3 = addc(v3, funnel(hi32(l2), lo32(l2), 10), c, c);
+    const uint32_t v4 = (hi32(l2) >> 10) + c;
+    // fold bits >= 127 (2^127 == 1): x = (V mod 2^127) + (V >> 127) < 2^127 + 2^24
+    const uint32_t top = funnel(v4, v3, 31);
+    uint32_t x0 = addc(v0, top, 0u, c);
+    uint32_t x1 = addc(v1, 0u, c, c);
+    uint32_t x2 = addc(v2, 0u, c, c);
+    uint32_t x3 = (v3 & 0x7FFFFFFFu) + c;
+    // canonical: x >= 2^127 -> x - p = (x - 2^127) + 1, where x - 2^127 < 2^24 (no carry); x == p -> 0
+    const uint32_t t = x3 >> 31;
+    x3 &= 0x7FFFFFFFu;
+    x0 += t;
+    const bool is_p = (x3 == 0x7FFFFFFFu) & ((x0 & x1 & x2) == 0xFFFFFFFFu);
+    if (is_p) { x0 = 0; x1 = 0; x2 = 0; x3 = 0; }
+    return fp{join32(x0, x1), join32(x2, x3)};
 }
 
 // canonical representative of any 128-bit word pair (fp_from_words, field.hpp:26-48)

@@ -377,24 +377,43 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         fp sumP[KI], sumM[KI];
         uint32_t kt[KI], eb[KI], bk[KI];
         uint64_t myor = 0;
+        // all reads first (the zeroing stores below would otherwise pin every later read behind
+        // them: same LDS array), then the arithmetic, then the zeroing
+        ulonglong2 lim[KI][3];
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
-            kt[k] = kTInf; eb[k] = 0; bk[k] = 0;
+            kt[k] = s < KS ? tkey[s] : kTInf;
+        }
+#pragma unroll
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t s = tid + (uint32_t)k * BS;
+            const ulonglong2* q = (const ulonglong2*)(acc + (size_t)min(s, KS - 1u) * 6);
+            lim[k][0] = q[0]; lim[k][1] = q[1]; lim[k][2] = q[2];
+        }
+#pragma unroll
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t s = tid + (uint32_t)k * BS;
+            eb[k] = 0; bk[k] = 0;
             sumP[k] = fp{0, 0};
             sumM[k] = fp{0, 0};
-            if (s < KS) kt[k] = tkey[s];
             if (kt[k] != kTInf) {
                 // s / B for s < 1536: the float quotient of s + 1/2 is exact after floor
                 const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), r = s - lp * Bm;
-                unsigned long long* q = acc + (size_t)s * 6;
-                sumP[k] = fp_fold3_lazy(q[0], q[1], q[2]);
-                sumM[k] = fp_fold3_lazy(q[3], q[4], q[5]);
-                q[0] = 0; q[1] = 0; q[2] = 0; q[3] = 0; q[4] = 0; q[5] = 0;
+                sumP[k] = fp_fold3_lazy(lim[k][0].x, lim[k][0].y, lim[k][1].x);
+                sumM[k] = fp_fold3_lazy(lim[k][1].y, lim[k][2].x, lim[k][2].y);
                 eb[k] = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
                 const uint64_t key = ((uint64_t)lp << 32) | r;
                 bk[k] = (uint32_t)fmod64(key * kGolden, fm);   // std::hash -> bucket
                 if (eb[k]) myor |= 1ull << lp;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t s = tid + (uint32_t)k * BS;
+            if (kt[k] != kTInf) {
+                ulonglong2* q = (ulonglong2*)(acc + (size_t)s * 6);
+                q[0] = make_ulonglong2(0, 0); q[1] = make_ulonglong2(0, 0); q[2] = make_ulonglong2(0, 0);
             }
         }
         myor = wave_or_u64(myor);
@@ -408,14 +427,17 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         uint16_t* G = (uint16_t*)(heads + nbk);
         uint16_t* nxtl = G + n;
         ulonglong2* ksum = (ulonglong2*)(accw + sum_base);   // [2 s] = P, [2 s + 1] = M
+        uint32_t prev[KI];
+#pragma unroll
+        for (int k = 0; k < KI; ++k)   // exchanges back to back, one wait for all
+            prev[k] = kt[k] != kTInf ? atomicExch(&heads[bk[k]], tid + (uint32_t)k * BS + 1u) : 0u;
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
             if (kt[k] != kTInf) {
                 ksum[2 * s] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
                 ksum[2 * s + 1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
-                const uint32_t prev = atomicExch(&heads[bk[k]], s + 1);
-                nxtl[s] = (uint16_t)(prev | (eb[k] << 14));
+                nxtl[s] = (uint16_t)(prev[k] | (eb[k] << 14));
             }
         }
         __syncthreads();
@@ -424,28 +446,38 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 
         // ---- S2c: walk chains -> bucket first-insert time, rank inside the bucket, group sizes;
         //      wave 0 then runs compact_layers (encrypt.hpp:73-104) as a bitmask closure
-        uint32_t tb[KI], within[KI];
+        uint32_t tb[KI], within[KI], cq[KI], cE[KI];
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            tb[k] = 0;
+            tb[k] = kt[k];
             within[k] = 0;
-            if (kt[k] != kTInf) {
-                uint32_t q = heads[bk[k]], tmin = kt[k], w = 0, E = 0;
-                while (q) {
-                    const uint32_t s2 = q - 1;
-                    const uint32_t t2 = tkey[s2];
-                    const uint32_t nx = nxtl[s2];
-                    const uint32_t e2 = __popc(nx >> 14);
-                    tmin = t2 < tmin ? t2 : tmin;
-                    w += t2 > kt[k] ? e2 : 0u;
-                    E += e2;
-                    q = nx & 0x3FFFu;
+            cE[k] = 0;
+            cq[k] = kt[k] != kTInf ? heads[bk[k]] : 0u;
+        }
+        // the three walks advance together: one LDS round trip per step for all of them
+        while (cq[0] | cq[1] | cq[2]) {
+            static_assert(KI == 3, "walk interleave assumes three slots per thread");
+            uint32_t t2[KI], nx[KI];
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s2 = (cq[k] ? cq[k] : 1u) - 1u;
+                t2[k] = tkey[s2];
+                nx[k] = nxtl[s2];
+            }
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                if (cq[k]) {
+                    const uint32_t e2 = __popc(nx[k] >> 14);
+                    tb[k] = t2[k] < tb[k] ? t2[k] : tb[k];
+                    within[k] += t2[k] > kt[k] ? e2 : 0u;
+                    cE[k] += e2;
+                    cq[k] = nx[k] & 0x3FFFu;
                 }
-                tb[k] = tmin;
-                within[k] = w;
-                if (tmin == kt[k]) G[tmin] = (uint16_t)E;
             }
         }
+#pragma unroll
+        for (int k = 0; k < KI; ++k)
+            if (kt[k] != kTInf && tb[k] == kt[k]) G[tb[k]] = (uint16_t)cE[k];
         if (wave == 0) {
             const uint64_t all = Lc >= 64 ? ~0ull : ((1ull << Lc) - 1ull);
             uint64_t used_lp = 0;
@@ -460,7 +492,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 keep = nk;
             }
             if ((uint32_t)lane < Lc)
-                remap[lane] = ((keep >> lane) & 1ull) ? (uint32_t)__popcll(keep & ((1ull << lane) - 1ull)) : kTInf;
+                remap[lane] = ((keep >> lane) & 1ull)   // popcount of the kept layers below this one
+                                  ? __builtin_amdgcn_mbcnt_hi((uint32_t)(keep >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u))
+                                  : kTInf;
             if (lane == 0) {
                 *(uint64_t*)(misc + MF_KEEP) = keep;
                 misc[MF_IDENT] = keep == all;

@@ -12,6 +12,15 @@ shift || true
 OUT="$ROOT/gpurun_out/pmc"
 mkdir -p "$OUT"
 BENCH=(python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu --no-extras "$@")
+if [ "${PMC_SET:-}" = "detail" ]; then
+  # issue/stall attribution (no HBM passes)
+  passes=(
+    "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS"
+    "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_INSTS_LDS_ATOMIC SQ_WAIT_INST_LDS SQ_WAIT_ANY"
+    "SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_CYCLES SQ_BUSY_CYCLES"
+    "GRBM_GUI_ACTIVE GRBM_COUNT"
+  )
+else
 passes=(
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY"
   "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM"
@@ -19,6 +28,7 @@ passes=(
   "WRITE_SIZE"
   "GRBM_GUI_ACTIVE GRBM_COUNT"
 )
+fi
 i=0
 for p in "${passes[@]}"; do
   i=$((i + 1))
