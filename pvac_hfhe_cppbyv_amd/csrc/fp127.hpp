@@ -63,41 +63,6 @@ __device__ __forceinline__ fp fp_neg(const fp& a) { return fp_from_words(kAll - 
 
 __device__ __forceinline__ fp fp_sub(const fp& a, const fp& b) { return fp_add(a, fp_neg(b)); }
 
-// field.hpp:113-213: exact 256-bit product, two Mersenne folds, canonicalise.
-__device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
-    uint64_t p00l, p00h, p01l, p01h, p10l, p10h, p11l, p11h;
-    mul_64x64(a.lo, b.lo, p00l, p00h);
-    mul_64x64(a.lo, b.hi, p01l, p01h);
-    mul_64x64(a.hi, b.lo, p10l, p10h);
-    mul_64x64(a.hi, b.hi, p11l, p11h);
-    // z1 = p00h + p01l + p10l ; carries into z2
-    uint64_t c1, c2;
-    uint64_t z1 = add_co(p00h, p01l, c1);
-    z1 = add_co(z1, p10l, c2);
-    const uint64_t k1 = c1 + c2;
-    uint64_t c3, c4, c5;
-    uint64_t z2 = add_co(p01h, p10h, c3);
-    z2 = add_co(z2, p11l, c4);
-    z2 = add_co(z2, k1, c5);
-    const uint64_t z3 = p11h + c3 + c4 + c5;
-    const uint64_t z0 = p00l;
-    // fold 1: (z mod 2^127) + (z >> 127)
-    const uint64_t h0 = (z1 >> 63) | (z2 << 1);
-    const uint64_t h1 = (z2 >> 63) | (z3 << 1);
-    const uint64_t h2 = z3 >> 63;
-    uint64_t d0, d1, d2;
-    const uint64_t x0 = add_co(z0, h0, d0);
-    uint64_t x1 = add_co(z1 & kM63, h1, d1);
-    x1 = add_co(x1, d0, d2);
-    const uint64_t x2 = h2 + d1 + d2;
-    // fold 2
-    const uint64_t yh = (x1 >> 63) | (x2 << 1);
-    uint64_t e0;
-    const uint64_t y0 = add_co(x0, yh, e0);
-    const uint64_t y1 = (x1 & kM63) + e0;
-    return fp_from_words(y0, y1);
-}
-
 __device__ __forceinline__ bool fp_nonzero(const fp& a) { return (a.lo | a.hi) != 0; }
 
 // ---- lazy products for sums ------------------------------------------------------------
@@ -196,6 +161,62 @@ __device__ __forceinline__ fp fp_fold3_lazy(uint64_t l0, uint64_t l1, uint64_t l
     const bool is_p = (x3 == 0x7FFFFFFFu) & ((x0 & x1 & x2) == 0xFFFFFFFFu);
     if (is_p) { x0 = 0; x1 = 0; x2 = 0; x3 = 0; }
     return fp{join32(x0, x1), join32(x2, x3)};
+}
+
+// field.hpp:113-213 (mul128x128 + fp_reduce256 + fp_from_words): the exact 256-bit product
+// of ANY two 128-bit inputs, two Mersenne folds, canonical result. The reference's value is the
+// unique canonical residue of a*b, so any exact evaluation is bit-identical; this one runs on
+// 32-bit words (16 v_mad_u64_u32 + carry chains).
+__device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
+    const uint32_t A[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
+    const uint32_t B[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
+    uint32_t z[8];
+    {
+        uint64_t t = (uint64_t)A[0] * B[0];
+        z[0] = lo32(t);
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+            t = (uint64_t)A[0] * B[j] + (t >> 32);
+            z[j] = lo32(t);
+        }
+        z[4] = hi32(t);
+    }
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        uint32_t r[5];
+        uint64_t t = (uint64_t)A[i] * B[0];
+        r[0] = lo32(t);
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+            t = (uint64_t)A[i] * B[j] + (t >> 32);
+            r[j] = lo32(t);
+        }
+        r[4] = hi32(t);
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[i + j] = addc(z[i + j], r[j], c, c);
+        z[i + 4] = r[4] + c;
+    }
+    // fold 1: x = (z mod 2^127) + (z >> 127) < 2^127 + 2^129 (five words)
+    uint32_t c = 0;
+    const uint32_t x0 = addc(z[0], funnel(z[4], z[3], 31), 0u, c);
+    const uint32_t x1 = addc(z[1], funnel(z[5], z[4], 31), c, c);
+    const uint32_t x2 = addc(z[2], funnel(z[6], z[5], 31), c, c);
+    const uint32_t x3 = addc(z[3] & 0x7FFFFFFFu, funnel(z[7], z[6], 31), c, c);
+    const uint32_t x4 = (z[7] >> 31) + c;
+    // fold 2: y = (x mod 2^127) + (x >> 127) < 2^127 + 8
+    const uint32_t top = funnel(x4, x3, 31);
+    uint32_t y0 = addc(x0, top, 0u, c);
+    uint32_t y1 = addc(x1, 0u, c, c);
+    uint32_t y2 = addc(x2, 0u, c, c);
+    uint32_t y3 = (x3 & 0x7FFFFFFFu) + c;
+    // canonical: y >= 2^127 -> (y - 2^127) + 1 (< 9, no carry); y == p -> 0
+    const uint32_t t = y3 >> 31;
+    y3 &= 0x7FFFFFFFu;
+    y0 += t;
+    const bool is_p = (y3 == 0x7FFFFFFFu) & ((y0 & y1 & y2) == 0xFFFFFFFFu);
+    if (is_p) { y0 = 0; y1 = 0; y2 = 0; y3 = 0; }
+    return fp{join32(y0, y1), join32(y2, y3)};
 }
 
 // canonical representative of any 128-bit word pair (fp_from_words, field.hpp:26-48)
