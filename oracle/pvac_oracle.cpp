@@ -276,8 +276,10 @@ void compact_layers(Ct& C) {
 
 // ops/encrypt.hpp:39-71 — merge equal (layer, idx, ch): sequential fp_add of weights in edge
 // order (quirk-exact), XOR of sigmas; drop merged entries with w == 0 and sigma == 0; output
-// ordered by (layer, idx, P before M). With sigma tracking off the sigma test counts as
-// "nonzero" (a merged real sigma is zero only for exact cancellations).
+// ordered by (layer, idx, P before M). With sigma tracking off (weights-only projection) a
+// merged entry is dropped when its weight is zero: real sigmas XOR to zero exactly when copies
+// of the same edge cancel (A - A: w = 0 and sigma = 0, dropped by the reference), while a zero
+// sum of distinct edges (whose sigmas would not cancel) has probability ~1/p.
 void compact_edges(Ct& C, uint32_t B, uint32_t sigma_words, bool track_sigma) {
     struct Acc { bool hp = false, hm = false; F wp{0, 0}, wm{0, 0}; std::vector<u64> sp, sm; };
     const size_t L = C.L.size();
@@ -294,7 +296,7 @@ void compact_edges(Ct& C, uint32_t B, uint32_t sigma_words, bool track_sigma) {
     }
     auto nonzero = [&](const F& w, const std::vector<u64>& s) {
         if (w.lo | w.hi) return true;
-        if (!track_sigma) return true;
+        if (!track_sigma) return false;
         for (u64 x : s) if (x) return true;
         return false;
     };

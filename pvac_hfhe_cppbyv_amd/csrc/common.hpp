@@ -112,7 +112,9 @@ hipError_t launch_plan_mul(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_
 hipError_t launch_gather_large(const pvac_ct_batch& A, const pvac_ct_batch& B, const uint64_t* ids, uint64_t n,
                                uint64_t* out, hipStream_t st);
 hipError_t launch_plan_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, plan_stats* stats,
-                           hipStream_t st);
+                           uint8_t* pair_class, uint64_t* merge_ids, uint64_t edge_budget, hipStream_t st);
+hipError_t launch_gather_merge(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C,
+                               const uint64_t* ids, uint64_t n, uint64_t* out, hipStream_t st);
 // in-place exclusive scan of n u64 values; scratch >= scan_scratch_words(n) u64
 size_t scan_scratch_words(size_t n);
 hipError_t launch_exclusive_scan_u64(uint64_t* data, size_t n, uint64_t* scratch, unsigned long long* total_out,
@@ -156,6 +158,17 @@ struct mul_fresh_args {
 hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st);
 // args_dev: device copy of `a` (the kernel reads its arguments from memory, see k_mul_fresh.hip)
 hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* args_dev, int num_cus, hipStream_t st);
+
+// ---- ct_add / ct_sub over edge_budget (k_add_merge.hip): compact_edges + compact_layers per pair
+struct merge_pair_info {
+    uint64_t pair, aeo, beo, ceo, nA, nB;
+    uint32_t LA, L;
+};
+size_t merge_scratch_bytes(uint64_t n_edges, uint32_t n_layers);
+// counters: 2 device u64 (groups, kept edges) owned by the caller
+hipError_t launch_add_merge(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, uint64_t pr,
+                            const merge_pair_info& info, uint32_t Bm, int negate_b, void* scratch, size_t scratch_bytes,
+                            unsigned long long* counters, hipStream_t st);
 
 // ---- ct_mul, general path (k_mul_large.hip): multi-kernel, global scratch, one workgroup
 // per (A-layer, B-layer) product task. The host prepares one descriptor per large pair with
@@ -217,6 +230,6 @@ struct mul_large_args {
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
 
 hipError_t launch_ct_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, int negate_b,
-                         uint32_t max_layers, hipStream_t st);
+                         uint32_t max_layers, const uint8_t* pair_class, hipStream_t st);
 
 }  // namespace pvhip

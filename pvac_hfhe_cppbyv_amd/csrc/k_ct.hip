@@ -69,13 +69,36 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
 }
 
 __global__ __launch_bounds__(kPlanBlock) void k_plan_add(pvac_ct_batch A, pvac_ct_batch B, pvac_ct_batch C,
-                                                        plan_stats* stats) {
+                                                        plan_stats* stats, uint8_t* pair_class, uint64_t* merge_ids,
+                                                        uint64_t edge_budget) {
     const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
     if (i >= A.n) return;
     const uint64_t capL = A.l_cnt[i] + B.l_cnt[i];
+    const uint64_t capE = A.e_cnt[i] + B.e_cnt[i];
     C.l_off[i] = capL;
-    C.e_off[i] = A.e_cnt[i] + B.e_cnt[i];
+    C.e_off[i] = capE;
+    // guard_budget (encrypt.hpp:106-111): over-budget pairs take the merge path (k_add_merge.hip)
+    const bool merge = capE > edge_budget;
+    pair_class[i] = merge ? PAIR_LARGE : PAIR_SMALL;
+    if (merge) merge_ids[atomicAdd(&stats->n_large, 1ull)] = i;
     atomicMax(&stats->max_layers, (unsigned)(capL > 0xFFFFFFFFull ? 0xFFFFFFFFull : capL));
+}
+
+// shapes and offsets of the over-budget ct_add pairs: {pair, LA, LB, nA, nB, aeo, beo, ceo}
+__global__ __launch_bounds__(kPlanBlock) void k_gather_merge(pvac_ct_batch A, pvac_ct_batch B, pvac_ct_batch C,
+                                                            const uint64_t* ids, uint64_t n, uint64_t* out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t p = ids[k];
+    uint64_t* o = out + 8 * k;
+    o[0] = p;
+    o[1] = A.l_cnt[p];
+    o[2] = B.l_cnt[p];
+    o[3] = A.e_cnt[p];
+    o[4] = B.e_cnt[p];
+    o[5] = A.e_off[p];
+    o[6] = B.e_off[p];
+    o[7] = C.e_off[p];
 }
 
 // shapes of the general-path pairs for the host's descriptor build: {pair, LA, LB, nA, nB}
@@ -169,13 +192,14 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* data, size_
 constexpr int kAddBlock = 256;
 
 __global__ __launch_bounds__(kAddBlock) void k_ct_add(pvac_ct_batch A, pvac_ct_batch B, pvac_ct_batch C, int negate_b,
-                                                     uint32_t lds_layers) {
+                                                     uint32_t lds_layers, const uint8_t* pair_class) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t* keep = (uint32_t*)lds;                 // [lds_layers] then remap in place
     __shared__ uint32_t flags[4];
     __shared__ uint32_t part[kAddBlock / 64];
     const uint64_t pr = blockIdx.x;
     if (pr >= A.n) return;
+    if (pair_class && pair_class[pr] == PAIR_LARGE) return;   // over edge_budget: k_add_merge.hip
     const int tid = threadIdx.x;
     const uint32_t LA = (uint32_t)A.l_cnt[pr], LB = (uint32_t)B.l_cnt[pr];
     const uint32_t L = LA + LB;
@@ -297,10 +321,18 @@ hipError_t launch_gather_large(const pvac_ct_batch& A, const pvac_ct_batch& B, c
 }
 
 hipError_t launch_plan_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, plan_stats* stats,
-                           hipStream_t st) {
+                           uint8_t* pair_class, uint64_t* merge_ids, uint64_t edge_budget, hipStream_t st) {
     if (!A.n) return hipSuccess;
     hipLaunchKernelGGL(k_plan_add, dim3((unsigned)((A.n + kPlanBlock - 1) / kPlanBlock)), dim3(kPlanBlock), 0, st, A,
-                       B, C, stats);
+                       B, C, stats, pair_class, merge_ids, edge_budget);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_merge(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C,
+                               const uint64_t* ids, uint64_t n, uint64_t* out, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_merge, dim3((unsigned)((n + kPlanBlock - 1) / kPlanBlock)), dim3(kPlanBlock), 0, st, A,
+                       B, C, ids, n, out);
     return hipGetLastError();
 }
 
@@ -317,11 +349,12 @@ hipError_t launch_exclusive_scan_u64(uint64_t* data, size_t n, uint64_t* scratch
 }
 
 hipError_t launch_ct_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, int negate_b,
-                         uint32_t max_layers, hipStream_t st) {
+                         uint32_t max_layers, const uint8_t* pair_class, hipStream_t st) {
     if (!A.n) return hipSuccess;
     const size_t lds = ((size_t)max_layers * 4 + 15) & ~(size_t)15;
     if (lds > 120 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ct_add, dim3((unsigned)A.n), dim3(kAddBlock), lds, st, A, B, C, negate_b, max_layers);
+    hipLaunchKernelGGL(k_ct_add, dim3((unsigned)A.n), dim3(kAddBlock), lds, st, A, B, C, negate_b, max_layers,
+                       pair_class);
     return hipGetLastError();
 }
 

@@ -43,6 +43,10 @@ struct pvac_hip_ctx {
     uint8_t* pair_class = nullptr;
     uint32_t* pair_status = nullptr;
     fresh_rec* fresh_recs = nullptr;   // per-pair header records of the fresh ct_mul path
+    std::vector<merge_pair_info> merge_host;   // over-budget ct_add pairs of the latest add plan
+    void* merge_scratch = nullptr;
+    size_t merge_cap = 0;
+    unsigned long long* merge_counters = nullptr;
     uint64_t* large_ids = nullptr;
     uint64_t* large_info = nullptr;
     size_t pair_cap = 0;
@@ -139,7 +143,7 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
         hipError_t e = hipMalloc(&c->pair_class, cap);
         if (e == hipSuccess) e = hipMalloc(&c->pair_status, cap * 4);
         if (e == hipSuccess) e = hipMalloc(&c->large_ids, cap * 8);
-        if (e == hipSuccess) e = hipMalloc(&c->large_info, cap * 40);
+        if (e == hipSuccess) e = hipMalloc(&c->large_info, cap * 64);   // 5 (mul) or 8 (add merge) words per pair
         if (e == hipSuccess) e = hipMalloc(&c->fresh_recs, cap * sizeof(fresh_rec));
         if (e != hipSuccess) { c->pair_cap = 0; return hip_fail(c, e, "alloc pair scratch"); }
         c->pair_cap = cap;
@@ -305,6 +309,8 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->arena);
     hipFree(c->salt_pos);
     hipFree(c->fresh_args);
+    hipFree(c->merge_scratch);
+    hipFree(c->merge_counters);
     hipFree(c->scan_scratch);
     hipFree(c->stats);
     hipFree(c->totals);
@@ -579,8 +585,11 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (!A->n) return PVAC_OK;
     int rc = ensure_pairs(c, A->n);
     if (rc) return rc;
+    c->merge_host.clear();
+    plan->reserved[0] = ++c->plan_stamp;
     hipError_t e = hipMemsetAsync(c->stats, 0, sizeof(plan_stats), c->stream);
-    if (e == hipSuccess) e = launch_plan_add(*A, *B, *C, c->stats, c->stream);
+    if (e == hipSuccess)
+        e = launch_plan_add(*A, *B, *C, c->stats, c->pair_class, c->large_ids, c->prm.edge_budget, c->stream);
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->l_off, A->n, c->scan_scratch, &c->totals[0], c->stream);
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->e_off, A->n, c->scan_scratch, &c->totals[1], c->stream);
     plan_stats st{};
@@ -592,7 +601,35 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     plan->total_layer_slots = tot[0];
     plan->total_edge_slots = tot[1];
     plan->max_layers = st.max_layers;
-    plan->n_small = A->n;
+    plan->n_large = st.n_large;
+    plan->n_small = A->n - st.n_large;
+    if (st.n_large) {   // guard_budget pairs: shapes and offsets for the per-pair merge launches
+        std::vector<uint64_t> info(8 * st.n_large);
+        e = launch_gather_merge(*A, *B, *C, c->large_ids, st.n_large, c->large_info, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(info.data(), c->large_info, info.size() * 8, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "ct_add_plan (merge)");
+        for (uint64_t k = 0; k < st.n_large; ++k) {
+            const uint64_t* o = &info[8 * k];
+            merge_pair_info m{};
+            m.pair = o[0];
+            m.LA = (uint32_t)o[1];
+            m.L = (uint32_t)(o[1] + o[2]);
+            m.nA = o[3];
+            m.nB = o[4];
+            m.aeo = o[5];
+            m.beo = o[6];
+            m.ceo = o[7];
+            if (m.nA + m.nB >= (1ull << 31) || (uint64_t)m.L * c->prm.B * 2 >= 0xFFFFFFFFull) {
+                c->merge_host.clear();
+                return fail(c, PVAC_ENOSYS, "ct_add_plan: over-budget pair beyond 2^31 edges or 2^32 keys");
+            }
+            c->merge_host.push_back(m);
+        }
+        std::sort(c->merge_host.begin(), c->merge_host.end(),
+                  [](const merge_pair_info& x, const merge_pair_info& y) { return x.pair < y.pair; });
+    }
     return PVAC_OK;
 }
 
@@ -603,9 +640,40 @@ int pvac_hip_ct_add_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
     if (A->n != plan->n_pairs || B->n != plan->n_pairs) return fail(c, PVAC_EINVAL, "ct_add_exec: plan mismatch");
     if (!A->n) return PVAC_OK;
     if (plan->max_layers > 30000) return fail(c, PVAC_ENOSYS, "ct_add_exec: > 30000 layers per cipher");
-    // guard_budget: pairs whose |A.E|+|B.E| exceed edge_budget need compact_edges (layer-dense path)
-    scoped_timer t(c, "ct_add");
-    return hip_fail(c, launch_ct_add(*A, *B, *C, negate_b, plan->max_layers, c->stream), "ct_add");
+    if (plan->n_large && (plan->reserved[0] != c->plan_stamp || plan->n_large != c->merge_host.size()))
+        return fail(c, PVAC_EINVAL, "ct_add_exec: plan is not this context's latest plan");
+    {
+        scoped_timer t(c, "ct_add");
+        const int rc = hip_fail(c,
+                                launch_ct_add(*A, *B, *C, negate_b, plan->max_layers,
+                                              plan->n_large ? c->pair_class : nullptr, c->stream),
+                                "ct_add");
+        if (rc) return rc;
+    }
+    if (!plan->n_large) return PVAC_OK;
+    // guard_budget (encrypt.hpp:106-111): compact_edges + compact_layers per over-budget pair
+    scoped_timer t(c, "ct_add_merge");
+    if (!c->merge_counters) {
+        hipError_t e = hipMalloc(&c->merge_counters, 2 * sizeof(unsigned long long));
+        if (e != hipSuccess) return hip_fail(c, e, "alloc merge counters");
+    }
+    for (const merge_pair_info& m : c->merge_host) {
+        const size_t need = merge_scratch_bytes(m.nA + m.nB, m.L);
+        if (need > c->merge_cap) {
+            hipFree(c->merge_scratch);
+            c->merge_scratch = nullptr;
+            c->merge_cap = 0;
+            hipError_t e = hipMalloc(&c->merge_scratch, need);
+            if (e != hipSuccess) return hip_fail(c, e, "alloc merge scratch");
+            c->merge_cap = need;
+        }
+        const int rc = hip_fail(c,
+                                launch_add_merge(*A, *B, *C, m.pair, m, c->prm.B, negate_b, c->merge_scratch,
+                                                 c->merge_cap, c->merge_counters, c->stream),
+                                "ct_add merge");
+        if (rc) return rc;
+    }
+    return PVAC_OK;
 }
 
 int pvac_hip_ct_scale(pvac_hip_ctx* c, pvac_ct_batch* X, uint64_t s_lo, uint64_t s_hi) {
