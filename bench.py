@@ -63,6 +63,9 @@ def main():
     if args.only == "chain":
         print(json.dumps(chain_bench(eng, args)), flush=True)
         return
+    if args.only == "sigma":
+        print(json.dumps(sigma_bench(eng, args, False)), flush=True)
+        return
     from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks
     n = args.pairs
     # weak scaling: rank r owns global pairs [r*n, (r+1)*n); inputs and nonces are keyed by the
@@ -293,7 +296,16 @@ def extras(eng, args, with_cpu):
             fp[name]["gpu_output_matches"] = bool(np.array_equal(glo, olo))
     res["fp127_cfg2"] = fp
     del bufs
-    # ---- full ct_mul WITH sigma (reference-complete ct_mul)
+    res["ct_mul_with_sigma"] = sigma_bench(eng, args, with_cpu)
+    res["cfg4_chain"] = chain_bench(eng, args)
+    return res
+
+
+def sigma_bench(eng, args, with_cpu):
+    """Full ct_mul WITH sigma (reference-complete ct_mul, f1) on a smaller batch."""
+    import torch
+    from pvac_hfhe_cppbyv_amd import MUL_WITH_SIGMA
+    dev = eng.device
     ns = args.sigma_pairs
     eng.gen_H()
     A = eng.gen_fresh(ns, 0x51, args.epl)
@@ -324,9 +336,7 @@ def extras(eng, args, with_cpu):
             "edges": edges}
     if with_cpu:
         full["cpu_baseline"] = _ref_full_baseline()
-    res["ct_mul_with_sigma"] = full
-    res["cfg4_chain"] = chain_bench(eng, args)
-    return res
+    return full
 
 
 def chain_bench(eng, args):

@@ -120,6 +120,72 @@ __device__ __forceinline__ void select_pass(const uint32_t (&val)[4], uint32_t* 
     have = have + group_total < K ? have + group_total : K;
 }
 
+// The same selection for two 32-lane groups (X and noise streams of one edge), without the
+// O(GS^2) shuffle scan. Each draw first reads the bitmap of values selected by EARLIER passes,
+// then sets its bit with a returning atomic OR: a bit found already set marks an equal value
+// elsewhere in THIS pass (LDS ops of a wave execute in issue order, so the reads see the
+// pre-pass bitmap). Every duplicated value has at least one marked draw; a wave-uniform loop
+// over the marked values finds all draws of each with four ballots and keeps only the first in
+// draw order (position 4*lane + q). Bits of draws ranked >= K are set too, but K is then reached
+// and the stream is finished. Selected set == select_pass<32>.
+__device__ __forceinline__ void select_pass2x32(const uint32_t (&val)[4], uint32_t* bm, uint32_t K, uint32_t& have,
+                                                int (&rank)[4]) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t gmask = lane < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
+    bool isnew[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t v = val[q];
+        isnew[q] = v != 0xFFFFFFFFu && !((bm[v >> 5] >> (v & 31)) & 1u);
+    }
+    uint32_t flagged = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (isnew[q]) {
+            const uint32_t bit = 1u << (val[q] & 31);
+            if (atomicOr(&bm[val[q] >> 5], bit) & bit) flagged |= 1u << q;
+        }
+    }
+    uint64_t fl = __ballot(flagged != 0);
+    while (fl) {   // wave-uniform; typically 0-2 iterations
+        const int L = __ffsll((unsigned long long)fl) - 1;
+        fl &= fl - 1;
+        uint32_t fq = __builtin_amdgcn_readlane(flagged, L);
+        const uint64_t lg = L < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
+        while (fq) {
+            const int q0 = __ffs(fq) - 1;
+            fq &= fq - 1;
+            const uint32_t mine = q0 == 0 ? val[0] : q0 == 1 ? val[1] : q0 == 2 ? val[2] : val[3];
+            const uint32_t v = __builtin_amdgcn_readlane(mine, L);
+            uint64_t m[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m[q] = __ballot(val[q] == v) & lg;
+            const int f = __ffsll((unsigned long long)(m[0] | m[1] | m[2] | m[3])) - 1;   // first lane
+            const int qf = ((m[0] >> f) & 1) ? 0 : ((m[1] >> f) & 1) ? 1 : ((m[2] >> f) & 1) ? 2 : 3;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (((m[q] >> lane) & 1) && !(lane == f && q == qf)) isnew[q] = false;
+        }
+    }
+    (void)gmask;
+    const uint32_t cnt = (uint32_t)isnew[0] + isnew[1] + isnew[2] + isnew[3];
+    uint32_t x = wave_incl_scan_u32(cnt);
+    const uint32_t lowtot = __builtin_amdgcn_readlane(x, 31);
+    const uint32_t alltot = __builtin_amdgcn_readlane(x, 63);
+    if (lane >= 32) x -= lowtot;
+    const uint32_t group_total = lane < 32 ? lowtot : alltot - lowtot;
+    uint32_t r = have + x - cnt;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        rank[q] = -1;
+        if (isnew[q]) {
+            if (r < K) rank[q] = (int)r;
+            ++r;
+        }
+    }
+    have = have + group_total < K ? have + group_total : K;
+}
+
 struct sig_args {
     pvac_ct_batch X;
     const uint64_t* salts;
@@ -133,7 +199,9 @@ struct sig_args {
 };
 
 // per-wave LDS: sigma [m_bits/32] | bmX [n_bits/32] | bmN [m_bits/32] | cols [x_col_wt] u16
-__global__ __launch_bounds__(kSigBlock) void k_sigma(sig_args a) {
+// 6 blocks per CU (6 waves per SIMD): the compiler keeps the pass loop within 80 VGPRs without
+// spills instead of hoisting the whole SHA-256 message schedule (149 VGPRs, 3 waves per SIMD)
+__global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t slds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t sw32 = a.m_bits / 32, bx32 = a.n_bits / 32, bn32 = a.m_bits / 32;
@@ -164,21 +232,35 @@ __global__ __launch_bounds__(kSigBlock) void k_sigma(sig_args a) {
             const uint64_t words[7] = {a.canon, L.ztag, L.nonce_lo, L.nonce_hi, (uint64_t)meta_idx(m),
                                        (uint64_t)meta_ch(m), salt};
             // midstates: block 0 of both messages, selected per lane group
-            uint32_t bx[16], bn[16], blk[16];
-            build_block<15, 7>(bx, 0, kLabX, words, 0);
-            build_block<14, 7>(bn, 0, kLabN, words, 0);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) blk[i] = isX ? bx[i] : bn[i];
+            uint32_t tm[16];
             sha_state mid;
-            sha_init(mid);
-            sha_compress(mid, blk);
+            {
+                uint32_t bx[16], bn[16];
+                build_block<15, 7>(bx, 0, kLabX, words, 0);
+                build_block<14, 7>(bn, 0, kLabN, words, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) tm[i] = isX ? bx[i] : bn[i];
+                sha_init(mid);
+                sha_compress(mid, tm);
+                // block 1 template (counter 0); each pass ORs its counter in below
+                build_block<15, 7>(bx, 1, kLabX, words, 0);
+                build_block<14, 7>(bn, 1, kLabN, words, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) tm[i] = isX ? bx[i] : bn[i];
+            }
+            // the le64 counter sits at block-1 byte offset 7 (X: 15-byte label) or 6 (noise: 14):
+            // as a big-endian 96-bit window over words 1..3 that is bswap64(ctr) << 8 or << 16
+            const uint32_t csh = isX ? 8u : 16u;
             uint32_t have = 0;
             for (uint32_t pass = 0; pass < kMaxPasses; ++pass) {   // bounded: never hang the GPU
                 const uint64_t ctr = (uint64_t)pass * 32 + (lane & 31);
-                build_block<15, 7>(bx, 1, kLabX, words, ctr);
-                build_block<14, 7>(bn, 1, kLabN, words, ctr);
+                const uint64_t bs = ((uint64_t)bswap32((uint32_t)ctr) << 32) | bswap32((uint32_t)(ctr >> 32));
+                uint32_t blk[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) blk[i] = isX ? bx[i] : bn[i];
+                for (int i = 0; i < 16; ++i) blk[i] = tm[i];
+                blk[1] |= (uint32_t)(bs >> (64u - csh));
+                blk[2] |= (uint32_t)((bs << csh) >> 32);
+                blk[3] |= (uint32_t)(bs << csh);
                 sha_state s = mid;
                 sha_compress(s, blk);
                 uint32_t val[4];
@@ -188,7 +270,7 @@ __global__ __launch_bounds__(kSigBlock) void k_sigma(sig_args a) {
                     val[q] = (have < K && x <= lim) ? (uint32_t)(x % Nmod) : 0xFFFFFFFFu;
                 }
                 int rank[4];
-                select_pass<32>(val, bm, K, have, rank);
+                select_pass2x32(val, bm, K, have, rank);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     if (rank[q] >= 0) {
@@ -200,15 +282,25 @@ __global__ __launch_bounds__(kSigBlock) void k_sigma(sig_args a) {
                 const bool doneN = __shfl(have, 32, 64) >= a.err_wt;
                 if (doneX && doneN) break;
             }
-            // XOR the selected H columns: K*width row flips spread over the wave
+            // XOR the selected H columns: every lane takes whole columns and reads their row lists
+            // with 16-byte loads (width is a multiple of 8), flipping bits with LDS atomic XOR
             const uint32_t W = a.width;
-            const uint32_t nflip = a.x_col_wt * W;
-            for (uint32_t f = lane; f < nflip; f += 64) {
-                const uint32_t ci2 = f / W, kk = f - ci2 * W;
-                const uint32_t col = cols[ci2];
-                if (kk < a.counts[col]) {
-                    const uint32_t r = a.rows[(size_t)col * W + kk];
-                    atomicXor(&sig[r >> 5], 1u << (r & 31));
+            for (uint32_t c = lane; c < a.x_col_wt; c += 64) {
+                const uint32_t col = cols[c];
+                const uint32_t cnt = a.counts[col];
+                const uint4* rp = (const uint4*)(a.rows + (size_t)col * W);
+                for (uint32_t k8 = 0; k8 < cnt; k8 += 8) {
+                    const uint4 v = rp[k8 >> 3];
+                    const uint32_t rr[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                                            v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+                    if (k8 + 8 <= cnt) {   // full group (always, for gen_H tables)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) atomicXor(&sig[rr[j] >> 5], 1u << (rr[j] & 31));
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            if (k8 + j < cnt) atomicXor(&sig[rr[j] >> 5], 1u << (rr[j] & 31));
+                    }
                 }
             }
             // write 8192 bits: one 16-byte store per lane, then clear the wave's LDS
@@ -313,7 +405,8 @@ hipError_t sigma_tables_from_dense(sigma_tables& T, const pvac_hip_params& prm, 
         cnt[c] = k;
         width = k > width ? k : width;
     }
-    if (width == 0) width = 1;
+    width = (width + 7) & ~7u;   // row lists padded to 16-byte multiples (k_sigma reads uint4)
+    if (width == 0) width = 8;
     std::vector<uint16_t> rows((size_t)prm.n_bits * width, 0);
     for (uint32_t c = 0; c < prm.n_bits; ++c) {
         uint32_t k = 0;
@@ -337,7 +430,8 @@ hipError_t sigma_tables_from_dense(sigma_tables& T, const pvac_hip_params& prm, 
 hipError_t sigma_tables_generate(sigma_tables& T, const pvac_hip_params& prm, uint8_t digest[32], hipStream_t st) {
     if (prm.h_col_wt == 0 || prm.h_col_wt > prm.m_bits || prm.m_bits % 32 || prm.m_bits > 65536)
         return hipErrorInvalidValue;
-    hipError_t e = alloc_tables(T, prm.n_bits, prm.h_col_wt);
+    // row lists padded to 16-byte multiples (k_sigma reads uint4); counts bound every reader
+    hipError_t e = alloc_tables(T, prm.n_bits, (prm.h_col_wt + 7) & ~7u);
     if (e != hipSuccess) return e;
     const size_t lds = (size_t)4 * (prm.m_bits / 32) * 4;
     hipLaunchKernelGGL(k_gen_H, dim3(2048), dim3(256), lds, st, T.rows, T.counts, T.width, prm.m_bits, prm.n_bits,
@@ -358,7 +452,7 @@ hipError_t sigma_tables_generate(sigma_tables& T, const pvac_hip_params& prm, ui
             for (int i = 0; i < 8; ++i) msg[4 + 8 * k + i] = (uint8_t)(hdr[k] >> (8 * i));
         uint8_t* cols = msg.data() + 28;
         for (uint32_t c = 0; c < prm.n_bits; ++c)
-            for (uint32_t k = 0; k < T.width; ++k) {
+            for (uint32_t k = 0; k < prm.h_col_wt; ++k) {
                 const uint32_t r = rows[(size_t)c * T.width + k];
                 cols[(size_t)c * colbytes + (r >> 3)] |= (uint8_t)(1u << (r & 7));
             }
