@@ -195,6 +195,31 @@ uint64_t pvac_hip_bucket_count(uint64_t n);
 /* per-cipher FNV-1a digest over (meta, w_lo, w_hi) of its edges in order (device out[n]). */
 int pvac_hip_batch_digest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
 
+/* ---------------------------------------------------------------- .ct codec (host memory)
+ * The reference's ciphertext file format (tests/add.cpp:22-155: saveCts / loadCts, putLayer,
+ * putEdge) <-> SoA batches in HOST memory; no context or device needed (copy to the device with
+ * hipMemcpy, or parse straight into pinned buffers). PROD layers carry no seed on disk, so parsed
+ * PROD layers have ztag = nonce = 0. Every edge of a file must carry the same sigma nbits. */
+#define PVAC_CT_MIXED_SIGMA 0x1u   /* pvac_ct_file_info.flags: edges disagree on sigma nbits */
+typedef struct pvac_ct_file_info {
+    uint64_t n_ciphers, total_layers, total_edges;
+    uint32_t sigma_bits;    /* nbits of every edge's sigma (0: the file carries no sigmas) */
+    uint32_t sigma_words;   /* ceil(sigma_bits / 64) */
+    uint32_t flags;
+    uint32_t pad;
+} pvac_ct_file_info;
+/* Validate a file image and size it (PVAC_EINVAL on a malformed or truncated image). */
+int pvac_ct_scan(const uint8_t* buf, size_t len, pvac_ct_file_info* info);
+/* Decode into X (host arrays sized from pvac_ct_scan; X->n = n_ciphers; X->sigma nullable, else
+ * X->sigma_words >= info.sigma_words). Writes dense CSR l_off/l_cnt/e_off/e_cnt. threads <= 0:
+ * one per hardware thread. PVAC_ENOSYS if edges disagree on sigma nbits. */
+int pvac_ct_parse(const uint8_t* buf, size_t len, pvac_ct_batch* X, int threads);
+/* Bytes pvac_ct_write produces for X; sigma_bits is written per edge when X->sigma != NULL
+ * (the reference writes m_bits = 8192), 0 otherwise. */
+int pvac_ct_serialized_size(const pvac_ct_batch* X, uint32_t sigma_bits, uint64_t* bytes);
+int pvac_ct_write(const pvac_ct_batch* X, uint32_t sigma_bits, uint8_t* out, size_t capacity, uint64_t* written,
+                  int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -89,6 +89,10 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_fill_random": ([vp, u64, vp, C.c_size_t], i32),
         "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_bucket_count": ([u64], u64),
+        "pvac_ct_scan": ([vp, C.c_size_t, vp], i32),
+        "pvac_ct_parse": ([vp, C.c_size_t, C.POINTER(CtBatch), i32], i32),
+        "pvac_ct_serialized_size": ([C.POINTER(CtBatch), u32, C.POINTER(u64)], i32),
+        "pvac_ct_write": ([C.POINTER(CtBatch), u32, vp, C.c_size_t, C.POINTER(u64), i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

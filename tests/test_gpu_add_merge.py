@@ -133,3 +133,26 @@ def test_exact_cancellations_drop_groups_and_layers(oracle):
     out = eng.ct_add(_dev_batch(eng, [x], True), _dev_batch(eng, [y], True), sigma=True).to_host()[0]
     assert out.nE == 10 and out.nL == 1
     _same(out, oracle.ct_add(x, y, edge_budget=100), sigma=True)
+
+
+def test_codec_interop_gpu():
+    """File -> native codec -> device -> ct_add / ct_sub -> native codec -> file, byte-identical
+    to the reference's own outputs (pair fixtures batched through one multi-cipher image, and
+    bounty2 a.ct + b.ct -> sum.ct)."""
+    from pvac_hfhe_cppbyv_amd import Engine, codec
+    from helpers import GOLD
+    eng = Engine(device=0)
+    xs = [codec.read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0] for p in range(8)]
+    ys = [codec.read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0] for p in range(8)]
+    A = codec.load_ct(codec.write_ct(xs), eng.device)
+    B = codec.load_ct(codec.write_ct(ys), eng.device)
+    for op, neg in (("add", False), ("sub", True)):
+        out = eng.ct_add(A, B, negate=neg, sigma=True)
+        for p, c in enumerate(out.to_host()):
+            with open(os.path.join(REF, f"pair{p}_{op}.ct"), "rb") as f:
+                assert codec.write_ct([c]) == f.read(), (op, p)
+    a = codec.load_ct(os.path.join(GOLD, "bounty", "a.ct"), eng.device)
+    b = codec.load_ct(os.path.join(GOLD, "bounty", "b.ct"), eng.device)
+    s = eng.ct_add(a, b, sigma=True)
+    with open(os.path.join(GOLD, "bounty", "sum.ct"), "rb") as f:
+        assert codec.write_ct(s.to_host()) == f.read()
