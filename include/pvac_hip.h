@@ -43,6 +43,7 @@ extern "C" {
 #define PVAC_FP_MUL 2
 #define PVAC_FP_NEG 3   /* b ignored */
 #define PVAC_FP_SCALE 4 /* b is ONE element, broadcast: c[i] = a[i] * b[0] */
+#define PVAC_FP_INV 5   /* fp_inv (field.hpp:229-273) = a^(p-2), inv(0) = 0; b ignored */
 
 /* ct_mul flags */
 #define PVAC_MUL_WITH_SIGMA 0x1u      /* also generate per-edge sigma (crypto/matrix.hpp:267-303) */
@@ -194,6 +195,20 @@ int pvac_hip_fill_random(pvac_hip_ctx* ctx, uint64_t seed, uint64_t* out, size_t
 uint64_t pvac_hip_bucket_count(uint64_t n);
 /* per-cipher FNV-1a digest over (meta, w_lo, w_hi) of its edges in order (device out[n]). */
 int pvac_hip_batch_digest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
+
+/* ---------------------------------------------------------------- decryption
+ * dec_value (ops/decrypt.hpp:12-89) over a batch, given the BASE-layer R values (prf_R of each
+ * BASE layer's seed under the secret key, crypto/lpn.hpp): R of every other layer is the product
+ * of its parents' (layer_R_cached), inverses are fp_inv (field.hpp:229-273), and
+ * dec = sum(+/- w * powg_B[idx] * R[layer]^-1), + for SGN_P. Bit-identical to the reference.
+ * set_powg: pk.powg_B as `count` >= B (lo, hi) pairs in HOST memory.
+ * R_base: device, 2 words per layer SLOT of X (parallel to X->layers; read for BASE layers only).
+ * out: device, 2 words (lo, hi) per cipher. status: device u32 per cipher: 0 ok; 1 the layer
+ * graph has a cycle or an out-of-range parent (the reference aborts); 2 an edge references a
+ * layer or idx out of range (out-of-bounds reads in the reference). out is undefined unless 0. */
+int pvac_hip_ctx_set_powg(pvac_hip_ctx* ctx, const uint64_t* powg_host, uint32_t count);
+int pvac_hip_dec_value(pvac_hip_ctx* ctx, const pvac_ct_batch* X, const uint64_t* R_base, uint64_t* out,
+                       uint32_t* status);
 
 /* ---------------------------------------------------------------- .ct codec (host memory)
  * The reference's ciphertext file format (tests/add.cpp:22-155: saveCts / loadCts, putLayer,

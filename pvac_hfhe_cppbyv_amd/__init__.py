@@ -24,7 +24,7 @@ _LIB_PATH = os.path.join(_HERE, "lib", "libpvac_hip.so")
 LAYER_DT = np.dtype([("rule", "<u4"), ("pa", "<u4"), ("pb", "<u4"), ("pad", "<u4"),
                      ("ztag", "<u8"), ("nonce_lo", "<u8"), ("nonce_hi", "<u8")])
 
-FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE = 0, 1, 2, 3, 4
+FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE, FP_INV = 0, 1, 2, 3, 4, 5
 MUL_WITH_SIGMA, MUL_ORDER_CANONICAL = 0x1, 0x2
 
 P = (1 << 127) - 1
@@ -89,6 +89,8 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_fill_random": ([vp, u64, vp, C.c_size_t], i32),
         "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_bucket_count": ([u64], u64),
+        "pvac_hip_ctx_set_powg": ([vp, vp, u32], i32),
+        "pvac_hip_dec_value": ([vp, C.POINTER(CtBatch), vp, vp, vp], i32),
         "pvac_ct_scan": ([vp, C.c_size_t, vp], i32),
         "pvac_ct_parse": ([vp, C.c_size_t, C.POINTER(CtBatch), i32], i32),
         "pvac_ct_serialized_size": ([C.POINTER(CtBatch), u32, C.POINTER(u64)], i32),
@@ -233,6 +235,27 @@ class Engine:
         self._check(self.lib.pvac_hip_fp_binop(self.ctx, op, p(a_lo), p(a_hi), p(b_lo), p(b_hi), p(c_lo), p(c_hi),
                                                n))
         return c_lo, c_hi
+
+    # ---- decryption (ops/decrypt.hpp:12-89)
+    def set_powg(self, powg):
+        """pk.powg_B: u64 array of B (lo, hi) pairs (host)."""
+        a = np.ascontiguousarray(np.asarray(powg, dtype=np.uint64).reshape(-1))
+        self._check(self.lib.pvac_hip_ctx_set_powg(self.ctx, C.c_void_p(a.ctypes.data), len(a) // 2))
+
+    def dec_value(self, X: DeviceBatch, R_base):
+        """R_base: 2 u64 per layer slot of X (host array or device tensor; BASE entries used).
+        Returns (values: list[int], status: numpy u32 per cipher)."""
+        torch = self.torch
+        if isinstance(R_base, np.ndarray):
+            R_base = _t(np.ascontiguousarray(R_base, np.uint64)).to(self.device)
+        out = torch.zeros(2 * max(X.n, 1), dtype=torch.int64, device=self.device)
+        status = torch.zeros(max(X.n, 1), dtype=torch.int32, device=self.device)
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_dec_value(self.ctx, C.byref(sx), C.c_void_p(R_base.data_ptr()),
+                                                C.c_void_p(out.data_ptr()), C.c_void_p(status.data_ptr())))
+        o = out.cpu().numpy().view(np.uint64)
+        vals = [int(o[2 * i]) | (int(o[2 * i + 1]) << 64) for i in range(X.n)]
+        return vals, status.cpu().numpy().view(np.uint32)[: X.n]
 
     # ---- ciphertext ops
     def ct_mul_plan(self, A: DeviceBatch, B: DeviceBatch):

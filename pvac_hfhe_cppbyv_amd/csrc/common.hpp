@@ -159,6 +159,12 @@ hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st);
 // args_dev: device copy of `a` (the kernel reads its arguments from memory, see k_mul_fresh.hip)
 hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* args_dev, int num_cus, hipStream_t st);
 
+// ---- dec_value (k_dec.hip): BASE-layer R supplied, PROD R tree, inversions, signed edge sum
+size_t dec_scratch_bytes(uint64_t total_layers);
+hipError_t launch_dec_value(const pvac_ct_batch& X, const uint64_t* Rbase, const uint64_t* powg, uint32_t Bm,
+                            const uint64_t* roff, uint64_t total_layers, void* scratch, uint64_t* out,
+                            uint32_t* status, hipStream_t st);
+
 // ---- ct_add / ct_sub over edge_budget (k_add_merge.hip): compact_edges + compact_layers per pair
 struct merge_pair_info {
     uint64_t pair, aeo, beo, ceo, nA, nB;

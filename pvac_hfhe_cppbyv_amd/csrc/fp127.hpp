@@ -219,6 +219,28 @@ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
     return fp{join32(y0, y1), join32(y2, y3)};
 }
 
+// field.hpp:229-273 fp_inv = a^(p-2) (fp_inv_ct's windowed ladder). The power is unique, so any
+// exact chain is bit-identical: a Mersenne addition chain x_k = a^(2^k - 1),
+// a^(p-2) = a^(2^127 - 3) = (x_125)^4 * a: 126 squarings + 11 multiplies; fp_inv(0) = 0.
+__device__ __forceinline__ fp fp_sqr_n(fp x, int n) {
+    for (int i = 0; i < n; ++i) x = fp_mul(x, x);
+    return x;
+}
+__device__ __forceinline__ fp fp_inv(const fp& a) {
+    const fp x1 = a;
+    const fp x2 = fp_mul(fp_sqr_n(x1, 1), x1);
+    const fp x3 = fp_mul(fp_sqr_n(x2, 1), x1);
+    const fp x6 = fp_mul(fp_sqr_n(x3, 3), x3);
+    const fp x12 = fp_mul(fp_sqr_n(x6, 6), x6);
+    const fp x24 = fp_mul(fp_sqr_n(x12, 12), x12);
+    const fp x48 = fp_mul(fp_sqr_n(x24, 24), x24);
+    const fp x96 = fp_mul(fp_sqr_n(x48, 48), x48);
+    const fp x120 = fp_mul(fp_sqr_n(x96, 24), x24);
+    const fp x123 = fp_mul(fp_sqr_n(x120, 3), x3);
+    const fp x125 = fp_mul(fp_sqr_n(x123, 2), x2);
+    return fp_mul(fp_sqr_n(x125, 2), x1);
+}
+
 // canonical representative of any 128-bit word pair (fp_from_words, field.hpp:26-48)
 __device__ __forceinline__ fp fp_canon(uint64_t lo, uint64_t hi) { return fp_from_words(lo, hi); }
 

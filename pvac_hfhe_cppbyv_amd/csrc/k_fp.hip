@@ -17,6 +17,7 @@ __device__ __forceinline__ fp apply(const fp& a, const fp& b) {
     if constexpr (OP == PVAC_FP_ADD) return fp_add(a, b);
     else if constexpr (OP == PVAC_FP_SUB) return fp_sub(a, b);
     else if constexpr (OP == PVAC_FP_NEG) return fp_neg(a);
+    else if constexpr (OP == PVAC_FP_INV) return fp_inv(a);
     else return fp_mul(a, b);   // MUL and SCALE
 }
 
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(kFpBlock) void k_fp_binop_vec(const ulonglong2* __r
             if (v < nvec) {
                 al[u] = alo[v];
                 ah[u] = ahi[v];
-                if constexpr (OP != PVAC_FP_NEG && OP != PVAC_FP_SCALE) {
+                if constexpr (OP != PVAC_FP_NEG && OP != PVAC_FP_SCALE && OP != PVAC_FP_INV) {
                     bl[u] = blo[v];
                     bh[u] = bhi[v];
                 }
@@ -52,7 +53,7 @@ __global__ __launch_bounds__(kFpBlock) void k_fp_binop_vec(const ulonglong2* __r
                 fp b0, b1;
                 if constexpr (OP == PVAC_FP_SCALE) {
                     b0 = fp{slo, shi}; b1 = b0;
-                } else if constexpr (OP == PVAC_FP_NEG) {
+                } else if constexpr (OP == PVAC_FP_NEG || OP == PVAC_FP_INV) {
                     b0 = fp{0, 0}; b1 = b0;
                 } else {
                     b0 = fp{bl[u].x, bh[u].x}; b1 = fp{bl[u].y, bh[u].y};
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(kFpBlock) void k_fp_binop_scalar(const uint64_t* al
     for (size_t i = lo_idx + (size_t)blockIdx.x * kFpBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kFpBlock) {
         fp b{0, 0};
         if constexpr (OP == PVAC_FP_SCALE) b = fp{blo[0], bhi[0]};
-        else if constexpr (OP != PVAC_FP_NEG) b = fp{blo[i], bhi[i]};
+        else if constexpr (OP != PVAC_FP_NEG && OP != PVAC_FP_INV) b = fp{blo[i], bhi[i]};
         const fp r = apply<OP>(fp{alo[i], ahi[i]}, b);
         clo[i] = r.lo;
         chi[i] = r.hi;
@@ -85,7 +86,8 @@ hipError_t run_binop(const uint64_t* alo, const uint64_t* ahi, const uint64_t* b
                      uint64_t* chi, size_t n, hipStream_t st) {
     auto aligned = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
     bool vec_ok = aligned(alo) && aligned(ahi) && aligned(clo) && aligned(chi);
-    if constexpr (OP != PVAC_FP_NEG && OP != PVAC_FP_SCALE) vec_ok = vec_ok && aligned(blo) && aligned(bhi);
+    if constexpr (OP != PVAC_FP_NEG && OP != PVAC_FP_SCALE && OP != PVAC_FP_INV)
+        vec_ok = vec_ok && aligned(blo) && aligned(bhi);
     size_t done = 0;
     if (vec_ok && n >= 2) {
         const size_t nvec = n / 2;
@@ -218,6 +220,7 @@ hipError_t launch_fp_binop(int op, const uint64_t* alo, const uint64_t* ahi, con
         case PVAC_FP_MUL: return run_binop<PVAC_FP_MUL>(alo, ahi, blo, bhi, clo, chi, n, st);
         case PVAC_FP_NEG: return run_binop<PVAC_FP_NEG>(alo, ahi, blo, bhi, clo, chi, n, st);
         case PVAC_FP_SCALE: return run_binop<PVAC_FP_SCALE>(alo, ahi, blo, bhi, clo, chi, n, st);
+        case PVAC_FP_INV: return run_binop<PVAC_FP_INV>(alo, ahi, blo, bhi, clo, chi, n, st);
         default: return hipErrorInvalidValue;
     }
 }

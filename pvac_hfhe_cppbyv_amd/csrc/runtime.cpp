@@ -47,6 +47,12 @@ struct pvac_hip_ctx {
     void* merge_scratch = nullptr;
     size_t merge_cap = 0;
     unsigned long long* merge_counters = nullptr;
+    uint64_t* powg = nullptr;          // pk.powg_B on the device, B x (lo, hi)
+    uint32_t powg_n = 0;
+    void* dec_scratch = nullptr;
+    size_t dec_cap = 0;
+    uint64_t* dec_roff = nullptr;
+    size_t dec_roff_cap = 0;
     uint64_t* large_ids = nullptr;
     uint64_t* large_info = nullptr;
     size_t pair_cap = 0;
@@ -311,6 +317,9 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->fresh_args);
     hipFree(c->merge_scratch);
     hipFree(c->merge_counters);
+    hipFree(c->powg);
+    hipFree(c->dec_scratch);
+    hipFree(c->dec_roff);
     hipFree(c->scan_scratch);
     hipFree(c->stats);
     hipFree(c->totals);
@@ -370,9 +379,9 @@ int pvac_hip_timing_reset(pvac_hip_ctx* c) {
 int pvac_hip_fp_binop(pvac_hip_ctx* c, int op, const uint64_t* a_lo, const uint64_t* a_hi, const uint64_t* b_lo,
                       const uint64_t* b_hi, uint64_t* c_lo, uint64_t* c_hi, size_t n) {
     if (!c) return PVAC_EINVAL;
-    if (op < PVAC_FP_ADD || op > PVAC_FP_SCALE) return fail(c, PVAC_EINVAL, "fp_binop: bad op");
+    if (op < PVAC_FP_ADD || op > PVAC_FP_INV) return fail(c, PVAC_EINVAL, "fp_binop: bad op");
     if (n && (!a_lo || !a_hi || !c_lo || !c_hi)) return fail(c, PVAC_EINVAL, "fp_binop: null array");
-    if (n && op != PVAC_FP_NEG && (!b_lo || !b_hi)) return fail(c, PVAC_EINVAL, "fp_binop: null b");
+    if (n && op != PVAC_FP_NEG && op != PVAC_FP_INV && (!b_lo || !b_hi)) return fail(c, PVAC_EINVAL, "fp_binop: null b");
     scoped_timer t(c, "fp_binop");
     return hip_fail(c, launch_fp_binop(op, a_lo, a_hi, b_lo, b_hi, c_lo, c_hi, n, c->stream), "fp_binop");
 }
@@ -708,6 +717,51 @@ int pvac_hip_sigma_batch(pvac_hip_ctx* c, pvac_ct_batch* X, const uint64_t* salt
     if (!c->H.ready) return fail(c, PVAC_EINVAL, "sigma_batch: H not set");
     scoped_timer t(c, "sigma");
     return hip_fail(c, launch_sigma(c->H, c->prm, *X, salts, nullptr, c->num_cus, c->stream), "sigma");
+}
+
+// ---------------------------------------------------------------- dec_value
+int pvac_hip_ctx_set_powg(pvac_hip_ctx* c, const uint64_t* powg_host, uint32_t count) {
+    if (!c || !powg_host || count < c->prm.B) return fail(c, PVAC_EINVAL, "set_powg: need B (lo, hi) pairs");
+    hipFree(c->powg);
+    c->powg = nullptr;
+    c->powg_n = 0;
+    hipError_t e = hipMalloc(&c->powg, (size_t)count * 16);
+    if (e == hipSuccess) e = hipMemcpy(c->powg, powg_host, (size_t)count * 16, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(c, e, "set_powg");
+    c->powg_n = count;
+    return PVAC_OK;
+}
+
+int pvac_hip_dec_value(pvac_hip_ctx* c, const pvac_ct_batch* X, const uint64_t* R_base, uint64_t* out,
+                       uint32_t* status) {
+    if (!c || !batch_ok(X) || !out || !status || (X->n && !R_base)) return fail(c, PVAC_EINVAL, "dec_value: arguments");
+    if (!c->powg) return fail(c, PVAC_EINVAL, "dec_value: powg_B not set (pvac_hip_ctx_set_powg)");
+    if (!X->n) return PVAC_OK;
+    int rc = ensure_pairs(c, X->n);
+    if (rc) return rc;
+    rc = ensure_dev(c, c->dec_roff, c->dec_roff_cap, X->n, "alloc dec offsets");
+    if (rc) return rc;
+    // dense per-cipher layer offsets (the batch may be capacity-padded)
+    hipError_t e = hipMemcpyAsync(c->dec_roff, X->l_cnt, X->n * 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = launch_exclusive_scan_u64(c->dec_roff, X->n, c->scan_scratch, &c->totals[0], c->stream);
+    unsigned long long total = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&total, &c->totals[0], 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "dec_value (offsets)");
+    const size_t need = dec_scratch_bytes(total);
+    if (need > c->dec_cap) {
+        hipFree(c->dec_scratch);
+        c->dec_scratch = nullptr;
+        c->dec_cap = 0;
+        e = hipMalloc(&c->dec_scratch, need);
+        if (e != hipSuccess) return hip_fail(c, e, "alloc dec scratch");
+        c->dec_cap = need;
+    }
+    scoped_timer t(c, "dec_value");
+    return hip_fail(c,
+                    launch_dec_value(*X, R_base, c->powg, c->prm.B, c->dec_roff, total, c->dec_scratch, out, status,
+                                     c->stream),
+                    "dec_value");
 }
 
 // ---------------------------------------------------------------- synthetic / checks
