@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <cmath>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -337,6 +338,271 @@ void sigma_of(const orc_params* prm, const u64* H, u64 ztag, u64 nlo, u64 nhi, u
         out[(size_t)r >> 6] ^= 1ULL << (r & 63);
 }
 
+// ------------------------------------------------------------------ LPN PRF (crypto/lpn.hpp)
+// AES-256 (FIPS-197), byte-oriented: SubBytes / ShiftRows / MixColumns / AddRoundKey.
+const uint8_t kSbox[256] = {
+    0x63,0x7c,0x77,0x7b,0xf2,0x6b,0x6f,0xc5,0x30,0x01,0x67,0x2b,0xfe,0xd7,0xab,0x76,0xca,0x82,0xc9,0x7d,0xfa,0x59,0x47,0xf0,
+    0xad,0xd4,0xa2,0xaf,0x9c,0xa4,0x72,0xc0,0xb7,0xfd,0x93,0x26,0x36,0x3f,0xf7,0xcc,0x34,0xa5,0xe5,0xf1,0x71,0xd8,0x31,0x15,
+    0x04,0xc7,0x23,0xc3,0x18,0x96,0x05,0x9a,0x07,0x12,0x80,0xe2,0xeb,0x27,0xb2,0x75,0x09,0x83,0x2c,0x1a,0x1b,0x6e,0x5a,0xa0,
+    0x52,0x3b,0xd6,0xb3,0x29,0xe3,0x2f,0x84,0x53,0xd1,0x00,0xed,0x20,0xfc,0xb1,0x5b,0x6a,0xcb,0xbe,0x39,0x4a,0x4c,0x58,0xcf,
+    0xd0,0xef,0xaa,0xfb,0x43,0x4d,0x33,0x85,0x45,0xf9,0x02,0x7f,0x50,0x3c,0x9f,0xa8,0x51,0xa3,0x40,0x8f,0x92,0x9d,0x38,0xf5,
+    0xbc,0xb6,0xda,0x21,0x10,0xff,0xf3,0xd2,0xcd,0x0c,0x13,0xec,0x5f,0x97,0x44,0x17,0xc4,0xa7,0x7e,0x3d,0x64,0x5d,0x19,0x73,
+    0x60,0x81,0x4f,0xdc,0x22,0x2a,0x90,0x88,0x46,0xee,0xb8,0x14,0xde,0x5e,0x0b,0xdb,0xe0,0x32,0x3a,0x0a,0x49,0x06,0x24,0x5c,
+    0xc2,0xd3,0xac,0x62,0x91,0x95,0xe4,0x79,0xe7,0xc8,0x37,0x6d,0x8d,0xd5,0x4e,0xa9,0x6c,0x56,0xf4,0xea,0x65,0x7a,0xae,0x08,
+    0xba,0x78,0x25,0x2e,0x1c,0xa6,0xb4,0xc6,0xe8,0xdd,0x74,0x1f,0x4b,0xbd,0x8b,0x8a,0x70,0x3e,0xb5,0x66,0x48,0x03,0xf6,0x0e,
+    0x61,0x35,0x57,0xb9,0x86,0xc1,0x1d,0x9e,0xe1,0xf8,0x98,0x11,0x69,0xd9,0x8e,0x94,0x9b,0x1e,0x87,0xe9,0xce,0x55,0x28,0xdf,
+    0x8c,0xa1,0x89,0x0d,0xbf,0xe6,0x42,0x68,0x41,0x99,0x2d,0x0f,0xb0,0x54,0xbb,0x16};
+
+inline uint8_t xt(uint8_t b) { return (uint8_t)((b << 1) ^ ((b & 0x80) ? 0x1b : 0)); }
+
+struct Aes256 {
+    uint8_t rk[15][16];
+    void init(const uint8_t key[32]) {
+        uint8_t w[60][4];
+        for (int i = 0; i < 8; ++i) for (int j = 0; j < 4; ++j) w[i][j] = key[4 * i + j];
+        uint8_t rcon = 1;
+        for (int i = 8; i < 60; ++i) {
+            uint8_t t[4] = {w[i - 1][0], w[i - 1][1], w[i - 1][2], w[i - 1][3]};
+            if (i % 8 == 0) {
+                const uint8_t t0 = t[0];
+                t[0] = kSbox[t[1]] ^ rcon; t[1] = kSbox[t[2]]; t[2] = kSbox[t[3]]; t[3] = kSbox[t0];
+                rcon = xt(rcon);
+            } else if (i % 8 == 4) {
+                for (auto& b : t) b = kSbox[b];
+            }
+            for (int j = 0; j < 4; ++j) w[i][j] = w[i - 8][j] ^ t[j];
+        }
+        for (int r = 0; r < 15; ++r) for (int c = 0; c < 4; ++c) for (int j = 0; j < 4; ++j) rk[r][4 * c + j] = w[4 * r + c][j];
+    }
+    void encrypt(uint8_t s[16]) const {   // s[4c + r] = row r of column c
+        for (int i = 0; i < 16; ++i) s[i] ^= rk[0][i];
+        for (int r = 1; r <= 14; ++r) {
+            uint8_t t[16];
+            for (int c = 0; c < 4; ++c)
+                for (int row = 0; row < 4; ++row) t[4 * c + row] = kSbox[s[4 * ((c + row) & 3) + row]];   // Sub+Shift
+            if (r < 14)
+                for (int c = 0; c < 4; ++c) {   // MixColumns
+                    const uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+                    t[4 * c] = xt(a0) ^ (xt(a1) ^ a1) ^ a2 ^ a3;
+                    t[4 * c + 1] = a0 ^ xt(a1) ^ (xt(a2) ^ a2) ^ a3;
+                    t[4 * c + 2] = a0 ^ a1 ^ xt(a2) ^ (xt(a3) ^ a3);
+                    t[4 * c + 3] = (xt(a0) ^ a0) ^ a1 ^ a2 ^ xt(a3);
+                }
+            for (int i = 0; i < 16; ++i) s[i] = t[i] ^ rk[r][i];
+        }
+    }
+};
+
+// crypto/lpn.hpp:41-147 AesCtr256: counter block = le64(nonce + i) || 0^64, u64 stream with a
+// one-word buffer, rejection-bounded draws.
+struct Ctr {
+    Aes256 aes;
+    u64 ctr = 0, buf = 0;
+    bool has = false;
+    void init(const uint8_t key[32], u64 nonce) { aes.init(key); ctr = nonce; has = false; }
+    u64 next() {
+        if (has) { has = false; return buf; }
+        uint8_t b[16] = {0};
+        for (int i = 0; i < 8; ++i) b[i] = (uint8_t)(ctr >> (8 * i));
+        ++ctr;
+        aes.encrypt(b);
+        buf = le64(b + 8);
+        has = true;
+        return le64(b);
+    }
+    u64 bounded(u64 M) {
+        if (M <= 1) return 0;
+        const u64 lim = ~0ULL - (~0ULL % M);
+        for (;;) { const u64 x = next(); if (x < lim) return x % M; }
+    }
+};
+
+u64 fnv1a(const char* d) {   // lpn.hpp:150-157
+    u64 h = 0xcbf29ce484222325ull;
+    for (const char* p = d; *p; ++p) { h ^= (uint8_t)*p; h *= 0x100000001b3ull; }
+    return h;
+}
+
+// lpn.hpp:159-186
+void derive_key(const orc_secret* sk, u64 canon, u64 ztag, u64 nlo, u64 nhi, const char* dom, uint8_t key[32],
+                u64& nonce) {
+    Sha h; h.begin();
+    for (int i = 0; i < 4; ++i) h.feed64(sk->prf_k[i]);
+    h.feed64(canon);
+    h.feed(sk->H_digest, 32);
+    h.feed64(ztag); h.feed64(nlo); h.feed64(nhi);
+    const u64 dh = fnv1a(dom);
+    h.feed64(dh);
+    h.end(key);
+    nonce = dh ^ nlo;
+}
+
+inline int parity(u64 x) { return __builtin_parityll(x); }
+
+const char* const kDoms[6] = {"pvac.prf.r.1", "pvac.prf.r.2", "pvac.prf.r.3",
+                              "pvac.prf.noise.1", "pvac.prf.noise.2", "pvac.prf.noise.3"};
+
+// lpn.hpp:188-261 prf_R_core. toep_127 keeps the low 127 coefficients of ybits x top over GF(2),
+// and coefficient j only involves coefficients <= j of either factor, so rows >= 127 of the LPN
+// stream never reach the output: rows = 127 is exact. full_rows = 1 runs all lpn_t rows.
+F prf_core(const orc_secret* sk, u64 canon, u64 ztag, u64 nlo, u64 nhi, const char* dom, bool full_rows) {
+    const uint32_t sw = (sk->lpn_n + 63) / 64;
+    uint8_t key[32];
+    u64 nonce;
+    derive_key(sk, canon, ztag, nlo, nhi, dom, key, nonce);
+    Ctr prg;
+    prg.init(key, nonce);
+    const uint32_t rows = full_rows ? sk->lpn_t : std::min<uint32_t>(sk->lpn_t, 127);
+    u64 y[2] = {0, 0};
+    for (uint32_t r = 0; r < rows; ++r) {
+        u64 acc = 0;
+        for (uint32_t w = 0; w < sw; ++w) acc ^= prg.next() & sk->lpn_s[w];
+        const int e = prg.bounded(sk->tau_den) < sk->tau_num ? 1 : 0;
+        if (r < 128) y[r >> 6] |= (u64)(parity(acc) ^ e) << (r & 63);
+    }
+    uint8_t tk[32];
+    u64 tn;
+    derive_key(sk, canon, ztag, nlo, nhi, "pvac.dom.toeplitz", tk, tn);
+    tn ^= fnv1a(dom);
+    Ctr tp;
+    tp.init(tk, tn);
+    const u64 t0 = tp.next(), t1 = tp.next();
+    // low 127 bits of y * top (carry-less)
+    u64 lo = 0, hi = 0;
+    for (int i = 0; i < 127; ++i) {
+        if (!((y[i >> 6] >> (i & 63)) & 1)) continue;
+        if (i == 0) { lo ^= t0; hi ^= t1; }
+        else if (i < 64) { lo ^= t0 << i; hi ^= (t1 << i) | (t0 >> (64 - i)); }
+        else if (i == 64) { hi ^= t0; }
+        else { hi ^= t0 << (i - 64); }
+    }
+    hi &= 0x7FFFFFFFFFFFFFFFull;
+    F r = from_words(lo, hi);   // hash_to_fp_nonzero (lpn.hpp:25-37)
+    if (!(r.lo | r.hi)) r = F{1, 0};
+    return r;
+}
+
+F prf_R(const orc_secret* sk, u64 canon, u64 z, u64 lo, u64 hi) {   // lpn.hpp:263-268
+    return mul(mul(prf_core(sk, canon, z, lo, hi, kDoms[0], false), prf_core(sk, canon, z, lo, hi, kDoms[1], false)),
+               prf_core(sk, canon, z, lo, hi, kDoms[2], false));
+}
+F prf_R_noise(const orc_secret* sk, u64 canon, u64 z, u64 lo, u64 hi) {   // lpn.hpp:270-275
+    return mul(mul(prf_core(sk, canon, z, lo, hi, kDoms[3], false), prf_core(sk, canon, z, lo, hi, kDoms[4], false)),
+               prf_core(sk, canon, z, lo, hi, kDoms[5], false));
+}
+// ops/encrypt.hpp:113-128
+F prf_noise_delta(const orc_secret* sk, u64 canon, u64 z, u64 lo, u64 hi, uint32_t group, uint32_t kind) {
+    const u64 g = (u64)group + 1, k = (u64)kind + 1;
+    lo ^= 0x9e3779b97f4a7c15ull * g;
+    hi ^= 0x94d049bb133111ebull * g;
+    z ^= 0x517cc1b727220a95ull * g;
+    lo ^= k;
+    hi ^= k << 32;
+    z ^= k << 48;
+    return prf_R_noise(sk, canon, z, lo, hi);
+}
+
+// ------------------------------------------------------------------ enc_value (ops/encrypt.hpp)
+struct Stream {
+    const u64* p;
+    size_t n, i = 0;
+    bool over = false;
+    u64 next() { if (i < n) return p[i++]; over = true; return 0; }
+};
+
+F rand_fp_nonzero(Stream& rs) {   // types.hpp:145-155
+    for (;;) {
+        const u64 lo = rs.next();
+        const u64 hi = rs.next() & 0x7FFFFFFFFFFFFFFFull;
+        const F x = from_words(lo, hi);
+        if ((x.lo | x.hi) || rs.over) return x;
+    }
+}
+
+// ops/encrypt.hpp:162-258 enc_fp_depth
+Ct enc_fp_depth(const orc_params* prm, const orc_secret* sk, const u64* H, const u64* powg, const F& v, int Z2, int Z3,
+                Stream& rs) {
+    const uint32_t B = prm->B, sw = (prm->m_bits + 63) / 64;
+    auto pg = [&](uint32_t i) { return F{powg[2 * i], powg[2 * i + 1]}; };
+    Ct C;
+    Lyr L{0, 0, 0, 0, 0, 0};
+    L.nlo = rs.next();
+    L.nhi = rs.next();
+    L.ztag = ztag_of(prm->canon_tag, L.nlo, L.nhi);
+    C.L.push_back(L);
+    constexpr int S = 8;
+    int idx[S];
+    uint8_t ch[S];
+    F r[S];
+    std::vector<int> used;
+    for (int j = 0; j < S; ++j) {
+        int x;
+        do { x = (int)(rs.next() % B); } while (std::find(used.begin(), used.end(), x) != used.end() && !rs.over);
+        used.push_back(x);
+        idx[j] = x;
+        ch[j] = (uint8_t)(rs.next() & 1);
+    }
+    F sumg{0, 0};
+    for (int j = 0; j < S - 1; ++j) {
+        r[j] = rand_fp_nonzero(rs);
+        const F term = mul(r[j], pg(idx[j]));
+        sumg = ch[j] == 0 ? add(sumg, term) : sub(sumg, term);
+    }
+    const F r_last = mul(sub(v, sumg), inv(pg(idx[S - 1])));
+    r[S - 1] = ch[S - 1] == 0 ? r_last : neg(r_last);
+    const F R = prf_R(sk, prm->canon_tag, L.ztag, L.nlo, L.nhi);
+    auto edge = [&](uint32_t i, uint8_t c, const F& w) {
+        Edg e{0, (uint16_t)i, c, w, nullptr, {}};
+        const u64 salt = rs.next();
+        if (H) { e.s.assign(sw, 0); sigma_of(prm, H, L.ztag, L.nlo, L.nhi, i, c, salt, e.s.data()); }
+        C.E.push_back(std::move(e));
+    };
+    for (int j = 0; j < S; ++j) edge((uint32_t)idx[j], ch[j], mul(r[j], R));
+    const int total = Z2 + Z3;
+    F dacc{0, 0};
+    int gid = 0;
+    auto next_delta = [&](int left, uint32_t kind) {
+        if (left <= 1) return neg(dacc);
+        const F d = prf_noise_delta(sk, prm->canon_tag, L.ztag, L.nlo, L.nhi, (uint32_t)gid, kind);
+        dacc = add(dacc, d);
+        return d;
+    };
+    for (int t = 0; t < Z2; ++t, ++gid) {
+        const uint32_t i = (uint32_t)(rs.next() % B);
+        uint32_t j;
+        do { j = (uint32_t)(rs.next() % B); } while (j == i && !rs.over);
+        const uint8_t s1 = (uint8_t)(rs.next() & 1), s2 = s1 ^ 1;
+        const F D = next_delta(total - gid, 0);
+        const F Dp = s1 == 0 ? D : neg(D);
+        const F ri = rand_fp_nonzero(rs);
+        const F rj = mul(sub(mul(ri, pg(i)), Dp), inv(pg(j)));
+        edge(i, s1, mul(ri, R));
+        edge(j, s2, mul(rj, R));
+    }
+    for (int t = 0; t < Z3; ++t, ++gid) {
+        const uint32_t i = (uint32_t)(rs.next() % B);
+        uint32_t j, k;
+        do { j = (uint32_t)(rs.next() % B); } while (j == i && !rs.over);
+        do { k = (uint32_t)(rs.next() % B); } while ((k == i || k == j) && !rs.over);
+        const uint8_t s1 = (uint8_t)(rs.next() & 1), s2 = (uint8_t)(rs.next() & 1), s3 = (uint8_t)(rs.next() & 1);
+        const F D = next_delta(total - gid, 1);
+        const F a = rand_fp_nonzero(rs), b = rand_fp_nonzero(rs);
+        F t1 = mul(a, pg(i)), t2 = mul(b, pg(j));
+        if (s1) t1 = neg(t1);
+        if (s2) t2 = neg(t2);
+        const F gk = s3 == 0 ? pg(k) : neg(pg(k));
+        const F c = mul(sub(D, add(t1, t2)), inv(gk));
+        edge(i, s1, mul(a, R));
+        edge(j, s2, mul(b, R));
+        edge(k, s3, mul(c, R));
+    }
+    compact_edges(C, B, sw, H != nullptr);
+    guard(prm, C, sw, H != nullptr);
+    const size_t n = C.E.size();   // shuffle_edges (encrypt.hpp:156-160)
+    for (size_t i = n > 1 ? n - 1 : 0; i > 0; --i) std::swap(C.E[i], C.E[rs.next() % (i + 1)]);
+    return C;
+}
+
 struct MulHash { size_t operator()(u64 x) const noexcept { return x * 0x9E3779B97F4A7C15ull; } };
 
 // ops/arithmetic.hpp:47-106
@@ -549,6 +815,61 @@ void orc_commit_ct(const orc_params* prm, const uint8_t Hd[32], const orc_cipher
 }
 
 // ops/decrypt.hpp:12-89, with BASE-layer R supplied by the caller (fixtures hold them).
+void orc_prf_core(const orc_secret* sk, uint64_t canon, uint64_t z, uint64_t lo, uint64_t hi, int dom, int full,
+                  uint64_t out[2]) {
+    const F r = prf_core(sk, canon, z, lo, hi, kDoms[dom], full != 0);
+    out[0] = r.lo; out[1] = r.hi;
+}
+void orc_prf_R(const orc_secret* sk, uint64_t canon, uint64_t z, uint64_t lo, uint64_t hi, int noise, uint64_t out[2]) {
+    const F r = noise ? prf_R_noise(sk, canon, z, lo, hi) : prf_R(sk, canon, z, lo, hi);
+    out[0] = r.lo; out[1] = r.hi;
+}
+void orc_prf_noise_delta(const orc_secret* sk, uint64_t canon, uint64_t z, uint64_t lo, uint64_t hi, uint32_t g,
+                         uint32_t kind, uint64_t out[2]) {
+    const F r = prf_noise_delta(sk, canon, z, lo, hi, g, kind);
+    out[0] = r.lo; out[1] = r.hi;
+}
+
+// ops/encrypt.hpp:16-27 with the default Params (noise_entropy_bits 120, tuple2_fraction 0.55,
+// depth_slope_bits 16)
+static void plan_noise(uint32_t B, int depth, int& z2, int& z3) {
+    const double budget = 120.0 + 16.0 * std::max(0, depth);
+    const double per2 = 2.0 * std::log2((double)B), per3 = 3.0 * std::log2((double)B);
+    z2 = std::max(0, (int)std::floor((budget * 0.55) / std::max(1e-6, per2)));
+    z3 = std::max(0, (int)std::floor((budget * (1.0 - 0.55)) / std::max(1e-6, per3)));
+    if (z2 + z3 == 1) { if (z3 > 0) ++z3; else ++z2; }
+}
+
+int orc_enc_value(const orc_params* prm, const orc_secret* sk, const uint64_t* H, const uint64_t* powg, uint64_t v,
+                  const uint64_t* stream, size_t n, int order, orc_cipher* out, size_t* consumed) {
+    Stream rs{stream, n};
+    int Z2, Z3;
+    plan_noise(prm->B, 0, Z2, Z3);
+    const F val{v, 0};
+    const F mask = rand_fp_nonzero(rs);   // encrypt.hpp:281-287
+    Ct a, b;
+    if (order == 0) {
+        a = enc_fp_depth(prm, sk, H, powg, add(val, mask), Z2, Z3, rs);
+        b = enc_fp_depth(prm, sk, H, powg, neg(mask), Z2, Z3, rs);
+    } else {
+        b = enc_fp_depth(prm, sk, H, powg, neg(mask), Z2, Z3, rs);
+        a = enc_fp_depth(prm, sk, H, powg, add(val, mask), Z2, Z3, rs);
+    }
+    // combine_ciphers (encrypt.hpp:260-279)
+    Ct C;
+    C.L = a.L;
+    const uint32_t off = (uint32_t)a.L.size();
+    for (Lyr L : b.L) { if (L.rule == 1) { L.pa += off; L.pb += off; } C.L.push_back(L); }
+    C.E = std::move(a.E);
+    for (auto& e : b.E) { e.layer += off; C.E.push_back(std::move(e)); }
+    const uint32_t sw = (prm->m_bits + 63) / 64;
+    guard(prm, C, sw, H != nullptr);
+    compact_layers(C);
+    if (consumed) *consumed = rs.i;
+    if (rs.over) return -1;
+    return store(C, out, H ? sw : 0) ? -2 : 0;
+}
+
 void orc_dec_value(const orc_params* prm, const uint64_t* powg, const orc_cipher* C, const uint64_t* R_base,
                    uint64_t out[2]) {
     const u64 L = C->nL;

@@ -45,6 +45,14 @@ typedef struct orc_cipher {
     uint32_t sigma_words;
 } orc_cipher;
 
+/* secret-key material of the LPN PRF (crypto/lpn.hpp; SecKey core/types.hpp:134-137) */
+typedef struct orc_secret {
+    uint64_t prf_k[4];
+    const uint64_t* lpn_s;   /* ceil(lpn_n / 64) words */
+    uint32_t lpn_n, lpn_t, tau_num, tau_den;
+    uint8_t H_digest[32];
+} orc_secret;
+
 /* ---- Fp over p = 2^127-1 (core/field.hpp) ---- */
 void orc_fp_from_words(const uint64_t* lo, const uint64_t* hi, uint64_t* olo, uint64_t* ohi, size_t n);
 void orc_fp_add(const uint64_t* alo, const uint64_t* ahi, const uint64_t* blo, const uint64_t* bhi,
@@ -81,6 +89,21 @@ void orc_commit_ct(const orc_params* prm, const uint8_t H_digest[32], const orc_
 /* dec_value with caller-provided BASE-layer R values (ops/decrypt.hpp:12-89) */
 void orc_dec_value(const orc_params* prm, const uint64_t* powg /*B x 2*/, const orc_cipher* C,
                    const uint64_t* R_base /* nL x 2, PROD entries ignored */, uint64_t out[2]);
+/* ---- LPN PRF and encryption (crypto/lpn.hpp, ops/encrypt.hpp) ----
+ * dom: 0..5 = pvac.prf.r.1..3, pvac.prf.noise.1..3. full_rows = 0 evaluates the 127 LPN rows that
+ * reach toep_127's output, 1 all lpn_t rows (the reference's loop). */
+void orc_prf_core(const orc_secret* sk, uint64_t canon, uint64_t ztag, uint64_t nlo, uint64_t nhi, int dom,
+                  int full_rows, uint64_t out[2]);
+void orc_prf_R(const orc_secret* sk, uint64_t canon, uint64_t ztag, uint64_t nlo, uint64_t nhi, int noise,
+               uint64_t out[2]);
+void orc_prf_noise_delta(const orc_secret* sk, uint64_t canon, uint64_t ztag, uint64_t nlo, uint64_t nhi,
+                         uint32_t group, uint32_t kind, uint64_t out[2]);
+/* enc_value (ops/encrypt.hpp:281-287) driven by `stream` (the csprng_u64 draws, in order). H_dense
+ * NULL: weights only. order: 0 = combine_ciphers' first argument is evaluated first, 1 = second.
+ * Returns 0 ok, -1 stream exhausted, -2 capacity. *consumed = draws used. */
+int orc_enc_value(const orc_params* prm, const orc_secret* sk, const uint64_t* H_dense, const uint64_t* powg,
+                  uint64_t v, const uint64_t* stream, size_t stream_len, int order, orc_cipher* out,
+                  size_t* consumed);
 /* libstdc++ bucket count after unordered_map::reserve(n) (the emit-order pin) */
 uint64_t orc_bucket_count_after_reserve(uint64_t n);
 

@@ -417,6 +417,72 @@ static void cmd_time_mul(int npairs, int threads) {
                 npairs, threads, s, npairs / s, et);
 }
 
+// ---- f2 fixtures: key material, prf_R_core / prf_R / prf_noise_delta on seeded seeds, and
+//      complete enc_value outputs with the exact getrandom stream each consumed.
+static void cmd_enc(const std::string& dir, int nenc) {
+    reseed(0x5EED0C00ULL);   // the same key as cmd_fixtures
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    g_logging = true;
+    write_u64(dir + "/sk_prf_k.u64", std::vector<uint64_t>(sk.prf_k.begin(), sk.prf_k.end()));
+    write_u64(dir + "/sk_lpn_s.u64", sk.lpn_s_bits);
+    auto zz = plan_noise(pk, 0);
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ",\n  \"lpn_n\": " << prm.lpn_n << ", \"lpn_t\": " << prm.lpn_t
+       << ", \"lpn_tau_num\": " << prm.lpn_tau_num << ", \"lpn_tau_den\": " << prm.lpn_tau_den
+       << ",\n  \"Z2\": " << zz.first << ", \"Z3\": " << zz.second << ",\n";
+    // prf outputs: per seed {ztag, nonce lo, hi} then R1 R2 R3 N1 N2 N3 (prf_R_core), prf_R,
+    // prf_R_noise, prf_noise_delta(group 0..4, kind 0) and (group 0..4, kind 1): 2 words each
+    reseed(0x5EED0E00ULL);
+    g_logging = false;
+    const char* doms[] = {Dom::PRF_R1, Dom::PRF_R2, Dom::PRF_R3, Dom::PRF_NOISE1, Dom::PRF_NOISE2, Dom::PRF_NOISE3};
+    std::vector<uint64_t> seeds, outs;
+    const int nseed = 12;
+    for (int k = 0; k < nseed; ++k) {
+        RSeed sd;
+        sd.ztag = splitmix64_next();
+        sd.nonce.lo = splitmix64_next();
+        sd.nonce.hi = splitmix64_next();
+        seeds.push_back(sd.ztag); seeds.push_back(sd.nonce.lo); seeds.push_back(sd.nonce.hi);
+        for (const char* d : doms) { Fp r = prf_R_core(pk, sk, sd, d); outs.push_back(r.lo); outs.push_back(r.hi); }
+        Fp R = prf_R(pk, sk, sd), N = prf_R_noise(pk, sk, sd);
+        outs.push_back(R.lo); outs.push_back(R.hi); outs.push_back(N.lo); outs.push_back(N.hi);
+        for (int kind = 0; kind < 2; ++kind)
+            for (uint32_t g = 0; g < 5; ++g) {
+                Fp d = prf_noise_delta(pk, sk, sd, g, (uint8_t)kind);
+                outs.push_back(d.lo); outs.push_back(d.hi);
+            }
+    }
+    write_u64(dir + "/prf_seeds.u64", seeds);
+    write_u64(dir + "/prf_out.u64", outs);
+    js << "  \"prf_seeds\": " << nseed << ",\n  \"enc\": [\n";
+    // enc_value with logged streams
+    const uint64_t vals[] = {0, 1, 2, 2016733, 7083881, 1000002, ~0ULL, 0x123456789abcdefULL,
+                             42, 65537, 3, 999};
+    g_logging = true;
+    for (int i = 0; i < nenc; ++i) {
+        const uint64_t v = vals[i % 12];
+        reseed(0x5EED0E10ULL + (uint64_t)i);
+        std::vector<uint64_t> stream;
+        Cipher X = run_logged([&] { return enc_value(pk, sk, v); }, stream);
+        const std::string pre = dir + "/enc" + std::to_string(i);
+        write_ct(pre + ".ct", {X}, true);
+        write_u64(pre + "_stream.u64", stream);
+        g_logging = false;
+        dump_R(pre + "_R.u64", base_layer_R(pk, sk, X));
+        Fp dv = dec_value(pk, sk, X);
+        g_logging = true;
+        js << "    {\"v\": " << v << ", \"seed\": " << (0x5EED0E10ULL + (uint64_t)i) << ", \"edges\": " << X.E.size()
+           << ", \"layers\": " << X.L.size() << ", \"stream\": " << stream.size() << ", \"dec\": " << fpjson(dv) << "}"
+           << (i + 1 < nenc ? "," : "") << "\n";
+    }
+    js << "  ]\n}\n";
+    std::ofstream(dir + "/enc_manifest.json") << js.str();
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: ref_harness fp|fixtures|time_mul ...\n"); return 2; }
     std::string cmd = argv[1];
@@ -426,6 +492,10 @@ int main(int argc, char** argv) {
         int cs = argc > 4 ? std::atoi(argv[4]) : 3;
         int ss = argc > 5 ? std::atoi(argv[5]) : 2;
         cmd_fixtures(argv[2], np, cs, ss);
+        return 0;
+    }
+    if (cmd == "enc" && argc >= 3) {
+        cmd_enc(argv[2], argc > 3 ? std::atoi(argv[3]) : 12);
         return 0;
     }
     if (cmd == "time_mul") {

@@ -163,6 +163,31 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
+class OrcSecret(C.Structure):
+    _fields_ = [("prf_k", C.c_uint64 * 4), ("lpn_s", C.c_void_p), ("lpn_n", C.c_uint32), ("lpn_t", C.c_uint32),
+                ("tau_num", C.c_uint32), ("tau_den", C.c_uint32), ("H_digest", C.c_uint8 * 32)]
+
+
+def fixture_secret():
+    """Key material the reference harness minted (oracle/ref_harness.cpp cmd_enc): OrcSecret + keep-alive."""
+    import json
+    man = json.load(open(os.path.join(REF, "manifest.json")))
+    em = json.load(open(os.path.join(REF, "enc_manifest.json")))
+    k = read_u64("sk_prf_k.u64")
+    sbits = np.ascontiguousarray(read_u64("sk_lpn_s.u64"))
+    sk = OrcSecret()
+    for i in range(4):
+        sk.prf_k[i] = int(k[i])
+    sk.lpn_s = sbits.ctypes.data
+    sk.lpn_n, sk.lpn_t = em["lpn_n"], em["lpn_t"]
+    sk.tau_num, sk.tau_den = em["lpn_tau_num"], em["lpn_tau_den"]
+    hd = bytes.fromhex(man["H_digest"])
+    for i in range(32):
+        sk.H_digest[i] = hd[i]
+    sk._keep = sbits
+    return sk, man, em
+
+
 def default_params(canon_tag=0, edge_budget=1200000, B=337):
     return OrcParams(B=B, m_bits=8192, n_bits=16384, h_col_wt=192, x_col_wt=128, err_wt=128,
                      edge_budget=edge_budget, canon_tag=canon_tag)
@@ -211,6 +236,11 @@ class Oracle:
         lib.orc_ct_mul_batch_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 12 + \
             [C.c_int, u64p, u64p]
         lib.orc_ct_mul_batch_timed.restype = C.c_double
+        lib.orc_prf_core.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_int, C.c_int, u64p]
+        lib.orc_prf_R.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_int, u64p]
+        lib.orc_prf_noise_delta.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_uint32, C.c_uint32, u64p]
+        lib.orc_enc_value.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSecret), u64p, u64p, C.c_uint64, u64p,
+                                      C.c_size_t, C.c_int, C.POINTER(OrcCipher), C.POINTER(C.c_size_t)]
 
     # ---- Fp
     def fp(self, op, a_lo, a_hi, b_lo=None, b_hi=None):
@@ -310,6 +340,32 @@ class Oracle:
         self.lib.orc_dec_value(C.byref(prm), _p(np.ascontiguousarray(powg, np.uint64)), C.byref(self._view(c)),
                                _p(R), _p(out))
         return int(out[0]), int(out[1])
+
+    def prf_core(self, sk, canon, seed, dom, full=False):
+        out = np.zeros(2, np.uint64)
+        self.lib.orc_prf_core(C.byref(sk), canon, int(seed[0]), int(seed[1]), int(seed[2]), dom, int(full), _p(out))
+        return int(out[0]), int(out[1])
+
+    def prf_R(self, sk, canon, seed, noise=False):
+        out = np.zeros(2, np.uint64)
+        self.lib.orc_prf_R(C.byref(sk), canon, int(seed[0]), int(seed[1]), int(seed[2]), int(noise), _p(out))
+        return int(out[0]), int(out[1])
+
+    def prf_noise_delta(self, sk, canon, seed, group, kind):
+        out = np.zeros(2, np.uint64)
+        self.lib.orc_prf_noise_delta(C.byref(sk), canon, int(seed[0]), int(seed[1]), int(seed[2]), group, kind,
+                                     _p(out))
+        return int(out[0]), int(out[1])
+
+    def enc_value(self, sk, v, stream, powg, H=None, canon_tag=0, order=1):
+        prm = default_params(canon_tag)
+        oc, ov = self._out(4, 64, H is not None)
+        used = C.c_size_t()
+        st = np.ascontiguousarray(stream, np.uint64)
+        rc = self.lib.orc_enc_value(C.byref(prm), C.byref(sk), _p(H), _p(np.ascontiguousarray(powg, np.uint64)),
+                                    int(v), _p(st), len(st), order, C.byref(ov), C.byref(used))
+        assert rc == 0, rc
+        return self._trim(oc, ov), used.value
 
     def bucket_count(self, n):
         return self.lib.orc_bucket_count_after_reserve(n)
