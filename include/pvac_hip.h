@@ -196,6 +196,18 @@ uint64_t pvac_hip_bucket_count(uint64_t n);
 /* per-cipher FNV-1a digest over (meta, w_lo, w_hi) of its edges in order (device out[n]). */
 int pvac_hip_batch_digest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
 
+/* ---------------------------------------------------------------- LPN PRF
+ * SecKey (core/types.hpp:134-137): prf_k and the LPN secret (ceil(lpn_n/64) words, host) with
+ * pk.prm's lpn_t and noise rate tau_num/tau_den. The PRF also needs pk.H_digest: it is taken
+ * from gen_H / set_H, or given with set_H_digest. */
+int pvac_hip_ctx_set_secret(pvac_hip_ctx* ctx, const uint64_t prf_k[4], const uint64_t* lpn_s_host, uint32_t lpn_n,
+                            uint32_t lpn_t, uint32_t tau_num, uint32_t tau_den);
+int pvac_hip_ctx_set_H_digest(pvac_hip_ctx* ctx, const uint8_t digest[32]);
+/* prf over n seeds (device, 3 words per seed: {ztag, nonce_lo, nonce_hi} = pvac::RSeed):
+ * kind 0..5 = prf_R_core with domain pvac.prf.r.1..3 / pvac.prf.noise.1..3 (crypto/lpn.hpp:188-261),
+ * 6 = prf_R (:263-268), 7 = prf_R_noise (:270-275). out: device, 2 words (lo, hi) per seed. */
+int pvac_hip_prf(pvac_hip_ctx* ctx, int kind, size_t n, const uint64_t* seeds, uint64_t* out);
+
 /* ---------------------------------------------------------------- decryption
  * dec_value (ops/decrypt.hpp:12-89) over a batch, given the BASE-layer R values (prf_R of each
  * BASE layer's seed under the secret key, crypto/lpn.hpp): R of every other layer is the product

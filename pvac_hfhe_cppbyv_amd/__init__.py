@@ -90,6 +90,9 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_bucket_count": ([u64], u64),
         "pvac_hip_ctx_set_powg": ([vp, vp, u32], i32),
+        "pvac_hip_ctx_set_secret": ([vp, vp, vp, u32, u32, u32, u32], i32),
+        "pvac_hip_ctx_set_H_digest": ([vp, vp], i32),
+        "pvac_hip_prf": ([vp, i32, C.c_size_t, vp, vp], i32),
         "pvac_hip_dec_value": ([vp, C.POINTER(CtBatch), vp, vp, vp], i32),
         "pvac_ct_scan": ([vp, C.c_size_t, vp], i32),
         "pvac_ct_parse": ([vp, C.c_size_t, C.POINTER(CtBatch), i32], i32),
@@ -235,6 +238,29 @@ class Engine:
         self._check(self.lib.pvac_hip_fp_binop(self.ctx, op, p(a_lo), p(a_hi), p(b_lo), p(b_hi), p(c_lo), p(c_hi),
                                                n))
         return c_lo, c_hi
+
+    # ---- LPN PRF (crypto/lpn.hpp)
+    def set_secret(self, prf_k, lpn_s, lpn_n=4096, lpn_t=16384, tau_num=1, tau_den=8):
+        k = np.ascontiguousarray(np.asarray(prf_k, dtype=np.uint64).reshape(4))
+        s = np.ascontiguousarray(np.asarray(lpn_s, dtype=np.uint64))
+        self._check(self.lib.pvac_hip_ctx_set_secret(self.ctx, C.c_void_p(k.ctypes.data), C.c_void_p(s.ctypes.data),
+                                                     lpn_n, lpn_t, tau_num, tau_den))
+
+    def set_H_digest(self, digest: bytes):
+        b = C.create_string_buffer(bytes(digest), 32)
+        self._check(self.lib.pvac_hip_ctx_set_H_digest(self.ctx, b))
+
+    def prf(self, kind, seeds):
+        """seeds: (n, 3) u64 {ztag, nonce_lo, nonce_hi}; kind 0..5 core(dom), 6 prf_R, 7 prf_R_noise.
+        Returns a list of ints."""
+        torch = self.torch
+        a = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64).reshape(-1, 3))
+        n = len(a)
+        sd = _t(a.reshape(-1) if n else np.zeros(3, np.uint64)).to(self.device)
+        out = torch.zeros(2 * max(n, 1), dtype=torch.int64, device=self.device)
+        self._check(self.lib.pvac_hip_prf(self.ctx, kind, n, C.c_void_p(sd.data_ptr()), C.c_void_p(out.data_ptr())))
+        o = out.cpu().numpy().view(np.uint64)
+        return [int(o[2 * i]) | (int(o[2 * i + 1]) << 64) for i in range(n)]
 
     # ---- decryption (ops/decrypt.hpp:12-89)
     def set_powg(self, powg):

@@ -159,6 +159,24 @@ hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st);
 // args_dev: device copy of `a` (the kernel reads its arguments from memory, see k_mul_fresh.hip)
 hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* args_dev, int num_cus, hipStream_t st);
 
+// ---- LPN PRF (k_prf.hip): prf_R_core / prf_R / prf_R_noise (crypto/lpn.hpp:159-275)
+struct prf_consts {
+    uint32_t mid[8];          // SHA-256 state after block 0 of the key derivation (prf_k, canon, H_digest[0..24))
+    uint64_t hd_tail;         // H_digest[24..32) as a little-endian u64
+    uint64_t dom_hash[6];     // fnv1a of pvac.prf.r.1..3, pvac.prf.noise.1..3 (lpn.hpp:150-157)
+    uint64_t toep_hash;       // fnv1a("pvac.dom.toeplitz")
+    const uint64_t* s_bits;   // LPN secret (device), s_words u64
+    uint32_t s_words, tau_num, tau_den, pad;
+};
+hipError_t prf_upload_tables(hipStream_t st);
+size_t prf_request_bytes();
+// n core requests (see k_prf.hip prf_request) -> out[2 n]
+hipError_t launch_prf_cores(const prf_consts& k, const void* req, uint64_t n, uint64_t* out, hipStream_t st);
+// seeds: 3 u64 per seed {ztag, nonce_lo, nonce_hi}; kind 0..5 one core, 6 prf_R, 7 prf_R_noise.
+// req_scratch: 3 n requests; core_scratch: 6 n u64 (kinds 6/7)
+hipError_t launch_prf(const prf_consts& k, int kind, const uint64_t* seeds, uint64_t n, void* req_scratch,
+                      uint64_t* core_scratch, uint64_t* out, hipStream_t st);
+
 // ---- dec_value (k_dec.hip): BASE-layer R supplied, PROD R tree, inversions, signed edge sum
 size_t dec_scratch_bytes(uint64_t total_layers);
 hipError_t launch_dec_value(const pvac_ct_batch& X, const uint64_t* Rbase, const uint64_t* powg, uint32_t Bm,

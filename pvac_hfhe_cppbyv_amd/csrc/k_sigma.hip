@@ -352,6 +352,8 @@ __global__ __launch_bounds__(256) void k_gen_H(uint16_t* rows, uint32_t* counts,
     }
 }
 
+}  // namespace
+
 // host SHA-256 over a contiguous buffer
 void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]) {
     sha_state s;
@@ -377,7 +379,6 @@ void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]) {
     }
 }
 
-}  // namespace
 
 void sigma_tables_free(sigma_tables& T) {
     hipFree(T.rows);

@@ -15,6 +15,7 @@
 
 #include "common.hpp"
 #include "sigma.hpp"
+#include "sha256.hpp"
 
 using namespace pvhip;
 
@@ -53,6 +54,18 @@ struct pvac_hip_ctx {
     size_t dec_cap = 0;
     uint64_t* dec_roff = nullptr;
     size_t dec_roff_cap = 0;
+    // LPN PRF key material (SecKey) and pk.H_digest
+    uint64_t prf_k[4] = {0, 0, 0, 0};
+    uint64_t* lpn_s = nullptr;
+    uint32_t lpn_words = 0, lpn_t = 0, tau_num = 0, tau_den = 0;
+    bool have_secret = false;
+    uint8_t H_digest[32] = {0};
+    bool have_digest = false;
+    bool aes_tables = false;
+    uint8_t* prf_req = nullptr;
+    size_t prf_req_cap = 0;
+    uint64_t* prf_core = nullptr;
+    size_t prf_core_cap = 0;
     uint64_t* large_ids = nullptr;
     uint64_t* large_info = nullptr;
     size_t pair_cap = 0;
@@ -318,6 +331,9 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->merge_scratch);
     hipFree(c->merge_counters);
     hipFree(c->powg);
+    hipFree(c->lpn_s);
+    hipFree(c->prf_req);
+    hipFree(c->prf_core);
     hipFree(c->dec_scratch);
     hipFree(c->dec_roff);
     hipFree(c->scan_scratch);
@@ -696,7 +712,21 @@ int pvac_hip_ctx_set_H(pvac_hip_ctx* c, const uint64_t* H, uint32_t n_cols, uint
     if (!c || !H) return PVAC_EINVAL;
     if (n_cols != c->prm.n_bits || wpc != (c->prm.m_bits + 63) / 64) return fail(c, PVAC_EINVAL, "set_H: shape");
     try {
-        return hip_fail(c, sigma_tables_from_dense(c->H, c->prm, H, c->stream), "set_H");
+        const int rc = hip_fail(c, sigma_tables_from_dense(c->H, c->prm, H, c->stream), "set_H");
+        if (rc) return rc;
+        // H_digest = SHA-256("H|v2" || le64 m || le64 n || le64 wt || column bytes) (matrix.hpp:218-250)
+        const size_t colbytes = (c->prm.m_bits + 7) / 8;
+        std::vector<uint8_t> msg(28 + (size_t)n_cols * colbytes);
+        std::memcpy(msg.data(), "H|v2", 4);
+        const uint64_t hdr[3] = {c->prm.m_bits, c->prm.n_bits, c->prm.h_col_wt};
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < 8; ++i) msg[4 + 8 * k + i] = (uint8_t)(hdr[k] >> (8 * i));
+        for (uint32_t col = 0; col < n_cols; ++col)
+            for (size_t b = 0; b < colbytes; ++b)
+                msg[28 + (size_t)col * colbytes + b] = (uint8_t)(H[(size_t)col * wpc + b / 8] >> (8 * (b % 8)));
+        sha256_host(msg.data(), msg.size(), c->H_digest);
+        c->have_digest = true;
+        return PVAC_OK;
     } catch (const std::exception& ex) {
         return fail(c, PVAC_ENOMEM, std::string("set_H: ") + ex.what());
     }
@@ -706,7 +736,13 @@ int pvac_hip_ctx_gen_H(pvac_hip_ctx* c, uint8_t digest[32]) {
     if (!c) return PVAC_EINVAL;
     try {
         scoped_timer t(c, "gen_H");
-        return hip_fail(c, sigma_tables_generate(c->H, c->prm, digest, c->stream), "gen_H");
+        uint8_t d[32];
+        const int rc = hip_fail(c, sigma_tables_generate(c->H, c->prm, d, c->stream), "gen_H");
+        if (rc) return rc;
+        std::memcpy(c->H_digest, d, 32);
+        c->have_digest = true;
+        if (digest) std::memcpy(digest, d, 32);
+        return PVAC_OK;
     } catch (const std::exception& ex) {
         return fail(c, PVAC_ENOMEM, std::string("gen_H: ") + ex.what());
     }
@@ -717,6 +753,100 @@ int pvac_hip_sigma_batch(pvac_hip_ctx* c, pvac_ct_batch* X, const uint64_t* salt
     if (!c->H.ready) return fail(c, PVAC_EINVAL, "sigma_batch: H not set");
     scoped_timer t(c, "sigma");
     return hip_fail(c, launch_sigma(c->H, c->prm, *X, salts, nullptr, c->num_cus, c->stream), "sigma");
+}
+
+// ---------------------------------------------------------------- LPN PRF
+int pvac_hip_ctx_set_secret(pvac_hip_ctx* c, const uint64_t prf_k[4], const uint64_t* lpn_s_host, uint32_t lpn_n,
+                            uint32_t lpn_t, uint32_t tau_num, uint32_t tau_den) {
+    if (!c || !prf_k || !lpn_s_host) return fail(c, PVAC_EINVAL, "set_secret: arguments");
+    const uint32_t words = (lpn_n + 63) / 64;
+    if (lpn_n == 0 || words > 64 || tau_den == 0 || tau_num > tau_den)
+        return fail(c, PVAC_EINVAL, "set_secret: lpn_n must be in [1, 4096], 0 <= tau_num <= tau_den, tau_den > 0");
+    if (lpn_t < 127) return fail(c, PVAC_ENOSYS, "set_secret: lpn_t < 127 not supported");
+    hipFree(c->lpn_s);
+    c->lpn_s = nullptr;
+    c->have_secret = false;
+    hipError_t e = hipMalloc(&c->lpn_s, 64 * 8);
+    if (e == hipSuccess) e = hipMemset(c->lpn_s, 0, 64 * 8);
+    if (e == hipSuccess) e = hipMemcpy(c->lpn_s, lpn_s_host, (size_t)words * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(c, e, "set_secret");
+    std::memcpy(c->prf_k, prf_k, 32);
+    c->lpn_words = words;
+    c->lpn_t = lpn_t;
+    c->tau_num = tau_num;
+    c->tau_den = tau_den;
+    c->have_secret = true;
+    return PVAC_OK;
+}
+
+int pvac_hip_ctx_set_H_digest(pvac_hip_ctx* c, const uint8_t digest[32]) {
+    if (!c || !digest) return PVAC_EINVAL;
+    std::memcpy(c->H_digest, digest, 32);
+    c->have_digest = true;
+    return PVAC_OK;
+}
+
+namespace {
+
+uint64_t fnv1a(const char* d) {   // lpn.hpp:150-157
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (const char* p = d; *p; ++p) { h ^= (uint8_t)*p; h *= 0x100000001b3ull; }
+    return h;
+}
+
+// constants of the key derivation (lpn.hpp:159-186); the first message block is fixed per key
+int prf_setup(pvac_hip_ctx* c, prf_consts& k) {
+    if (!c->have_secret) return fail(c, PVAC_EINVAL, "prf: secret key not set (pvac_hip_ctx_set_secret)");
+    if (!c->have_digest) return fail(c, PVAC_EINVAL, "prf: H_digest unknown (gen_H, set_H or set_H_digest)");
+    if (!c->aes_tables) {
+        hipError_t e = prf_upload_tables(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "prf tables");
+        c->aes_tables = true;
+    }
+    uint8_t m[64];
+    for (int i = 0; i < 4; ++i)
+        for (int b = 0; b < 8; ++b) m[8 * i + b] = (uint8_t)(c->prf_k[i] >> (8 * b));
+    for (int b = 0; b < 8; ++b) m[32 + b] = (uint8_t)(c->prm.canon_tag >> (8 * b));
+    std::memcpy(m + 40, c->H_digest, 24);
+    uint32_t w[16];
+    for (int i = 0; i < 16; ++i)
+        w[i] = (uint32_t)m[4 * i] << 24 | (uint32_t)m[4 * i + 1] << 16 | (uint32_t)m[4 * i + 2] << 8 | m[4 * i + 3];
+    sha_state st;
+    sha_init(st);
+    sha_compress(st, w);
+    std::memcpy(k.mid, st.h, 32);
+    uint64_t tail = 0;
+    for (int b = 0; b < 8; ++b) tail |= (uint64_t)c->H_digest[24 + b] << (8 * b);
+    k.hd_tail = tail;
+    static const char* const doms[6] = {"pvac.prf.r.1", "pvac.prf.r.2", "pvac.prf.r.3",
+                                        "pvac.prf.noise.1", "pvac.prf.noise.2", "pvac.prf.noise.3"};
+    for (int d = 0; d < 6; ++d) k.dom_hash[d] = fnv1a(doms[d]);
+    k.toep_hash = fnv1a("pvac.dom.toeplitz");
+    k.s_bits = c->lpn_s;
+    k.s_words = c->lpn_words;
+    k.tau_num = c->tau_num;
+    k.tau_den = c->tau_den;
+    return PVAC_OK;
+}
+
+int ensure_prf_scratch(pvac_hip_ctx* c, uint64_t cores) {
+    int rc = ensure_dev(c, c->prf_req, c->prf_req_cap, cores * prf_request_bytes(), "alloc prf requests");
+    if (rc) return rc;
+    return ensure_dev(c, c->prf_core, c->prf_core_cap, 2 * cores, "alloc prf cores");
+}
+
+}  // namespace
+
+int pvac_hip_prf(pvac_hip_ctx* c, int kind, size_t n, const uint64_t* seeds, uint64_t* out) {
+    if (!c || kind < 0 || kind > 7 || (n && (!seeds || !out))) return fail(c, PVAC_EINVAL, "prf: arguments");
+    if (!n) return PVAC_OK;
+    prf_consts k{};
+    int rc = prf_setup(c, k);
+    if (rc) return rc;
+    rc = ensure_prf_scratch(c, 3 * (uint64_t)n);
+    if (rc) return rc;
+    scoped_timer t(c, "prf");
+    return hip_fail(c, launch_prf(k, kind, seeds, n, c->prf_req, c->prf_core, out, c->stream), "prf");
 }
 
 // ---------------------------------------------------------------- dec_value

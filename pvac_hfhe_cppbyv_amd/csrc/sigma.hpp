@@ -17,6 +17,8 @@ struct sigma_tables {
 };
 
 void sigma_tables_free(sigma_tables& T);
+// host SHA-256 over a contiguous buffer
+void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]);
 // from a HOST dense H (n_bits columns x ceil(m_bits/64) words); synchronous
 hipError_t sigma_tables_from_dense(sigma_tables& T, const pvac_hip_params& prm, const uint64_t* H_host, hipStream_t st);
 // gen_H (crypto/matrix.hpp:191-251) on the device; digest computed on the host; synchronous
