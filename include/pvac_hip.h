@@ -208,6 +208,23 @@ int pvac_hip_ctx_set_H_digest(pvac_hip_ctx* ctx, const uint8_t digest[32]);
  * 6 = prf_R (:263-268), 7 = prf_R_noise (:270-275). out: device, 2 words (lo, hi) per seed. */
 int pvac_hip_prf(pvac_hip_ctx* ctx, int kind, size_t n, const uint64_t* seeds, uint64_t* out);
 
+/* ---------------------------------------------------------------- encryption
+ * enc_value (ops/encrypt.hpp:281-287) over n plaintexts (device u64). The reference draws every
+ * random choice from getrandom (csprng_u64); here value i's draws are rnd[i * rnd_stride ...], in
+ * the reference's order (mask, then enc_fp_depth(-mask), then enc_fp_depth(v + mask)): with the
+ * draws the reference consumed, the output is byte-identical. C: 2 layers and edges_per_value
+ * edge slots per value (pvac_hip_enc_caps), l_off/l_cnt/e_off/e_cnt written by the call
+ * (capacity-padded CSR). status: device u32 per value: 0 ok; 1 rnd_stride draws were not enough;
+ * 2 a merged edge group cancelled exactly (probability ~1/p; not reproduced). Needs set_secret,
+ * the H digest, set_powg, and H for PVAC_ENC_WITH_SIGMA. */
+#define PVAC_ENC_WITH_SIGMA 0x1u
+int pvac_hip_enc_caps(pvac_hip_ctx* ctx, uint32_t* layers_per_value, uint32_t* edges_per_value, uint32_t* draws_hint);
+int pvac_hip_enc_value(pvac_hip_ctx* ctx, size_t n, const uint64_t* values, const uint64_t* rnd, uint32_t rnd_stride,
+                       pvac_ct_batch* C, uint32_t flags, uint32_t* status);
+/* prf_R of every BASE layer of X (ops/decrypt.hpp:44-46): R_out device, 2 words per layer SLOT
+ * (slots addressed by l_off/l_cnt; PROD slots get 0) — the R_base input of pvac_hip_dec_value. */
+int pvac_hip_base_R(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* R_out);
+
 /* ---------------------------------------------------------------- decryption
  * dec_value (ops/decrypt.hpp:12-89) over a batch, given the BASE-layer R values (prf_R of each
  * BASE layer's seed under the secret key, crypto/lpn.hpp): R of every other layer is the product

@@ -26,6 +26,7 @@ LAYER_DT = np.dtype([("rule", "<u4"), ("pa", "<u4"), ("pb", "<u4"), ("pad", "<u4
 
 FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE, FP_INV = 0, 1, 2, 3, 4, 5
 MUL_WITH_SIGMA, MUL_ORDER_CANONICAL = 0x1, 0x2
+ENC_WITH_SIGMA = 0x1
 
 P = (1 << 127) - 1
 
@@ -93,6 +94,9 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_ctx_set_secret": ([vp, vp, vp, u32, u32, u32, u32], i32),
         "pvac_hip_ctx_set_H_digest": ([vp, vp], i32),
         "pvac_hip_prf": ([vp, i32, C.c_size_t, vp, vp], i32),
+        "pvac_hip_enc_caps": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], i32),
+        "pvac_hip_enc_value": ([vp, C.c_size_t, vp, vp, u32, C.POINTER(CtBatch), u32, vp], i32),
+        "pvac_hip_base_R": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_dec_value": ([vp, C.POINTER(CtBatch), vp, vp, vp], i32),
         "pvac_ct_scan": ([vp, C.c_size_t, vp], i32),
         "pvac_ct_parse": ([vp, C.c_size_t, C.POINTER(CtBatch), i32], i32),
@@ -261,6 +265,43 @@ class Engine:
         self._check(self.lib.pvac_hip_prf(self.ctx, kind, n, C.c_void_p(sd.data_ptr()), C.c_void_p(out.data_ptr())))
         o = out.cpu().numpy().view(np.uint64)
         return [int(o[2 * i]) | (int(o[2 * i + 1]) << 64) for i in range(n)]
+
+    # ---- encryption (ops/encrypt.hpp:281-287)
+    def enc_caps(self):
+        lp, ep, dh = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._check(self.lib.pvac_hip_enc_caps(self.ctx, C.byref(lp), C.byref(ep), C.byref(dh)))
+        return lp.value, ep.value, dh.value
+
+    def enc_value(self, values, rnd, sigma=False):
+        """values: n u64 (host array or device tensor); rnd: (n, stride) u64 draws per value (the
+        reference's csprng_u64 stream). Returns (DeviceBatch, status numpy u32)."""
+        torch = self.torch
+        if isinstance(values, np.ndarray) or isinstance(values, list):
+            values = _t(np.ascontiguousarray(np.asarray(values, dtype=np.uint64))).to(self.device)
+        if isinstance(rnd, np.ndarray):
+            rnd = _t(np.ascontiguousarray(rnd, np.uint64)).to(self.device)
+        n = values.numel()
+        stride = rnd.numel() // max(n, 1)
+        lp, ep, _ = self.enc_caps()
+        z = lambda k: torch.zeros(max(k, 1), dtype=torch.int64, device=self.device)
+        C_ = DeviceBatch(n, z(n), z(n), torch.zeros((max(lp * n, 1), 5), dtype=torch.int64, device=self.device), z(n),
+                         z(n), z(ep * n), z(ep * n), z(ep * n),
+                         torch.zeros((max(ep * n, 1), 128), dtype=torch.int64, device=self.device) if sigma else None)
+        status = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
+        sc = C_.struct()
+        self._check(self.lib.pvac_hip_enc_value(self.ctx, n, C.c_void_p(values.data_ptr()), C.c_void_p(rnd.data_ptr()),
+                                                stride, C.byref(sc), ENC_WITH_SIGMA if sigma else 0,
+                                                C.c_void_p(status.data_ptr())))
+        return C_, status.cpu().numpy().view(np.uint32)[:n]
+
+    def base_R(self, X: DeviceBatch):
+        """prf_R of every BASE layer slot of X (device tensor, 2 int64 words per slot)."""
+        torch = self.torch
+        slots = int((X.l_off + X.l_cnt).max().item()) if X.n else 0
+        R = torch.zeros(2 * max(slots, 1), dtype=torch.int64, device=self.device)
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_base_R(self.ctx, C.byref(sx), C.c_void_p(R.data_ptr())))
+        return R
 
     # ---- decryption (ops/decrypt.hpp:12-89)
     def set_powg(self, powg):

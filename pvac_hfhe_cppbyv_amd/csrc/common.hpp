@@ -168,6 +168,12 @@ struct prf_consts {
     const uint64_t* s_bits;   // LPN secret (device), s_words u64
     uint32_t s_words, tau_num, tau_den, pad;
 };
+// one prf_R_core evaluation: an RSeed and a domain index into prf_consts.dom_hash (0..5)
+struct prf_request {
+    uint64_t ztag, nonce_lo, nonce_hi;
+    uint32_t dom;
+    uint32_t pad;
+};
 hipError_t prf_upload_tables(hipStream_t st);
 size_t prf_request_bytes();
 // n core requests (see k_prf.hip prf_request) -> out[2 n]
@@ -176,6 +182,34 @@ hipError_t launch_prf_cores(const prf_consts& k, const void* req, uint64_t n, ui
 // req_scratch: 3 n requests; core_scratch: 6 n u64 (kinds 6/7)
 hipError_t launch_prf(const prf_consts& k, int kind, const uint64_t* seeds, uint64_t n, void* req_scratch,
                       uint64_t* core_scratch, uint64_t* out, hipStream_t st);
+// prf_R of every BASE layer slot of X (slots < n_slots), 0 for others: R_out[2 s], [2 s + 1]
+hipError_t launch_base_R(const prf_consts& k, const pvac_ct_batch& X, uint64_t n_slots, void* req_scratch,
+                         uint64_t* core_scratch, uint64_t* R_out, hipStream_t st);
+
+// ---- enc_value (k_enc.hip, ops/encrypt.hpp:114-291)
+constexpr uint32_t kEncPreMax = 48;   // pre-merge edges per half: 8 signal + 2 Z2 + 3 Z3 (Z2, Z3 <= 8)
+struct enc_plan_args {
+    const uint64_t* values;   // n plaintexts
+    const uint64_t* rnd;      // csprng_u64 draws: stride words per value
+    uint32_t stride;
+    uint32_t B, Z2, Z3;
+    uint64_t n;
+    uint64_t canon;
+    const uint64_t* powg;     // B x (lo, hi)
+};
+size_t enc_half_bytes();
+// per value: 2 output layers, <= 2 * (8 + 2 Z2 + 3 Z3) edges; cores per value = 2 * 3 * max(Z2 + Z3, 1)
+uint32_t enc_cores_per_value(uint32_t Z2, uint32_t Z3);
+// 1. draws (exact csprng order), merge groups, shuffle, PRF requests, and the pre-merge edge batch
+//    `pre` (2 layers and 2 * npre edge slots per value; salts in pre_salt) for sigma
+hipError_t launch_enc_plan(const enc_plan_args& a, void* halves, prf_request* req, pvac_ct_batch& pre,
+                           uint64_t* pre_salt, uint32_t* status, hipStream_t st);
+// 2. R, noise deltas and the solved coefficients -> pre-merge weights (pre.w_lo / w_hi)
+hipError_t launch_enc_weights(const enc_plan_args& a, void* halves, const uint64_t* cores, pvac_ct_batch& pre,
+                              hipStream_t st);
+// 3. merged groups (fp_add chains, sigma XOR) in shuffled order -> C (2 layers, CSR stride 2 * npre)
+hipError_t launch_enc_finish(const enc_plan_args& a, const void* halves, const pvac_ct_batch& pre, pvac_ct_batch& C,
+                             uint32_t* status, hipStream_t st);
 
 // ---- dec_value (k_dec.hip): BASE-layer R supplied, PROD R tree, inversions, signed edge sum
 size_t dec_scratch_bytes(uint64_t total_layers);

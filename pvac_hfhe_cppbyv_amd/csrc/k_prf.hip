@@ -28,12 +28,6 @@ constexpr int kPB = 256;   // 4 requests per block
 
 __constant__ aes_ttables c_aes;
 
-struct prf_request {
-    uint64_t ztag, nonce_lo, nonce_hi;
-    uint32_t dom;   // index into prf_consts.dom_hash (0..5)
-    uint32_t pad;
-};
-
 __device__ __forceinline__ uint32_t bswap32d(uint32_t x) { return __builtin_bswap32(x); }
 
 // block 2 of the derivation message (bytes 64..127): H_digest[24..32) | ztag | nlo | nhi | dom | pad
@@ -196,6 +190,36 @@ __global__ __launch_bounds__(kPB) void k_prf_requests(const uint64_t* seeds, uin
     }
 }
 
+// BASE-layer requests for base_R: slot s of cipher i -> 3 cores (doms 0..2); PROD slots get a
+// dummy request whose result is ignored (zeroed by k_base_R_out)
+__global__ __launch_bounds__(kPB) void k_base_R_requests(pvac_ct_batch X, uint64_t n_slots, prf_request* req,
+                                                         uint8_t* is_base) {
+    const uint64_t c = blockIdx.x;
+    if (c >= X.n) return;
+    const uint64_t lo = X.l_off[c], lc = X.l_cnt[c];
+    for (uint64_t l = threadIdx.x; l < lc; l += kPB) {
+        const uint64_t s = lo + l;
+        if (s >= n_slots) continue;
+        const pvac_layer y = X.layers[s];
+        for (uint32_t d = 0; d < 3; ++d) req[3 * s + d] = prf_request{y.ztag, y.nonce_lo, y.nonce_hi, d, 0};
+        is_base[s] = y.rule == 0 ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(kPB) void k_base_R_out(const uint64_t* cores, const uint8_t* is_base, uint64_t n_slots,
+                                                    uint64_t* R) {
+    const uint64_t s = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    if (s >= n_slots) return;
+    fp r{0, 0};
+    if (is_base[s]) {
+        const fp a{cores[6 * s], cores[6 * s + 1]}, b{cores[6 * s + 2], cores[6 * s + 3]},
+            c{cores[6 * s + 4], cores[6 * s + 5]};
+        r = fp_mul(fp_mul(a, b), c);
+    }
+    R[2 * s] = r.lo;
+    R[2 * s + 1] = r.hi;
+}
+
 }  // namespace
 
 hipError_t prf_upload_tables(hipStream_t st) {
@@ -222,6 +246,24 @@ hipError_t launch_prf(const prf_consts& k, int kind, const uint64_t* seeds, uint
     hipError_t e = launch_prf_cores(k, req_scratch, cores, kind >= 6 ? core_scratch : out, st);
     if (e != hipSuccess || kind < 6) return e;
     hipLaunchKernelGGL(k_prf_triple, dim3(blocks), dim3(kPB), 0, st, core_scratch, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_base_R(const prf_consts& k, const pvac_ct_batch& X, uint64_t n_slots, void* req_scratch,
+                         uint64_t* core_scratch, uint64_t* R_out, hipStream_t st) {
+    if (!X.n || !n_slots) return hipSuccess;
+    if (X.n > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    prf_request* req = (prf_request*)req_scratch;
+    // requests for slots not covered by any cipher stay as they were: mark them non-BASE first
+    uint8_t* is_base = (uint8_t*)(core_scratch + 6 * n_slots);   // scratch tail (caller sized 8 n_slots words)
+    hipError_t e = hipMemsetAsync(is_base, 0, n_slots, st);
+    if (e == hipSuccess) e = hipMemsetAsync(req, 0, n_slots * 3 * sizeof(prf_request), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_base_R_requests, dim3((unsigned)X.n), dim3(kPB), 0, st, X, n_slots, req, is_base);
+    e = launch_prf_cores(k, req, 3 * n_slots, core_scratch, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_base_R_out, dim3((unsigned)((n_slots + kPB - 1) / kPB)), dim3(kPB), 0, st, core_scratch,
+                       is_base, n_slots, R_out);
     return hipGetLastError();
 }
 

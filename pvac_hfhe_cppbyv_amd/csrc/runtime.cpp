@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -66,6 +67,8 @@ struct pvac_hip_ctx {
     size_t prf_req_cap = 0;
     uint64_t* prf_core = nullptr;
     size_t prf_core_cap = 0;
+    uint8_t* enc_arena = nullptr;
+    size_t enc_arena_cap = 0;
     uint64_t* large_ids = nullptr;
     uint64_t* large_info = nullptr;
     size_t pair_cap = 0;
@@ -334,6 +337,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->lpn_s);
     hipFree(c->prf_req);
     hipFree(c->prf_core);
+    hipFree(c->enc_arena);
     hipFree(c->dec_scratch);
     hipFree(c->dec_roff);
     hipFree(c->scan_scratch);
@@ -847,6 +851,124 @@ int pvac_hip_prf(pvac_hip_ctx* c, int kind, size_t n, const uint64_t* seeds, uin
     if (rc) return rc;
     scoped_timer t(c, "prf");
     return hip_fail(c, launch_prf(k, kind, seeds, n, c->prf_req, c->prf_core, out, c->stream), "prf");
+}
+
+// ---------------------------------------------------------------- enc_value
+namespace {
+// ops/encrypt.hpp:16-27 with the reference's default Params (noise_entropy_bits 120,
+// tuple2_fraction 0.55, depth_slope_bits 16); enc_value uses depth_hint 0
+void plan_noise(uint32_t B, int depth, uint32_t& z2, uint32_t& z3) {
+    const double budget = 120.0 + 16.0 * std::max(0, depth);
+    const double per2 = 2.0 * std::log2((double)B), per3 = 3.0 * std::log2((double)B);
+    int a = std::max(0, (int)std::floor((budget * 0.55) / std::max(1e-6, per2)));
+    int b = std::max(0, (int)std::floor((budget * (1.0 - 0.55)) / std::max(1e-6, per3)));
+    if (a + b == 1) { if (b > 0) ++b; else ++a; }
+    z2 = (uint32_t)a;
+    z3 = (uint32_t)b;
+}
+}  // namespace
+
+int pvac_hip_enc_caps(pvac_hip_ctx* c, uint32_t* layers_per_value, uint32_t* edges_per_value, uint32_t* draws_hint) {
+    if (!c) return PVAC_EINVAL;
+    uint32_t z2, z3;
+    plan_noise(c->prm.B, 0, z2, z3);
+    const uint32_t npre = 8 + 2 * z2 + 3 * z3;
+    if (layers_per_value) *layers_per_value = 2;
+    if (edges_per_value) *edges_per_value = 2 * npre;
+    // mask 2 + per half: nonce 2, signal 2*8 + 2*7, salts npre, noise picks/signs/coefficients, shuffle
+    if (draws_hint) *draws_hint = 2 + 2 * (2 + 16 + 14 + npre + z2 * 5 + z3 * 10 + npre) + 64;
+    return PVAC_OK;
+}
+
+int pvac_hip_enc_value(pvac_hip_ctx* c, size_t n, const uint64_t* values, const uint64_t* rnd, uint32_t rnd_stride,
+                       pvac_ct_batch* C, uint32_t flags, uint32_t* status) {
+    if (!c || !C || (n && (!values || !rnd || !status))) return fail(c, PVAC_EINVAL, "enc_value: arguments");
+    if (!C->l_off || !C->l_cnt || !C->layers || !C->e_off || !C->e_cnt || !C->meta || !C->w_lo || !C->w_hi)
+        return fail(c, PVAC_EINVAL, "enc_value: output arrays");
+    const bool with_sigma = (flags & PVAC_ENC_WITH_SIGMA) != 0;
+    if (with_sigma && (!C->sigma || !c->H.ready || C->sigma_words != c->prm.m_bits / 64))
+        return fail(c, PVAC_EINVAL, "enc_value: WITH_SIGMA needs C->sigma (m_bits/64 words per edge) and H");
+    if (!c->powg) return fail(c, PVAC_EINVAL, "enc_value: powg_B not set (pvac_hip_ctx_set_powg)");
+    C->n = n;
+    if (!n) return PVAC_OK;
+    prf_consts k{};
+    int rc = prf_setup(c, k);
+    if (rc) return rc;
+    enc_plan_args a{};
+    a.values = values;
+    a.rnd = rnd;
+    a.stride = rnd_stride;
+    a.B = c->prm.B;
+    plan_noise(c->prm.B, 0, a.Z2, a.Z3);
+    a.n = n;
+    a.canon = c->prm.canon_tag;
+    a.powg = c->powg;
+    const uint32_t npre = 8 + 2 * a.Z2 + 3 * a.Z3;
+    if (npre > kEncPreMax) return fail(c, PVAC_ENOSYS, "enc_value: noise plan beyond the supported group counts");
+    const uint64_t cores = (uint64_t)n * enc_cores_per_value(a.Z2, a.Z3);
+    const uint64_t pe = (uint64_t)n * 2 * npre;
+    const uint32_t sw = c->prm.m_bits / 64;
+    // arena: halves | requests | cores | pre CSR (4 x n) | pre layers | meta, w_lo, w_hi, salt | sigma
+    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+    const uint64_t off_req = al((uint64_t)2 * n * enc_half_bytes());
+    const uint64_t off_core = off_req + al(cores * prf_request_bytes());
+    const uint64_t off_csr = off_core + al(cores * 16);
+    const uint64_t off_lay = off_csr + al((uint64_t)n * 32);
+    const uint64_t off_e = off_lay + al((uint64_t)n * 2 * sizeof(pvac_layer));
+    const uint64_t off_sig = off_e + al(pe * 32);
+    const uint64_t total = off_sig + (with_sigma ? al(pe * sw * 8) : 0);
+    if (total > c->enc_arena_cap) {
+        hipFree(c->enc_arena);
+        c->enc_arena = nullptr;
+        c->enc_arena_cap = 0;
+        hipError_t e = hipMalloc(&c->enc_arena, total);
+        if (e != hipSuccess) return hip_fail(c, e, "alloc enc scratch");
+        c->enc_arena_cap = total;
+    }
+    uint8_t* A = c->enc_arena;
+    pvac_ct_batch pre{};
+    pre.n = n;
+    pre.l_off = (uint64_t*)(A + off_csr);
+    pre.l_cnt = pre.l_off + n;
+    pre.e_off = pre.l_cnt + n;
+    pre.e_cnt = pre.e_off + n;
+    pre.layers = (pvac_layer*)(A + off_lay);
+    pre.meta = (uint64_t*)(A + off_e);
+    pre.w_lo = pre.meta + pe;
+    pre.w_hi = pre.w_lo + pe;
+    uint64_t* pre_salt = pre.w_hi + pe;
+    pre.sigma = with_sigma ? (uint64_t*)(A + off_sig) : nullptr;
+    pre.sigma_words = with_sigma ? sw : 0;
+    scoped_timer t(c, "enc_value");
+    hipError_t e = launch_enc_plan(a, A, (prf_request*)(A + off_req), pre, pre_salt, status, c->stream);
+    if (e == hipSuccess) e = launch_prf_cores(k, A + off_req, cores, (uint64_t*)(A + off_core), c->stream);
+    if (e == hipSuccess) e = launch_enc_weights(a, A, (const uint64_t*)(A + off_core), pre, c->stream);
+    if (e == hipSuccess && with_sigma) e = launch_sigma(c->H, c->prm, pre, pre_salt, nullptr, c->num_cus, c->stream);
+    pvac_ct_batch out = *C;
+    if (!with_sigma) out.sigma = nullptr;
+    if (e == hipSuccess) e = launch_enc_finish(a, A, pre, out, status, c->stream);
+    return hip_fail(c, e, "enc_value");
+}
+
+int pvac_hip_base_R(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* R_out) {
+    if (!c || !batch_ok(X) || (X->n && !R_out)) return fail(c, PVAC_EINVAL, "base_R: arguments");
+    if (!X->n) return PVAC_OK;
+    prf_consts k{};
+    int rc = prf_setup(c, k);
+    if (rc) return rc;
+    // layer slots are addressed through l_off / l_cnt on the device: gather every slot's seed
+    std::vector<uint64_t> lo(X->n), lc(X->n);
+    hipError_t e = hipMemcpyAsync(lo.data(), X->l_off, X->n * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(lc.data(), X->l_cnt, X->n * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "base_R (offsets)");
+    uint64_t slots = 0;
+    for (uint64_t i = 0; i < X->n; ++i) slots = std::max(slots, lo[i] + lc[i]);
+    if (!slots) return PVAC_OK;
+    rc = ensure_prf_scratch(c, 4 * slots);   // 3 cores per slot + the BASE flags behind them
+    if (rc) return rc;
+    scoped_timer t(c, "base_R");
+    return hip_fail(c, launch_base_R(k, *X, slots, c->prf_req, c->prf_core, R_out, c->stream), "base_R");
 }
 
 // ---------------------------------------------------------------- dec_value

@@ -60,3 +60,73 @@ def test_prf_digest_from_dense_H(oracle):
     seeds = read_u64("prf_seeds.u64").reshape(-1, 3)
     outs = read_u64("prf_out.u64").reshape(len(seeds), -1, 2)
     assert eng.prf(6, seeds) == _pairs(outs[:, 6])
+
+
+def _streams(em, stride):
+    rnd = np.zeros((len(em["enc"]), stride), np.uint64)
+    for i in range(len(em["enc"])):
+        s = read_u64(f"enc{i}_stream.u64")
+        rnd[i, :len(s)] = s
+    return rnd
+
+
+@pytest.mark.parametrize("sigma", [False, True])
+def test_enc_value_fixtures(sigma):
+    """The reference's getrandom streams reproduce its enc_value outputs (with sigma: byte-exact .ct)."""
+    from helpers import write_ct
+    eng, _, man, em = _eng()
+    vals = np.array([r["v"] for r in em["enc"]], np.uint64)
+    C_, st = eng.enc_value(vals, _streams(em, 256), sigma=sigma)
+    assert not st.any()
+    out = C_.to_host()
+    for i in range(len(vals)):
+        ref = read_ct(os.path.join(REF, f"enc{i}.ct"))[0]
+        c = out[i]
+        assert c.nE == ref.nE and c.nL == ref.nL
+        assert np.array_equal(c.meta, ref.meta)
+        assert np.array_equal(c.w_lo, ref.w_lo) and np.array_equal(c.w_hi, ref.w_hi)
+        for f in ("rule", "ztag", "nonce_lo", "nonce_hi"):
+            assert np.array_equal(c.layers[f], ref.layers[f]), f
+        if sigma:
+            from helpers import Cipher
+            with open(os.path.join(REF, f"enc{i}.ct"), "rb") as f:
+                assert write_ct([Cipher(c.layers, c.meta, c.w_lo, c.w_hi, c.sigma)]) == f.read()
+
+
+def test_enc_value_random_vs_oracle(oracle):
+    eng, sk, man, em = _eng()
+    rng = np.random.default_rng(91)
+    n, stride = 64, 256
+    vals = rng.integers(0, 2**64, n, dtype=np.uint64)
+    rnd = rng.integers(0, 2**64, (n, stride), dtype=np.uint64)
+    C_, st = eng.enc_value(vals, rnd)
+    assert not st.any()
+    out = C_.to_host()
+    powg = read_u64("powg_B.u64")
+    for i in range(0, n, 5):
+        ref, used = oracle.enc_value(sk, int(vals[i]), rnd[i], powg, canon_tag=man["canon_tag"])
+        c = out[i]
+        assert c.nE == ref.nE
+        assert np.array_equal(c.meta, ref.meta)
+        assert np.array_equal(c.w_lo, ref.w_lo) and np.array_equal(c.w_hi, ref.w_hi)
+        assert np.array_equal(c.layers["ztag"], ref.layers["ztag"])
+
+
+def test_enc_short_stream_status():
+    eng, _, _, em = _eng()
+    C_, st = eng.enc_value(np.array([5, 6], np.uint64), np.ones((2, 100), np.uint64))
+    assert list(st) == [1, 1]
+
+
+def test_enc_dec_roundtrip_with_gpu_prf():
+    """dec(enc(v)) = v entirely on the GPU: enc_value, base_R (prf_R of BASE layers), dec_value."""
+    eng, _, man, em = _eng()
+    rng = np.random.default_rng(92)
+    n = 256
+    vals = rng.integers(0, 2**64, n, dtype=np.uint64)
+    vals[:4] = [0, 1, 2**64 - 1, 12345]
+    C_, st = eng.enc_value(vals, rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    got, st2 = eng.dec_value(C_, eng.base_R(C_))
+    assert not st2.any()
+    assert got == [int(v) for v in vals]
