@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--chain-inputs", type=int, default=1 << 12, help="cfg 4 chain inputs timed (per chunk run)")
     ap.add_argument("--chain-chunk", type=int, default=1 << 10)
     ap.add_argument("--chain-depth", type=int, default=8)
-    ap.add_argument("--only", choices=["chain", "sigma", "fp"], default=None,
+    ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
+    ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc"], default=None,
                     help="run one side measurement alone (profiling) and print its JSON")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
@@ -65,6 +66,9 @@ def main():
         return
     if args.only == "sigma":
         print(json.dumps(sigma_bench(eng, args, False)), flush=True)
+        return
+    if args.only == "enc":
+        print(json.dumps(enc_bench(eng, args, False)), flush=True)
         return
     from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks
     n = args.pairs
@@ -298,6 +302,7 @@ def extras(eng, args, with_cpu):
     del bufs
     res["ct_mul_with_sigma"] = sigma_bench(eng, args, with_cpu)
     res["cfg4_chain"] = chain_bench(eng, args)
+    res["enc_value"] = enc_bench(eng, args, with_cpu)
     return res
 
 
@@ -337,6 +342,66 @@ def sigma_bench(eng, args, with_cpu):
     if with_cpu:
         full["cpu_baseline"] = _ref_full_baseline()
     return full
+
+
+def enc_bench(eng, args, with_cpu):
+    """f2: batched enc_value (LPN PRF + signal/noise equations + sigma), synthetic key material
+    (random prf_k / LPN secret, powg_B = powers of a random element), draws from a device stream."""
+    import numpy as np
+    import torch
+    dev = eng.device
+    P = (1 << 127) - 1
+    rng = np.random.default_rng(0xE1C)
+    eng.gen_H()
+    eng.set_secret(rng.integers(0, 2**64, 4, dtype=np.uint64), rng.integers(0, 2**64, 64, dtype=np.uint64))
+    g = int(rng.integers(2, 2**62)) | 1
+    pg = np.zeros(2 * 337, np.uint64)
+    x = 1
+    for i in range(337):
+        pg[2 * i], pg[2 * i + 1] = x & (2**64 - 1), x >> 64
+        x = x * g % P
+    eng.set_powg(pg)
+    n, stride = args.enc_values, 256
+    vals = torch.empty(n, dtype=torch.int64, device=dev)
+    rnd = torch.empty(n * stride, dtype=torch.int64, device=dev)
+    eng.fill_random(vals, 0xE1)
+    eng.fill_random(rnd, 0xE2)
+    res = {"values": n}
+    for sig in (False, True):
+        C_, st = eng.enc_value(vals, rnd, sigma=sig)   # warm-up
+        torch.cuda.synchronize(dev)
+        eng.timing_reset()
+        eng.timing(True)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            C_, st = eng.enc_value(vals, rnd, sigma=sig)
+        torch.cuda.synchronize(dev)
+        el = (time.perf_counter() - t0) / reps
+        eng.timing(False)
+        ms, cnt = eng.timing_get("enc_value")
+        key = "with_sigma" if sig else "weights_only"
+        res[key] = {"enc_per_s": n / el, "ms_per_batch": el * 1000, "avg_call_ms": ms / max(cnt, 1),
+                    "edges": int(C_.e_cnt[:n].sum().item()), "status_nonzero": int((st != 0).sum())}
+    if with_cpu:
+        res["cpu_baseline"] = _ref_enc_baseline()
+    return res
+
+
+def _ref_enc_baseline():
+    """The UNMODIFIED reference enc_value (full, incl. sigma and the 16384-row LPN) on one core."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    try:
+        outp = subprocess.run([exe, "time_enc", "64"], capture_output=True, text=True, timeout=120)
+        line = [l for l in outp.stdout.splitlines() if l.startswith("{")][-1]
+        r = json.loads(line)
+        return {"value": r["enc_per_s"], "unit": "enc_value/s", "cores": 1, "kind": "reference",
+                "sample": f"{r['calls']} enc_value calls (reference pvac-hfhe 0.1.0), {r['seconds']:.2f} s"}
+    except Exception as ex:
+        return {"error": repr(ex)}
 
 
 def chain_bench(eng, args):

@@ -417,6 +417,21 @@ static void cmd_time_mul(int npairs, int threads) {
                 npairs, threads, s, npairs / s, et);
 }
 
+static void cmd_time_enc(int ncalls) {
+    reseed(0x5EED0D00ULL);
+    g_logging = false;
+    Params prm; PubKey pk; SecKey sk;
+    keygen(prm, pk, sk);
+    (void)enc_value(pk, sk, 1);   // warm-up (Toeplitz autotuner)
+    size_t edges = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < ncalls; ++i) edges += enc_value(pk, sk, (uint64_t)i * 7919u).E.size();
+    auto t1 = std::chrono::steady_clock::now();
+    double s = std::chrono::duration<double>(t1 - t0).count();
+    std::printf("{\"calls\": %d, \"seconds\": %.6f, \"enc_per_s\": %.3f, \"edges\": %zu}\n", ncalls, s, ncalls / s,
+                edges);
+}
+
 // ---- f2 fixtures: key material, prf_R_core / prf_R / prf_noise_delta on seeded seeds, and
 //      complete enc_value outputs with the exact getrandom stream each consumed.
 static void cmd_enc(const std::string& dir, int nenc) {
@@ -496,6 +511,10 @@ int main(int argc, char** argv) {
     }
     if (cmd == "enc" && argc >= 3) {
         cmd_enc(argv[2], argc > 3 ? std::atoi(argv[3]) : 12);
+        return 0;
+    }
+    if (cmd == "time_enc") {
+        cmd_time_enc(argc > 2 ? std::atoi(argv[2]) : 16);
         return 0;
     }
     if (cmd == "time_mul") {
