@@ -11,7 +11,11 @@
 //   pvac::ct_add(pk, A, B)  (ops/arithmetic.hpp:12)  -> pvac_hip::ct_add(pk, A, B)
 //   pvac::ct_sub(pk, A, B)  (ops/arithmetic.hpp:43)  -> pvac_hip::ct_sub(pk, A, B)
 //   pvac::ct_scale(pk, A,s) (ops/arithmetic.hpp:33)  -> pvac_hip::ct_scale(pk, A, s)
+//   pvac::enc_value(pk, sk, v) (ops/encrypt.hpp:289)  -> pvac_hip::enc_value<Cipher>(pk, sk, v)
+//   pvac::dec_value(pk, sk, C) (ops/decrypt.hpp:62)  -> pvac_hip::dec_value(pk, sk, C)
+//   saveCts / loadCts          (tests/add.cpp:22-155) -> pvac_hip::save_cts_bytes / load_cts_bytes
 // plus batched forms (std::vector of pairs in, std::vector out) that keep one launch per batch.
+// enc/dec also read pk.H_digest, pk.powg_B, pk.prm.lpn_* and the SecKey's prf_k / lpn_s_bits.
 //
 // Randomness: like the reference (core/random.hpp:40-110), nonces (2 words per new product
 // layer, (la, lb) row-major, lo then hi) and salts (1 word per emitted edge, in emit order) come
@@ -37,6 +41,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -363,14 +368,144 @@ public:
         detail::hip_ok(hipStreamSynchronize(stream_), "sync");
     }
 
+    // Key material of enc_value / dec_value (core/types.hpp:121-137): pk.H_digest and pk.powg_B
+    // from the PubKey, prf_k and lpn_s_bits from the SecKey. Uploaded once; a different SecKey
+    // under the same canon_tag replaces the device copy.
+    template <class PubKeyT, class SecKeyT>
+    void ensure_keys(const PubKeyT& pk, const SecKeyT& sk) {
+        const std::vector<uint64_t> fp = key_fingerprint(sk);
+        if (keys_ready_ && fp == key_fp_) return;
+        if (!keys_ready_) {
+            check(pvac_hip_ctx_set_H_digest(ctx_, pk.H_digest.data()));
+            std::vector<uint64_t> pg(2 * pk.powg_B.size());
+            for (size_t i = 0; i < pk.powg_B.size(); ++i) { pg[2 * i] = pk.powg_B[i].lo; pg[2 * i + 1] = pk.powg_B[i].hi; }
+            check(pvac_hip_ctx_set_powg(ctx_, pg.data(), (uint32_t)pk.powg_B.size()));
+        }
+        check(pvac_hip_ctx_set_secret(ctx_, sk.prf_k.data(), sk.lpn_s_bits.data(), (uint32_t)pk.prm.lpn_n,
+                                      (uint32_t)pk.prm.lpn_t, (uint32_t)pk.prm.lpn_tau_num,
+                                      (uint32_t)pk.prm.lpn_tau_den));
+        key_fp_ = fp;
+        keys_ready_ = true;
+    }
+
+    // Batched enc_value (ops/encrypt.hpp:281-290, depth hint 0). Value i takes `stride`
+    // (enc_caps draws_hint) consecutive words of rnd, in the reference's draw order, so a single
+    // value encrypted from a replayed getrandom stream is byte-identical to the reference's; the
+    // source is advanced by the whole stride. A value whose rejection sampling outruns its stride
+    // (status 1, never seen in practice) is re-run with its own draws extended, prefix kept.
+    template <class PubKeyT, class SecKeyT, class CipherT>
+    std::vector<CipherT> enc_value(const PubKeyT& pk, const SecKeyT& sk, const std::vector<uint64_t>& vs,
+                                   bool with_sigma, const RandomSource& rnd) {
+        const size_t n = vs.size();
+        if (!n) return {};
+        ensure_keys(pk, sk);
+        if (with_sigma) ensure_H(pk);
+        uint32_t lpv = 0, epv = 0, stride = 0;
+        check(pvac_hip_enc_caps(ctx_, &lpv, &epv, &stride));
+        std::vector<uint64_t> draws((size_t)n * stride);
+        for (auto& x : draws) x = rnd();
+        std::vector<uint32_t> status;
+        std::vector<CipherT> out = enc_run<CipherT>(vs, draws, stride, lpv, epv, with_sigma, status);
+        for (uint32_t grow = stride; ; grow *= 2) {
+            std::vector<size_t> redo;
+            for (size_t i = 0; i < n; ++i) {
+                if (status[i] == 2) throw Error(PVAC_EINVAL, "enc_value: a merged edge group cancelled (p ~ 1/p)");
+                if (status[i] == 1) redo.push_back(i);
+            }
+            if (redo.empty()) break;
+            if (grow > (1u << 20)) throw Error(PVAC_EINVAL, "enc_value: random source keeps being rejected");
+            const uint32_t s2 = stride + grow;
+            std::vector<uint64_t> v2(redo.size()), d2((size_t)redo.size() * s2);
+            for (size_t k = 0; k < redo.size(); ++k) {
+                v2[k] = vs[redo[k]];
+                std::memcpy(&d2[k * s2], &draws[redo[k] * stride], (size_t)stride * 8);
+                for (uint32_t j = stride; j < s2; ++j) d2[k * s2 + j] = rnd();
+            }
+            std::vector<uint32_t> st2;
+            std::vector<CipherT> o2 = enc_run<CipherT>(v2, d2, s2, lpv, epv, with_sigma, st2);
+            // the redone values' draws become their prefix for a further round
+            std::vector<uint64_t> nd((size_t)n * s2, 0);
+            for (size_t i = 0; i < n; ++i) std::memcpy(&nd[i * s2], &draws[i * stride], (size_t)stride * 8);
+            for (size_t k = 0; k < redo.size(); ++k) {
+                out[redo[k]] = std::move(o2[k]);
+                status[redo[k]] = st2[k];
+                std::memcpy(&nd[redo[k] * s2], &d2[k * s2], (size_t)s2 * 8);
+            }
+            draws.swap(nd);
+            stride = s2;
+        }
+        return out;
+    }
+
+    // Batched dec_value (ops/decrypt.hpp:12-89): prf_R of every BASE layer on the device
+    // (pvac_hip_base_R), then the R-tree, inverses and weighted sum (pvac_hip_dec_value).
+    template <class PubKeyT, class SecKeyT, class CipherT, class FpT>
+    std::vector<FpT> dec_value(const PubKeyT& pk, const SecKeyT& sk, const std::vector<const CipherT*>& cs) {
+        const size_t n = cs.size();
+        if (!n) return {};
+        ensure_keys(pk, sk);
+        detail::batch x;
+        detail::to_host(cs, sigma_words(), false, x);
+        detail::upload(x, stream_, false);
+        pvac_ct_batch vx = x.view(false);
+        detail::dev_array<uint64_t> R(2 * (x.layers.size() ? x.layers.size() : 1)), out(2 * n);
+        detail::dev_array<uint32_t> st(n);
+        check(pvac_hip_base_R(ctx_, &vx, R.p));
+        check(pvac_hip_dec_value(ctx_, &vx, R.p, out.p, st.p));
+        std::vector<uint64_t> o(2 * n);
+        std::vector<uint32_t> s(n);
+        out.download(o.data(), 2 * n, stream_);
+        st.download(s.data(), n, stream_);
+        detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+        std::vector<FpT> r(n);
+        for (size_t i = 0; i < n; ++i) {
+            if (s[i] == 1) throw Error(PVAC_EINVAL, "dec_value: layer graph has a cycle or a bad parent");
+            if (s[i] == 2) throw Error(PVAC_EINVAL, "dec_value: edge references a layer or idx out of range");
+            r[i].lo = o[2 * i];
+            r[i].hi = o[2 * i + 1];
+        }
+        return r;
+    }
+
 private:
     void check(int rc) {
         if (rc) throw Error(rc, std::string("pvac_hip: ") + pvac_hip_last_error(ctx_));
     }
+
+    template <class SecKeyT>
+    static std::vector<uint64_t> key_fingerprint(const SecKeyT& sk) {
+        std::vector<uint64_t> f(sk.prf_k.begin(), sk.prf_k.end());
+        f.insert(f.end(), sk.lpn_s_bits.begin(), sk.lpn_s_bits.end());
+        return f;
+    }
+
+    // one pvac_hip_enc_value launch over (vs, draws) with a fixed stride; status per value
+    template <class CipherT>
+    std::vector<CipherT> enc_run(const std::vector<uint64_t>& vs, const std::vector<uint64_t>& draws, uint32_t stride,
+                                 uint32_t lpv, uint32_t epv, bool with_sigma, std::vector<uint32_t>& status) {
+        const size_t n = vs.size();
+        detail::dev_array<uint64_t> d_v(n), d_r(draws.size());
+        d_v.upload(vs.data(), n, stream_);
+        d_r.upload(draws.data(), draws.size(), stream_);
+        detail::batch c;
+        c.d_l_off.alloc(n); c.d_l_cnt.alloc(n); c.d_e_off.alloc(n); c.d_e_cnt.alloc(n);
+        const uint64_t lslots = (uint64_t)n * lpv, eslots = (uint64_t)n * epv;
+        detail::alloc_out(c, n, lslots, eslots, sigma_words(), with_sigma);
+        pvac_ct_batch vc = c.view(with_sigma);
+        vc.n = n;
+        detail::dev_array<uint32_t> st(n);
+        check(pvac_hip_enc_value(ctx_, n, d_v.p, d_r.p, stride, &vc, with_sigma ? PVAC_ENC_WITH_SIGMA : 0, st.p));
+        status.resize(n);
+        st.download(status.data(), n, stream_);
+        return detail::from_device<CipherT>(c, n, lslots, eslots, prm_.m_bits, with_sigma, stream_);
+    }
+
     pvac_hip_params prm_;
     pvac_hip_ctx* ctx_ = nullptr;
     hipStream_t stream_ = nullptr;
     bool h_ready_ = false;
+    bool keys_ready_ = false;
+    std::vector<uint64_t> key_fp_;
 };
 
 // Process-wide engines keyed by canon_tag (one public key = one context), device 0 unless
@@ -431,6 +566,102 @@ std::vector<CipherT> ct_add_batch(const PubKeyT& pk, const std::vector<CipherT>&
     for (auto& x : A) a.push_back(&x);
     for (auto& x : B) b.push_back(&x);
     return engine_for(pk).ct_add(a, b, negate_b);
+}
+
+// ---- encryption / decryption (ops/encrypt.hpp:289, ops/decrypt.hpp:62) --------------------
+template <class CipherT, class PubKeyT, class SecKeyT>
+CipherT enc_value(const PubKeyT& pk, const SecKeyT& sk, uint64_t v, const RandomSource& rnd = os_random_u64) {
+    return engine_for(pk).template enc_value<PubKeyT, SecKeyT, CipherT>(pk, sk, std::vector<uint64_t>{v}, true, rnd)[0];
+}
+
+template <class CipherT, class PubKeyT, class SecKeyT>
+std::vector<CipherT> enc_value_batch(const PubKeyT& pk, const SecKeyT& sk, const std::vector<uint64_t>& vs,
+                                     bool with_sigma = true, const RandomSource& rnd = os_random_u64) {
+    return engine_for(pk).template enc_value<PubKeyT, SecKeyT, CipherT>(pk, sk, vs, with_sigma, rnd);
+}
+
+template <class PubKeyT, class SecKeyT, class CipherT>
+auto dec_value(const PubKeyT& pk, const SecKeyT& sk, const CipherT& C) {
+    using FpT = std::decay_t<decltype(C.E[0].w)>;
+    return engine_for(pk).template dec_value<PubKeyT, SecKeyT, CipherT, FpT>(pk, sk, std::vector<const CipherT*>{&C})[0];
+}
+
+template <class PubKeyT, class SecKeyT, class CipherT>
+auto dec_value_batch(const PubKeyT& pk, const SecKeyT& sk, const std::vector<CipherT>& cs) {
+    using FpT = std::decay_t<decltype(cs[0].E[0].w)>;
+    std::vector<const CipherT*> p;
+    for (auto& x : cs) p.push_back(&x);
+    return engine_for(pk).template dec_value<PubKeyT, SecKeyT, CipherT, FpT>(pk, sk, p);
+}
+
+// ---- .ct files (the reference's tests/add.cpp:22-155 format) through the native codec ------
+// Layers of PROD rule come back with zero seeds (the format stores none). m_bits: nbits given to
+// every edge's sigma on load when the file carries none.
+template <class CipherT>
+std::vector<CipherT> load_cts_bytes(const std::vector<uint8_t>& buf, uint32_t m_bits = 8192) {
+    pvac_ct_file_info info{};
+    int rc = pvac_ct_scan(buf.data(), buf.size(), &info);
+    if (rc) throw Error(rc, "load_cts: malformed .ct image");
+    if (info.flags & PVAC_CT_MIXED_SIGMA) throw Error(PVAC_ENOSYS, "load_cts: edges disagree on sigma nbits");
+    const size_t n = info.n_ciphers, nl = info.total_layers, ne = info.total_edges;
+    const uint32_t sw = info.sigma_words;
+    std::vector<uint64_t> l_off(n), l_cnt(n), e_off(n), e_cnt(n), meta(ne), w_lo(ne), w_hi(ne), sig(ne * sw);
+    std::vector<pvac_layer> layers(nl);
+    pvac_ct_batch X{};
+    X.n = n; X.l_off = l_off.data(); X.l_cnt = l_cnt.data(); X.layers = layers.data();
+    X.e_off = e_off.data(); X.e_cnt = e_cnt.data(); X.meta = meta.data(); X.w_lo = w_lo.data(); X.w_hi = w_hi.data();
+    X.sigma = sw ? sig.data() : nullptr;
+    X.sigma_words = sw;
+    rc = pvac_ct_parse(buf.data(), buf.size(), &X, 0);
+    if (rc) throw Error(rc, "load_cts: parse failed");
+    std::vector<CipherT> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        CipherT& C = out[i];
+        C.L.resize(l_cnt[i]);
+        for (size_t l = 0; l < l_cnt[i]; ++l) {
+            const pvac_layer& y = layers[l_off[i] + l];
+            auto& L = C.L[l];
+            L.rule = static_cast<decltype(L.rule)>(y.rule);
+            L.pa = y.pa; L.pb = y.pb;
+            L.seed.ztag = y.ztag; L.seed.nonce.lo = y.nonce_lo; L.seed.nonce.hi = y.nonce_hi;
+        }
+        C.E.resize(e_cnt[i]);
+        for (size_t k = 0; k < e_cnt[i]; ++k) {
+            const size_t e = e_off[i] + k;
+            auto& E = C.E[k];
+            E.layer_id = (uint32_t)meta[e];
+            E.idx = (uint16_t)(meta[e] >> 32);
+            E.ch = (uint8_t)(meta[e] >> 48);
+            E.w.lo = w_lo[e]; E.w.hi = w_hi[e];
+            E.s.nbits = sw ? info.sigma_bits : m_bits;
+            if (sw) E.s.w.assign(&sig[e * sw], &sig[e * sw] + sw);
+            else E.s.w.assign((m_bits + 63) / 64, 0);
+        }
+    }
+    return out;
+}
+
+// Every edge's sigma is written with nbits = sigma_bits (the reference writes m_bits = 8192).
+template <class CipherT>
+std::vector<uint8_t> save_cts_bytes(const std::vector<CipherT>& cs, uint32_t sigma_bits = 8192) {
+    const uint32_t sw = (sigma_bits + 63) / 64;
+    std::vector<const CipherT*> p;
+    for (auto& x : cs) p.push_back(&x);
+    detail::batch b;
+    detail::to_host(p, sw, true, b);
+    pvac_ct_batch X{};
+    X.n = cs.size(); X.l_off = b.l_off.data(); X.l_cnt = b.l_cnt.data(); X.layers = b.layers.data();
+    X.e_off = b.e_off.data(); X.e_cnt = b.e_cnt.data(); X.meta = b.meta.data();
+    X.w_lo = b.w_lo.data(); X.w_hi = b.w_hi.data();
+    X.sigma = b.sigma.data();
+    X.sigma_words = sw;
+    uint64_t bytes = 0, written = 0;
+    int rc = pvac_ct_serialized_size(&X, sigma_bits, &bytes);
+    if (rc) throw Error(rc, "save_cts: size");
+    std::vector<uint8_t> out(bytes);
+    rc = pvac_ct_write(&X, sigma_bits, out.data(), out.size(), &written, 0);
+    if (rc || written != bytes) throw Error(rc ? rc : PVAC_EINVAL, "save_cts: write");
+    return out;
 }
 
 }  // namespace pvac_hip

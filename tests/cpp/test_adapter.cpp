@@ -4,6 +4,7 @@
 // the unmodified reference (tests/golden/ref, tests/golden/bounty). Runs on the GPU box:
 //   test_adapter <golden_dir> <canon_tag> <H_digest_hex>
 // Exit 0 = every check passed; failures abort with a message (like the reference's must()).
+#include <array>
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
@@ -26,8 +27,13 @@ struct Cipher { std::vector<Layer> L; std::vector<Edge> E; };
 struct Params {
     int B = 337, m_bits = 8192, n_bits = 16384, h_col_wt = 192, x_col_wt = 128, err_wt = 128;
     size_t edge_budget = 1200000;
+    int lpn_n = 4096, lpn_t = 16384, lpn_tau_num = 1, lpn_tau_den = 8;
 };
-struct PubKey { Params prm; uint64_t canon_tag = 0; std::vector<BitVec> H; };
+struct PubKey {
+    Params prm; uint64_t canon_tag = 0; std::vector<BitVec> H;
+    std::array<uint8_t, 32> H_digest{}; std::vector<Fp> powg_B;
+};
+struct SecKey { std::array<uint64_t, 4> prf_k{}; std::vector<uint64_t> lpn_s_bits; };
 }  // namespace mirror
 
 using mirror::Cipher;
@@ -183,9 +189,17 @@ struct replay {
     }
 };
 
+// replays an enc_value getrandom log; the adapter draws a whole stride per value, so reads
+// past the log return 0 (they are never consumed by the kernels) and are counted
+struct replay_pad {
+    std::vector<uint64_t> s;
+    size_t k = 0;
+    uint64_t operator()() { return k < s.size() ? s[k++] : (++k, 0ull); }
+};
+
 int main(int argc, char** argv) {
-    if (argc < 4) {
-        std::fprintf(stderr, "usage: %s <golden_dir> <canon_tag> <H_digest_hex>\n", argv[0]);
+    if (argc < 5) {
+        std::fprintf(stderr, "usage: %s <golden_dir> <canon_tag> <H_digest_hex> <v0,v1,...>\n", argv[0]);
         return 2;
     }
     const std::string gold = argv[1], ref = gold + "/ref", bounty = gold + "/bounty";
@@ -275,6 +289,52 @@ int main(int argc, char** argv) {
             MUST(lo == read_u64(ref + "/fp_" + op.second + "_lo.u64") && hi == read_u64(ref + "/fp_" + op.second + "_hi.u64"),
                  "fp_%s", op.second);
         }
+    }
+
+    // enc_value / dec_value (ops/encrypt.hpp:289, ops/decrypt.hpp:62) replaying the getrandom
+    // streams the reference consumed (harness cmd_enc): byte-identical .ct, decrypts to v
+    {
+        for (int i = 0; i < 32; ++i) pk.H_digest[i] = (uint8_t)std::strtoul(hdig.substr(2 * i, 2).c_str(), nullptr, 16);
+        const auto pg = read_u64(ref + "/powg_B.u64");
+        for (size_t i = 0; i + 1 < pg.size(); i += 2) pk.powg_B.push_back(mirror::Fp{pg[i], pg[i + 1]});
+        mirror::SecKey sk;
+        const auto kk = read_u64(ref + "/sk_prf_k.u64");
+        MUST(kk.size() == 4, "sk_prf_k.u64");
+        for (int i = 0; i < 4; ++i) sk.prf_k[i] = kk[i];
+        sk.lpn_s_bits = read_u64(ref + "/sk_lpn_s.u64");
+        std::vector<uint64_t> vs;
+        for (const char* p = argv[4]; *p;) {
+            char* e = nullptr;
+            vs.push_back(std::strtoull(p, &e, 10));
+            p = *e ? e + 1 : e;
+        }
+        MUST(!vs.empty(), "no enc values");
+        for (size_t i = 0; i < vs.size(); ++i) {
+            replay_pad rs{read_u64(ref + "/enc" + std::to_string(i) + "_stream.u64")};
+            const Cipher c = pvac_hip::enc_value<Cipher>(pk, sk, vs[i], std::ref(rs));
+            MUST(rs.k >= rs.s.size(), "enc %zu consumed %zu of %zu words", i, rs.k, rs.s.size());
+            MUST(write_ct({c}) == slurp(ref + "/enc" + std::to_string(i) + ".ct"), "enc_value %zu .ct bytes", i);
+            const auto m = pvac_hip::dec_value(pk, sk, c);
+            MUST(m.lo == vs[i] && m.hi == 0, "dec_value(enc %zu)", i);
+        }
+        // fresh randomness, batched both ways
+        const auto cs = pvac_hip::enc_value_batch<Cipher>(pk, sk, vs);
+        const auto ms = pvac_hip::dec_value_batch(pk, sk, cs);
+        for (size_t i = 0; i < vs.size(); ++i) MUST(ms[i].lo == vs[i] && ms[i].hi == 0, "batch roundtrip %zu", i);
+        // homomorphic: dec(enc(a) + enc(b)) = a + b, dec(enc(a) * enc(b)) = a * b (small values)
+        const Cipher s = pvac_hip::ct_add(pk, cs[1], cs[2]);
+        const Cipher p = pvac_hip::ct_mul(pk, cs[1], cs[2]);
+        MUST(pvac_hip::dec_value(pk, sk, s).lo == vs[1] + vs[2], "dec(ct_add)");
+        MUST(pvac_hip::dec_value(pk, sk, p).lo == vs[1] * vs[2], "dec(ct_mul)");
+    }
+
+    // .ct codec through the adapter: load then save reproduces the reference's file bytes
+    for (const char* f : {"/pair0_mul.ct", "/enc3.ct", "/chain3.ct"}) {
+        const auto bytes = slurp(ref + f);
+        const auto cs = pvac_hip::load_cts_bytes<Cipher>(bytes);
+        MUST(same_edges(cs[0], read_ct(ref + f)[0], true), "load_cts %s", f);
+        const uint32_t nb = cs[0].E.empty() ? 8192u : (uint32_t)cs[0].E[0].s.nbits;
+        MUST(pvac_hip::save_cts_bytes(cs, nb) == bytes, "save_cts %s", f);
     }
 
     std::printf("test_adapter: %d checks passed\n", g_checks);

@@ -1,6 +1,6 @@
 """The C++ drop-in adapter (include/pvac_hip.hpp): built by __graft_entry__.build() into
 tests/cpp/build/test_adapter; on the GPU box it replays the reference's golden streams through the
-by-value API (ct_add/ct_sub/ct_scale/ct_mul with sigma/chains/fp) and compares byte for byte."""
+by-value API (ct_add/ct_sub/ct_scale/ct_mul with sigma/chains/fp, enc_value/dec_value, .ct load/save) and compares byte for byte."""
 import json
 import os
 import subprocess
@@ -27,7 +27,9 @@ def test_adapter_against_golden():
     assert os.path.exists(EXE), "tests/cpp/build/test_adapter missing: build() must compile it"
     with open(os.path.join(GOLD, "ref", "manifest.json")) as f:
         man = json.load(f)
-    r = subprocess.run([EXE, GOLD, str(man["canon_tag"]), man["H_digest"]], capture_output=True, text=True,
+    with open(os.path.join(GOLD, "ref", "enc_manifest.json")) as f:
+        vs = ",".join(str(e["v"]) for e in json.load(f)["enc"])
+    r = subprocess.run([EXE, GOLD, str(man["canon_tag"]), man["H_digest"], vs], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "checks passed" in r.stdout
