@@ -595,10 +595,10 @@ auto dec_value_batch(const PubKeyT& pk, const SecKeyT& sk, const std::vector<Cip
 }
 
 // ---- .ct files (the reference's tests/add.cpp:22-155 format) through the native codec ------
-// Layers of PROD rule come back with zero seeds (the format stores none). m_bits: nbits given to
-// every edge's sigma on load when the file carries none.
+// Layers of PROD rule come back with zero seeds (the format stores none); sigmas come back as
+// stored (nbits 0 and no words when the file carries none).
 template <class CipherT>
-std::vector<CipherT> load_cts_bytes(const std::vector<uint8_t>& buf, uint32_t m_bits = 8192) {
+std::vector<CipherT> load_cts_bytes(const std::vector<uint8_t>& buf) {
     pvac_ct_file_info info{};
     int rc = pvac_ct_scan(buf.data(), buf.size(), &info);
     if (rc) throw Error(rc, "load_cts: malformed .ct image");
@@ -633,9 +633,8 @@ std::vector<CipherT> load_cts_bytes(const std::vector<uint8_t>& buf, uint32_t m_
             E.idx = (uint16_t)(meta[e] >> 32);
             E.ch = (uint8_t)(meta[e] >> 48);
             E.w.lo = w_lo[e]; E.w.hi = w_hi[e];
-            E.s.nbits = sw ? info.sigma_bits : m_bits;
-            if (sw) E.s.w.assign(&sig[e * sw], &sig[e * sw] + sw);
-            else E.s.w.assign((m_bits + 63) / 64, 0);
+            E.s.nbits = info.sigma_bits;
+            E.s.w.assign(sig.begin() + e * sw, sig.begin() + (e + 1) * sw);
         }
     }
     return out;
