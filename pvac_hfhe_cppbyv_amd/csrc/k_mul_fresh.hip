@@ -51,21 +51,24 @@ namespace {
 
 constexpr uint32_t kTInf = 0xFFFFFFFFu;
 static_assert(kFreshLayersMax <= 64, "layer masks are u64");
+static_assert(kFreshKeysMax <= 2048 && kFreshLayersMax <= 512, "writer entries pack slot, idx (11 bits each) and layer");
 
 // ---------------------------------------------------------------- layer records
-constexpr int kLayBlock = 128;
+constexpr int kLayBlock = 256;
+constexpr int kLayLanes = 4;   // lanes per pair: output layers (and their SHA-256 ztags) split over them
 
 __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g) {
-    const uint64_t pr = (uint64_t)blockIdx.x * kLayBlock + threadIdx.x;
+    const uint64_t pr = ((uint64_t)blockIdx.x * kLayBlock + threadIdx.x) / kLayLanes;
+    const uint32_t sub = threadIdx.x % kLayLanes;
     if (pr >= g.A.n) return;
     fresh_rec rec{};
     if (g.pair_class[pr] != PAIR_SMALL) {   // nbk = 0: the aggregation kernel skips the pair
-        g.recs[pr] = rec;
+        if (sub == 0) g.recs[pr] = rec;
         return;
     }
     const uint32_t LA = (uint32_t)g.A.l_cnt[pr], LB = (uint32_t)g.B.l_cnt[pr];
     const uint64_t alo = g.A.l_off[pr], blo = g.B.l_off[pr], clo = g.C.l_off[pr];
-    {
+    if (sub == 0) {
         const uint32_t nA = (uint32_t)g.A.e_cnt[pr], nB = (uint32_t)g.B.e_cnt[pr];
         rec.aeo = g.A.e_off[pr]; rec.beo = g.B.e_off[pr]; rec.ceo = g.C.e_off[pr];
         rec.alo = alo; rec.blo = blo; rec.clo = clo;
@@ -75,14 +78,17 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
         rec.LA = (uint8_t)LA; rec.LB = (uint8_t)LB;
         g.recs[pr] = rec;
     }
-    for (uint32_t l = 0; l < LA; ++l) g.C.layers[clo + l] = g.A.layers[alo + l];
-    for (uint32_t l = 0; l < LB; ++l) {
-        pvac_layer y = g.B.layers[blo + l];
-        if (y.rule == 1) { y.pa += LA; y.pb += LA; }
-        g.C.layers[clo + LA + l] = y;
-    }
     const uint32_t base = LA + LB, LP = LA * LB;
-    for (uint32_t lp = 0; lp < LP; ++lp) {
+    for (uint32_t l = sub; l < base; l += kLayLanes) {
+        if (l < LA) {
+            g.C.layers[clo + l] = g.A.layers[alo + l];
+        } else {
+            pvac_layer y = g.B.layers[blo + (l - LA)];
+            if (y.rule == 1) { y.pa += LA; y.pb += LA; }
+            g.C.layers[clo + l] = y;
+        }
+    }
+    for (uint32_t lp = sub; lp < LP; lp += kLayLanes) {
         const uint64_t slot = clo + base + lp;
         pvac_layer y;
         y.rule = 1;
@@ -274,7 +280,21 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const uint32_t Bm = gq->Bm;
-    const float inv_b = 1.0f / (float)Bm;
+    // The slots a thread owns (s = tid + k*BS) are the same for every pair: their (lp, r) split
+    // is computed once, and their libstdc++ buckets once per distinct bucket count. Packed per
+    // slot: bucket (15 bits) | r << 15 (11 bits) | lp << 26 (6 bits; only slots < KS are used,
+    // where lp < |C.L| <= 64).
+    uint32_t sinfo[KI];
+    uint32_t nbk_c = 0;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+        const uint32_t s = tid + (uint32_t)k * BS;
+        const uint32_t lp = s / Bm;
+        sinfo[k] = ((s - lp * Bm) << 15) | (min(lp, 63u) << 26);
+    }
+#define SLOT_LP(k) (sinfo[k] >> 26)
+#define SLOT_R(k) ((sinfo[k] >> 15) & 0x7FFu)
+#define SLOT_BK(k) (sinfo[k] & 0x7FFFu)
 
     // one-time clear: accumulators 0, first-insert times INF
     for (uint32_t w = tid; w < acc_words / 4u; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
@@ -373,7 +393,15 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 
         // ---- S2a: every thread owns key slots s = tid + k*BS: fold the limbs, clear them, hash
         //      the key to its libstdc++ bucket
-        const fastmod64 fm{nbk, cur.nb_magic};
+        if (nbk != nbk_c) {   // workgroup-uniform: a new reserve() size
+            const fastmod64 fm{nbk, cur.nb_magic};
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t b = (uint32_t)fmod64((((uint64_t)SLOT_LP(k) << 32) | SLOT_R(k)) * kGolden, fm);
+                sinfo[k] = (sinfo[k] & ~0x7FFFu) | b;   // std::hash -> bucket
+            }
+            nbk_c = nbk;
+        }
         fp sumP[KI], sumM[KI];
         uint32_t kt[KI], eb[KI], bk[KI];
         uint64_t myor = 0;
@@ -393,19 +421,15 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         }
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            const uint32_t s = tid + (uint32_t)k * BS;
-            eb[k] = 0; bk[k] = 0;
+            eb[k] = 0;
+            bk[k] = SLOT_BK(k);
             sumP[k] = fp{0, 0};
             sumM[k] = fp{0, 0};
             if (kt[k] != kTInf) {
-                // s / B for s < 1536: the float quotient of s + 1/2 is exact after floor
-                const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), r = s - lp * Bm;
                 sumP[k] = fp_fold3_lazy(lim[k][0].x, lim[k][0].y, lim[k][1].x);
                 sumM[k] = fp_fold3_lazy(lim[k][1].y, lim[k][2].x, lim[k][2].y);
                 eb[k] = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
-                const uint64_t key = ((uint64_t)lp << 32) | r;
-                bk[k] = (uint32_t)fmod64(key * kGolden, fm);   // std::hash -> bucket
-                if (eb[k]) myor |= 1ull << lp;
+                if (eb[k]) myor |= 1ull << SLOT_LP(k);
             }
         }
 #pragma unroll
@@ -537,7 +561,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         const bool gather = !canonical && inv_base + total <= acc_words;
         const uint64_t ceo = cur.ceo;
         uint32_t* inv = accw + inv_base;
+        const bool ident = misc[MF_IDENT] != 0;
         if (gather) {
+            // writer entry: slot (11 bits) | channel << 11 | idx << 12 | output layer << 23
 #pragma unroll
             for (int k = 0; k < KI; ++k) {
                 const uint32_t s = tid + (uint32_t)k * BS;
@@ -545,8 +571,12 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                     tkey[s] = kTInf;
                     nxtl[s] = 0;
                     uint32_t p = G[tb[k]] + within[k];
-                    if (eb[k] & 1u) inv[p++] = s << 1;
-                    if (eb[k] & 2u) inv[p] = (s << 1) | 1u;
+                    if (eb[k]) {
+                        const uint32_t lid = ident ? base + SLOT_LP(k) : remap[base + SLOT_LP(k)];
+                        const uint32_t e = s | (SLOT_R(k) << 12) | (lid << 23);
+                        if (eb[k] & 1u) inv[p++] = e;
+                        if (eb[k] & 2u) inv[p] = e | (1u << 11);
+                    }
                     if (!(eb[k] & 1u)) ksum[2 * s] = make_ulonglong2(0, 0);       // never read by a writer
                     if (!(eb[k] & 2u)) ksum[2 * s + 1] = make_ulonglong2(0, 0);
                 }
@@ -569,8 +599,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                     nxtl[s] = 0;
                 }
                 if (eb[k]) {
-                    const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), idx = s - lp * Bm;
-                    const uint32_t lid = remap[base + lp];
+                    const uint32_t idx = SLOT_R(k);
+                    const uint32_t lid = ident ? base + SLOT_LP(k) : remap[base + SLOT_LP(k)];
                     uint32_t* sp = gq->salt_pos;
                     if (eb[k] & 1u) {
                         const ulonglong2 w = ksum[2 * s];
@@ -624,9 +654,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             uint32_t* sp = gq->salt_pos;
             for (uint32_t p = tid; p < total; p += BS) {
                 const uint32_t e = inv[p];
-                const uint32_t s = e >> 1, ch = e & 1u;
-                const uint32_t lp = (uint32_t)__float2uint_rd(((float)s + 0.5f) * inv_b), idx = s - lp * Bm;
-                const uint32_t lid = remap[base + lp];
+                const uint32_t s = e & 0x7FFu, ch = (e >> 11) & 1u, idx = (e >> 12) & 0x7FFu, lid = e >> 23;
                 const ulonglong2 w = ksum[2 * s + ch];
                 inv[p] = 0;
                 ksum[2 * s + ch] = make_ulonglong2(0, 0);
@@ -654,6 +682,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         PHASE_STAMP(9);
         cur = nxt;
     }
+#undef SLOT_LP
+#undef SLOT_R
+#undef SLOT_BK
 #ifdef PVAC_PHASE_STAMPS
     if (threadIdx.x == 0 && blockIdx.x < 4096)
         for (int p = 0; p < kStampPhases; ++p) g_fresh_stamps[blockIdx.x * kStampPhases + p] = st_acc_[p];
@@ -671,7 +702,7 @@ extern "C" int pvac_hip_diag_fresh_stamps(unsigned long long* host, size_t n) {
 
 hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st) {
     if (!a.A.n) return hipSuccess;
-    hipLaunchKernelGGL(k_mul_layers_fresh, dim3((unsigned)((a.A.n + kLayBlock - 1) / kLayBlock)), dim3(kLayBlock), 0,
+    hipLaunchKernelGGL(k_mul_layers_fresh, dim3((unsigned)((a.A.n * kLayLanes + kLayBlock - 1) / kLayBlock)), dim3(kLayBlock), 0,
                        st, a);
     return hipGetLastError();
 }
