@@ -31,7 +31,7 @@ namespace pvhip {
 // Diagnostic build only (make diag -> lib/libpvac_hip_diag.so): wave 0 of every workgroup
 // accumulates s_memtime deltas per phase into a debug array; never touches kernel outputs.
 #ifdef PVAC_PHASE_STAMPS
-constexpr int kStampPhases = 12;
+constexpr int kStampPhases = 18;
 __device__ unsigned long long g_fresh_stamps[4096 * kStampPhases];
 #define PHASE_STAMP(ph)                                                  \
     do {                                                                 \
@@ -41,9 +41,18 @@ __device__ unsigned long long g_fresh_stamps[4096 * kStampPhases];
             st_last_ = now_;                                             \
         }                                                                \
     } while (0)
+// sub-phase stamp after this wave's LDS traffic has completed (diagnostic build only)
+#define PHASE_STAMP_SYNC(ph)                                   \
+    do {                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
+        PHASE_STAMP(ph);                                       \
+    } while (0)
 #else
 #define PHASE_STAMP(ph) \
     do {                \
+    } while (0)
+#define PHASE_STAMP_SYNC(ph) \
+    do {                     \
     } while (0)
 #endif
 
@@ -105,15 +114,19 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
 // ---------------------------------------------------------------- aggregation + emit
 struct fresh_layout {
     // byte offsets into dynamic LDS
-    uint32_t acc, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
+    uint32_t acc, heads, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
-__host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint32_t nb) {
+// A key slot is 48 bytes: during S1 the limbs P0 P1 P2 M0 M1 M2; from S2 on the P sum (bytes
+// 0-15), the M sum (16-31) and a zero tail (32-47) that hosts G (u16, bytes 32-39 of slot t/4)
+// and the writer map inv (u32, bytes 40-47 of slot p/2). heads: bucket chain heads (u32).
+__host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint32_t nb, uint32_t nbk) {
     fresh_layout L;
     uint32_t o = 0;
     L.acc = o;   o = align16(o + ks * 48u);           // 2 channels x 3 u64 limbs per key slot
+    L.heads = o; o = align16(o + nbk * 4u);
     L.tkey = o;  o = align16(o + ks * 4u);
     L.a_w = o;   o = align16(o + na * 16u);
     L.a_inf = o; o = align16(o + na * 4u);
@@ -265,8 +278,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     argp gq = launder((uint64_t)gp);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     unsigned long long* acc = (unsigned long long*)(lds + Ls.acc);
-    uint32_t* accw = (uint32_t*)(lds + Ls.acc);           // u32 view: heads | G | nxt | key sums | inv
-    const uint32_t acc_words = (Ls.tkey - Ls.acc) / 4u;
+    ulonglong2* ksu = (ulonglong2*)(lds + Ls.acc);        // 16-byte units: slot s = units 3s .. 3s+2
+    uint8_t* accb = lds + Ls.acc;
+    uint32_t* heads = (uint32_t*)(lds + Ls.heads);
     uint32_t* tkey = (uint32_t*)(lds + Ls.tkey);
     ulonglong2* a_w = (ulonglong2*)(lds + Ls.a_w);
     uint32_t* a_inf = (uint32_t*)(lds + Ls.a_inf);
@@ -296,8 +310,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 #define SLOT_R(k) ((sinfo[k] >> 15) & 0x7FFu)
 #define SLOT_BK(k) (sinfo[k] & 0x7FFFu)
 
-    // one-time clear: accumulators 0, first-insert times INF
-    for (uint32_t w = tid; w < acc_words / 4u; w += BS) ((uint4*)accw)[w] = make_uint4(0, 0, 0, 0);
+    // one-time clear: accumulators and bucket heads 0, first-insert times INF
+    for (uint32_t w = tid; w < (Ls.tkey - Ls.acc) / 16u; w += BS) ((uint4*)lds)[Ls.acc / 16u + w] = make_uint4(0, 0, 0, 0);
     for (uint32_t s = tid; s < gq->ks_max; s += BS) tkey[s] = kTInf;
     if (tid < 32) misc[tid] = 0;
     __syncthreads();
@@ -323,10 +337,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
         const uint32_t base = LA + LB, Lc = base + LP;
         const uint32_t nbk = cur.nbk;
-        // acc region reuse after S2a (u32 words): heads[nbk] | G u16[n] | nxt u16[KS] | key sums
-        // (8 words per slot) | inv[total]
-        const uint32_t sum_base = (nbk + (n + 1u) / 2u + (KS + 1u) / 2u + 3u) & ~3u;
-        const uint32_t inv_base = sum_base + 8u * KS;
+        // G[t] and inv[p] in the slot tails (see fresh_lds)
+        auto G_at = [&](uint32_t t) { return (uint16_t*)(accb + (t >> 2) * 48u + 32u + (t & 3u) * 2u); };
+        auto inv_at = [&](uint32_t q) { return (uint32_t*)(accb + (q >> 1) * 48u + 40u + (q & 1u) * 4u); };
 
         if (misc[MF_INVALID]) {   // invalid references: reject the pair (reference behaviour is UB)
             __syncthreads();
@@ -385,6 +398,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 }
             }
         }
+        PHASE_STAMP_SYNC(11);
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(1);
@@ -405,8 +419,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         fp sumP[KI], sumM[KI];
         uint32_t kt[KI], eb[KI], bk[KI];
         uint64_t myor = 0;
-        // all reads first (the zeroing stores below would otherwise pin every later read behind
-        // them: same LDS array), then the arithmetic, then the zeroing
+        // all reads first (the stores below would otherwise pin every later read behind them: same
+        // LDS array), then the arithmetic, then the exchanges and in-place stores
         ulonglong2 lim[KI][3];
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
@@ -416,9 +430,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
-            const ulonglong2* q = (const ulonglong2*)(acc + (size_t)min(s, KS - 1u) * 6);
+            const ulonglong2* q = ksu + (size_t)min(s, KS - 1u) * 3;
             lim[k][0] = q[0]; lim[k][1] = q[1]; lim[k][2] = q[2];
         }
+        PHASE_STAMP_SYNC(12);
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             eb[k] = 0;
@@ -432,41 +447,33 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 if (eb[k]) myor |= 1ull << SLOT_LP(k);
             }
         }
+        PHASE_STAMP(13);
+        // bucket chains: exchanges back to back, one wait for all (heads has its own region)
+        uint32_t prev[KI];
+#pragma unroll
+        for (int k = 0; k < KI; ++k)
+            prev[k] = kt[k] != kTInf ? atomicExch(&heads[bk[k]], tid + (uint32_t)k * BS + 1u) : 0u;
+        // key sums in place over the slot's own limbs (a zero sum is the zero unit), tail zeroed
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
             if (kt[k] != kTInf) {
-                ulonglong2* q = (ulonglong2*)(acc + (size_t)s * 6);
-                q[0] = make_ulonglong2(0, 0); q[1] = make_ulonglong2(0, 0); q[2] = make_ulonglong2(0, 0);
+                ulonglong2* q = ksu + (size_t)s * 3;
+                q[0] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
+                q[1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
+                q[2] = make_ulonglong2(0, 0);
             }
         }
         myor = wave_or_u64(myor);
         if (lane == 0) wave_lp[wave] = myor;
-        __syncthreads();   // every limb is read and zeroed: chains and key sums may use the region
-        gq = launder(gq);
-        PHASE_STAMP(2);
-
-        // ---- S2b: key sums to LDS (by slot, beside the chains), bucket chains
-        uint32_t* heads = accw;
-        uint16_t* G = (uint16_t*)(heads + nbk);
-        uint16_t* nxtl = G + n;
-        ulonglong2* ksum = (ulonglong2*)(accw + sum_base);   // [2 s] = P, [2 s + 1] = M
-        uint32_t prev[KI];
+        // chain entry: time (12 bits) | next slot + 1 (11 bits) << 12 | channels present << 23
 #pragma unroll
-        for (int k = 0; k < KI; ++k)   // exchanges back to back, one wait for all
-            prev[k] = kt[k] != kTInf ? atomicExch(&heads[bk[k]], tid + (uint32_t)k * BS + 1u) : 0u;
-#pragma unroll
-        for (int k = 0; k < KI; ++k) {
-            const uint32_t s = tid + (uint32_t)k * BS;
-            if (kt[k] != kTInf) {
-                ksum[2 * s] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
-                ksum[2 * s + 1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
-                nxtl[s] = (uint16_t)(prev[k] | (eb[k] << 14));
-            }
-        }
+        for (int k = 0; k < KI; ++k)
+            if (kt[k] != kTInf) tkey[tid + (uint32_t)k * BS] = kt[k] | (prev[k] << 12) | (eb[k] << 23);
+        PHASE_STAMP_SYNC(14);
         __syncthreads();
         gq = launder(gq);
-        PHASE_STAMP(3);
+        PHASE_STAMP(2);
 
         // ---- S2c: walk chains -> bucket first-insert time, rank inside the bucket, group sizes;
         //      wave 0 then runs compact_layers (encrypt.hpp:73-104) as a bitmask closure
@@ -481,27 +488,24 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         // the three walks advance together: one LDS round trip per step for all of them
         while (cq[0] | cq[1] | cq[2]) {
             static_assert(KI == 3, "walk interleave assumes three slots per thread");
-            uint32_t t2[KI], nx[KI];
+            uint32_t v[KI];
 #pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t s2 = (cq[k] ? cq[k] : 1u) - 1u;
-                t2[k] = tkey[s2];
-                nx[k] = nxtl[s2];
-            }
+            for (int k = 0; k < KI; ++k) v[k] = tkey[(cq[k] ? cq[k] : 1u) - 1u];
 #pragma unroll
             for (int k = 0; k < KI; ++k) {
                 if (cq[k]) {
-                    const uint32_t e2 = __popc(nx[k] >> 14);
-                    tb[k] = t2[k] < tb[k] ? t2[k] : tb[k];
-                    within[k] += t2[k] > kt[k] ? e2 : 0u;
+                    const uint32_t t2 = v[k] & 0xFFFu, e2 = __popc(v[k] >> 23);
+                    tb[k] = t2 < tb[k] ? t2 : tb[k];
+                    within[k] += t2 > kt[k] ? e2 : 0u;
                     cE[k] += e2;
-                    cq[k] = nx[k] & 0x3FFFu;
+                    cq[k] = (v[k] >> 12) & 0x7FFu;
                 }
             }
         }
+        PHASE_STAMP(15);
 #pragma unroll
         for (int k = 0; k < KI; ++k)
-            if (kt[k] != kTInf && tb[k] == kt[k]) G[tb[k]] = (uint16_t)cE[k];
+            if (kt[k] != kTInf && tb[k] == kt[k]) *G_at(tb[k]) = (uint16_t)cE[k];
         if (wave == 0) {
             const uint64_t all = Lc >= 64 ? ~0ull : ((1ull << Lc) - 1ull);
             uint64_t used_lp = 0;
@@ -534,13 +538,13 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             const uint32_t per = (n + BS - 1) / BS;
             const uint32_t r0 = tid * per;   // reversed positions r in [r0, r0 + per), t = n-1-r
             uint32_t local = 0;
-            for (uint32_t r = r0; r < r0 + per && r < n; ++r) local += G[n - 1 - r];
+            for (uint32_t r = r0; r < r0 + per && r < n; ++r) local += *G_at(n - 1 - r);
             uint32_t total;
             uint32_t run = block_exclusive_scan<BS>(local, misc + MF_PART, total);
             for (uint32_t r = r0; r < r0 + per && r < n; ++r) {
-                const uint32_t t = n - 1 - r;
-                const uint32_t v = G[t];
-                G[t] = (uint16_t)run;
+                uint16_t* g = G_at(n - 1 - r);
+                const uint32_t v = *g;
+                *g = (uint16_t)run;
                 run += v;
             }
             if (tid == 0) misc[MF_TOTAL] = total;
@@ -550,17 +554,25 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         PHASE_STAMP(5);
 
         // ---- S4: emit positions
+        // Stage the next pair first: its prefetched loads are the only vector-memory operations in
+        // flight here, so their wait does not also wait for this pair's output stores (S4/S5).
+        // a_w/a_inf/b_w/b_inf and pm are free (last read in S1 / S2c).
+#ifdef PVAC_PHASE_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHASE_STAMP(16);
+#endif
+        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+        PHASE_STAMP_SYNC(17);
         const uint32_t total = misc[MF_TOTAL];
         // guard_budget (encrypt.hpp:106-111): above edge_budget the reference runs compact_edges,
         // whose output is (layer, idx, P before M) order; product edges are already unique per
         // (layer, idx, ch) and nonzero, so it only re-orders them.
         const bool canonical = (gq->flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > gq->edge_budget;
-        // reference (hash) order: owners publish their edges' positions (inv[p] = slot, channel) and
-        // a writer pass stores positions p = tid, tid + BS, ... contiguously. Canonical order, or a
-        // pair whose inverse map does not fit beside the key sums, stores from the owners instead.
-        const bool gather = !canonical && inv_base + total <= acc_words;
+        // reference (hash) order: owners publish their edges' positions (inv[p]) and a writer pass
+        // stores positions p = tid, tid + BS, ... contiguously (total <= 2 KS: inv always fits).
+        // Canonical order stores from the owners instead.
+        const bool gather = !canonical;
         const uint64_t ceo = cur.ceo;
-        uint32_t* inv = accw + inv_base;
         const bool ident = misc[MF_IDENT] != 0;
         if (gather) {
             // writer entry: slot (11 bits) | channel << 11 | idx << 12 | output layer << 23
@@ -569,16 +581,13 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 const uint32_t s = tid + (uint32_t)k * BS;
                 if (kt[k] != kTInf) {
                     tkey[s] = kTInf;
-                    nxtl[s] = 0;
-                    uint32_t p = G[tb[k]] + within[k];
+                    uint32_t p = *G_at(tb[k]) + within[k];
                     if (eb[k]) {
                         const uint32_t lid = ident ? base + SLOT_LP(k) : remap[base + SLOT_LP(k)];
                         const uint32_t e = s | (SLOT_R(k) << 12) | (lid << 23);
-                        if (eb[k] & 1u) inv[p++] = e;
-                        if (eb[k] & 2u) inv[p] = e | (1u << 11);
+                        if (eb[k] & 1u) *inv_at(p++) = e;
+                        if (eb[k] & 2u) *inv_at(p) = e | (1u << 11);
                     }
-                    if (!(eb[k] & 1u)) ksum[2 * s] = make_ulonglong2(0, 0);       // never read by a writer
-                    if (!(eb[k] & 2u)) ksum[2 * s + 1] = make_ulonglong2(0, 0);
                 }
             }
         } else {
@@ -587,23 +596,20 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             for (int k = 0; k < KI; ++k) {
                 const uint32_t s = tid + (uint32_t)k * BS;
                 const bool own = kt[k] != kTInf;
-                const uint32_t hp = own ? G[tb[k]] + within[k] : 0u;
+                const uint32_t hp = own ? *G_at(tb[k]) + within[k] : 0u;
                 uint32_t p = hp;
                 if (canonical) {   // workgroup-uniform: row k = slots k*BS.., i.e. slot order
                     uint32_t rowtot;
                     p = rowbase + block_exclusive_scan<BS>(__popc(eb[k]), misc + MF_PART, rowtot);
                     rowbase += rowtot;
                 }
-                if (own) {
-                    tkey[s] = kTInf;
-                    nxtl[s] = 0;
-                }
+                if (own) tkey[s] = kTInf;
                 if (eb[k]) {
                     const uint32_t idx = SLOT_R(k);
                     const uint32_t lid = ident ? base + SLOT_LP(k) : remap[base + SLOT_LP(k)];
                     uint32_t* sp = gq->salt_pos;
                     if (eb[k] & 1u) {
-                        const ulonglong2 w = ksum[2 * s];
+                        const ulonglong2 w = ksu[3 * s];
                         gq->C.meta[ceo + p] = make_meta(lid, idx, 0);
                         gq->C.w_lo[ceo + p] = w.x;
                         gq->C.w_hi[ceo + p] = w.y;
@@ -611,7 +617,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                         ++p;
                     }
                     if (eb[k] & 2u) {
-                        const ulonglong2 w = ksum[2 * s + 1];
+                        const ulonglong2 w = ksu[3 * s + 1];
                         gq->C.meta[ceo + p] = make_meta(lid, idx, 1);
                         gq->C.w_lo[ceo + p] = w.x;
                         gq->C.w_hi[ceo + p] = w.y;
@@ -619,8 +625,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                     }
                 }
                 if (own) {
-                    ksum[2 * s] = make_ulonglong2(0, 0);
-                    ksum[2 * s + 1] = make_ulonglong2(0, 0);
+                    ksu[3 * s] = make_ulonglong2(0, 0);
+                    ksu[3 * s + 1] = make_ulonglong2(0, 0);
                 }
             }
         }
@@ -653,11 +659,12 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         if (gather) {
             uint32_t* sp = gq->salt_pos;
             for (uint32_t p = tid; p < total; p += BS) {
-                const uint32_t e = inv[p];
+                uint32_t* ip = inv_at(p);
+                const uint32_t e = *ip;
                 const uint32_t s = e & 0x7FFu, ch = (e >> 11) & 1u, idx = (e >> 12) & 0x7FFu, lid = e >> 23;
-                const ulonglong2 w = ksum[2 * s + ch];
-                inv[p] = 0;
-                ksum[2 * s + ch] = make_ulonglong2(0, 0);
+                const ulonglong2 w = ksu[3 * s + ch];
+                *ip = 0;
+                ksu[3 * s + ch] = make_ulonglong2(0, 0);
                 gq->C.meta[ceo + p] = make_meta(lid, idx, ch);
                 gq->C.w_lo[ceo + p] = w.x;
                 gq->C.w_hi[ceo + p] = w.y;
@@ -671,12 +678,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         //      cache warm-up); its value is consumed only after the barrier, whose wait it shares.
         uint32_t touch = 0;
         if (nxt.pr != kNoPair && nxt.pr + gridDim.x < gq->A.n) touch = ((recp)gq->recs)[nxt.pr + gridDim.x].nbk;
-        {
-            const uint32_t words = nbk + (n + 1u) / 2u;
-            for (uint32_t w = tid; w < words; w += BS) accw[w] = 0;
-        }
+        for (uint32_t w = tid; w < nbk; w += BS) heads[w] = 0;
+        for (uint32_t q = tid; q < (n + 3u) / 4u; q += BS) *(uint64_t*)(accb + q * 48u + 32u) = 0;   // G
         PHASE_STAMP(7);
-        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
         __syncthreads();
         asm volatile("" ::"s"(touch));
         PHASE_STAMP(9);
@@ -712,11 +716,10 @@ hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* ar
     if (a.ks_max > kFreshKeysMax || a.layers_max > kFreshLayersMax || a.na_max > kFreshEdgesMax ||
         a.nb_max > kFreshEdgesMax)
         return hipErrorInvalidValue;
-    const fresh_layout L = fresh_lds(a.ks_max, a.na_max, a.nb_max);
-    // chains (heads | G | nxt) and the key sums (8 words per key) share the accumulator region
-    // (the plan routes pairs that would not fit to the general path)
-    if ((uint64_t)(a.buckets_max + a.prod_max + a.ks_max + 3u) + 8ull * a.ks_max > (uint64_t)a.ks_max * 12u)
-        return hipErrorInvalidValue;
+    const fresh_layout L = fresh_lds(a.ks_max, a.na_max, a.nb_max, a.buckets_max);
+    // G (one u16 per product time) lives in the slot tails: 4 per slot (the plan keeps |A.E||B.E|
+    // <= 3 |A.L||B.L|B for fresh-path pairs)
+    if ((uint64_t)a.prod_max > 4ull * a.ks_max) return hipErrorInvalidValue;
     if (L.total > 160u * 1024u) return hipErrorInvalidValue;
     const int per_cu = L.total <= 80u * 1024u ? 2 : 1;
     uint64_t blocks = (uint64_t)num_cus * per_cu;

@@ -15,7 +15,9 @@ import torch  # noqa: E402
 from pvac_hfhe_cppbyv_amd import Engine, load_library  # noqa: E402
 
 PHASES = ["prologue", "S1 products", "S2a fold+bucket (after compact)", "S2b link", "S2c walk+closure", "S3 scan",
-          "S4 positions", "clear", "S5 writer", "stage next (prefetch wait)", "next header wait"]
+          "S4 positions", "clear", "S5 writer", "stage next (prefetch wait)", "next header wait",
+          "  S1 work (before barrier)", "  S2a reads", "  S2a fold", "  S2a zero+or", "  S2c walks (before closure)",
+          "  S4 prefetch wait", "  S4 stage"]
 
 
 def main():
@@ -30,9 +32,9 @@ def main():
         nonces = eng.fill_nonces(A, B, Cb, plan, 1)
         eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
     torch.cuda.synchronize()
-    st = np.zeros(4096 * 12, np.uint64)
+    st = np.zeros(4096 * 18, np.uint64)
     assert lib.pvac_hip_diag_fresh_stamps(st.ctypes.data_as(C.c_void_p), st.size) == 0
-    st = st.reshape(4096, 12)
+    st = st.reshape(4096, 18)
     used = st[st.sum(axis=1) > 0]
     tot = used.sum(axis=0).astype(np.float64)
     frac = tot / tot.sum()
