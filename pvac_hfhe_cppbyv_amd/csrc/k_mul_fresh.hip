@@ -192,6 +192,41 @@ __device__ __forceinline__ fresh_hdr load_hdr(argp g, uint64_t pr) {
     return h;
 }
 
+// The next pair's header is loaded by VECTOR memory (lane l < 16 of every wave holds dword l of
+// its record): its wait is vmcnt, so it never holds up an LDS wait the way a scalar load would
+// (lgkmcnt counts both, and scalar loads return out of order).
+__device__ __forceinline__ uint32_t hdr_issue(const fresh_rec* recs, uint64_t n_pairs, uint64_t q) {
+    if (q >= n_pairs) return 0;
+    return ((const uint32_t*)(recs + q))[threadIdx.x & 15u];
+}
+
+__device__ __forceinline__ fresh_hdr hdr_next(argp g, uint32_t v, uint64_t q, uint64_t n_pairs) {
+    fresh_hdr h{};
+    h.pr = kNoPair;
+    if (q >= n_pairs) return h;
+    auto rd = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane(v, k); };
+    const uint32_t w15 = rd(15);
+    if ((w15 & 0xFFFFu) == 0) return load_hdr(g, next_small(g, q + gridDim.x));   // not a fresh pair
+    h.pr = q;
+    h.aeo = ((uint64_t)rd(1) << 32) | rd(0);
+    h.beo = ((uint64_t)rd(3) << 32) | rd(2);
+    h.ceo = ((uint64_t)rd(5) << 32) | rd(4);
+    h.alo = ((uint64_t)rd(7) << 32) | rd(6);
+    h.blo = ((uint64_t)rd(9) << 32) | rd(8);
+    h.clo = ((uint64_t)rd(11) << 32) | rd(10);
+    h.nb_magic = ((uint64_t)rd(13) << 32) | rd(12);
+    const uint32_t shape = rd(14);
+    h.nA = shape & 0xFFFFu;
+    h.nB = shape >> 16;
+    h.nbk = w15 & 0xFFFFu;
+    h.LA = (w15 >> 16) & 0xFFu;
+    h.LB = w15 >> 24;
+    return h;
+}
+static_assert(offsetof(fresh_rec, nb_magic) == 48 && offsetof(fresh_rec, shape) == 56 && offsetof(fresh_rec, nbk) == 60 &&
+                  offsetof(fresh_rec, LA) == 62 && offsetof(fresh_rec, LB) == 63,
+              "hdr_next reads fresh_rec by dword");
+
 // The next pair's raw inputs ride in registers while the current pair is ordered and written:
 // thread t holds A edge t, B edge t and words 0..2 (rule, pa, pb) of input layer t. Nothing is
 // computed from them until stage_pair, so no wait is placed on the loads before then.
@@ -320,6 +355,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     unsigned long long st_acc_[kStampPhases] = {};
     unsigned long long st_last_ = __builtin_amdgcn_s_memtime();
 #endif
+    const fresh_rec* const recs = gq->recs;
+    const uint64_t n_pairs = gq->A.n;
     fresh_hdr cur = load_hdr(gq, next_small(gq, blockIdx.x));
     stage_pair(prefetch_pair(gq, cur), cur, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
     __syncthreads();
@@ -327,11 +364,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 
     while (cur.pr != kNoPair) {
         gq = launder(gq);
-        const fresh_hdr nxt = load_hdr(gq, next_small(gq, cur.pr + gridDim.x));
-#ifdef PVAC_PHASE_STAMPS
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // diag: header latency as its own phase
-        PHASE_STAMP(10);
-#endif
+        const uint64_t qn = cur.pr + gridDim.x;
+        const uint32_t hv = hdr_issue(recs, n_pairs, qn);   // decoded after S1
         const uint64_t pr = cur.pr;
         const uint32_t LA = cur.LA, LB = cur.LB, nA = cur.nA, nB = cur.nB;
         const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
@@ -350,9 +384,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 misc[MF_INVALID] = 0;
             }
             __syncthreads();
-            stage_pair(prefetch_pair(gq, nxt), nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+            const fresh_hdr nx = hdr_next(gq, hv, qn, n_pairs);
+            stage_pair(prefetch_pair(gq, nx), nx, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
             __syncthreads();
-            cur = nxt;
+            cur = nx;
             continue;
         }
 
@@ -399,11 +434,15 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             }
         }
         PHASE_STAMP_SYNC(11);
+        // next pair's header (its load has had S1 to land) and raw inputs: the pointer reads are
+        // scalar loads whose wait the barrier below pays anyway; the data loads stay in flight
+        // until stage_pair in S4
+        const fresh_hdr nxt = hdr_next(gq, hv, qn, n_pairs);
+        const fresh_pref pf = prefetch_pair(gq, nxt);
+        PHASE_STAMP(10);
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(1);
-        // next pair's raw inputs: loads in flight until stage_pair at the end of this iteration
-        const fresh_pref pf = prefetch_pair(gq, nxt);
 
         // ---- S2a: every thread owns key slots s = tid + k*BS: fold the limbs, clear them, hash
         //      the key to its libstdc++ bucket
@@ -673,16 +712,11 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         }
         PHASE_STAMP(8);
 
-        // ---- clear bucket heads and G for the next pair (the rest was cleared by its readers),
-        //      stage the next pair. The record of the pair after next is touched here (scalar-
-        //      cache warm-up); its value is consumed only after the barrier, whose wait it shares.
-        uint32_t touch = 0;
-        if (nxt.pr != kNoPair && nxt.pr + gridDim.x < gq->A.n) touch = ((recp)gq->recs)[nxt.pr + gridDim.x].nbk;
+        // ---- clear bucket heads and G for the next pair (the rest was cleared by its readers)
         for (uint32_t w = tid; w < nbk; w += BS) heads[w] = 0;
         for (uint32_t q = tid; q < (n + 3u) / 4u; q += BS) *(uint64_t*)(accb + q * 48u + 32u) = 0;   // G
         PHASE_STAMP(7);
         __syncthreads();
-        asm volatile("" ::"s"(touch));
         PHASE_STAMP(9);
         cur = nxt;
     }

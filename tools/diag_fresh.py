@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from pvac_hfhe_cppbyv_amd import Engine, load_library  # noqa: E402
 
 PHASES = ["prologue", "S1 products", "S2a fold+bucket (after compact)", "S2b link", "S2c walk+closure", "S3 scan",
-          "S4 positions", "clear", "S5 writer", "stage next (prefetch wait)", "next header wait",
+          "S4 positions", "clear", "S5 writer", "end barrier", "S1 next header + prefetch issue",
           "  S1 work (before barrier)", "  S2a reads", "  S2a fold", "  S2a zero+or", "  S2c walks (before closure)",
           "  S4 prefetch wait", "  S4 stage"]
 
