@@ -113,18 +113,21 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
 
 // ---------------------------------------------------------------- aggregation + emit
 struct fresh_layout {
-    // byte offsets into dynamic LDS
-    uint32_t acc, heads, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
+    // byte offsets into dynamic LDS; ks = slots per accumulator array
+    uint32_t acc, heads, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total, ks;
 };
 
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
-// A key slot is 48 bytes: during S1 the limbs P0 P1 P2 M0 M1 M2; from S2 on the P sum (bytes
-// 0-15), the M sum (16-31) and a zero tail (32-47) that hosts G (u16, bytes 32-39 of slot t/4)
-// and the writer map inv (u32, bytes 40-47 of slot p/2). heads: bucket chain heads (u32).
+// Accumulators: six u64 arrays X0..X5 of ks slots (structure of arrays: a slot's u64 words sit
+// 8 bytes apart across lanes, so random-slot atomics spread over 32 bank pairs and owner reads are
+// contiguous). S1: X0..X2 = P limbs, X3..X5 = M limbs. From S2 on: P sum (X0 lo, X1 hi), M sum
+// (X2, X3), X4 = G (u16 per product time), X5 = the writer map inv (u32 per emit position), both
+// zero outside their use. heads: bucket chain heads (u32).
 __host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint32_t nb, uint32_t nbk) {
     fresh_layout L;
     uint32_t o = 0;
+    L.ks = ks;
     L.acc = o;   o = align16(o + ks * 48u);           // 2 channels x 3 u64 limbs per key slot
     L.heads = o; o = align16(o + nbk * 4u);
     L.tkey = o;  o = align16(o + ks * 4u);
@@ -313,8 +316,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     argp gq = launder((uint64_t)gp);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     unsigned long long* acc = (unsigned long long*)(lds + Ls.acc);
-    ulonglong2* ksu = (ulonglong2*)(lds + Ls.acc);        // 16-byte units: slot s = units 3s .. 3s+2
-    uint8_t* accb = lds + Ls.acc;
+    const uint32_t KSM = Ls.ks;                           // accumulator array stride (slots)
+    unsigned long long* X4 = acc + 4u * KSM;
+    unsigned long long* X5 = acc + 5u * KSM;
     uint32_t* heads = (uint32_t*)(lds + Ls.heads);
     uint32_t* tkey = (uint32_t*)(lds + Ls.tkey);
     ulonglong2* a_w = (ulonglong2*)(lds + Ls.a_w);
@@ -372,8 +376,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         const uint32_t base = LA + LB, Lc = base + LP;
         const uint32_t nbk = cur.nbk;
         // G[t] and inv[p] in the slot tails (see fresh_lds)
-        auto G_at = [&](uint32_t t) { return (uint16_t*)(accb + (t >> 2) * 48u + 32u + (t & 3u) * 2u); };
-        auto inv_at = [&](uint32_t q) { return (uint32_t*)(accb + (q >> 1) * 48u + 40u + (q & 1u) * 4u); };
+        auto G_at = [&](uint32_t t) { return (uint16_t*)X4 + t; };
+        auto inv_at = [&](uint32_t q) { return (uint32_t*)X5 + q; };
 
         if (misc[MF_INVALID]) {   // invalid references: reject the pair (reference behaviour is UB)
             __syncthreads();
@@ -423,10 +427,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                             uint64_t x0, x1, l0, l1, l2;
                             fp_mul_fold1(fp{x[u].x, x[u].y}, yb, x0, x1);
                             fp_split3_128(x0, x1, l0, l1, l2);
-                            unsigned long long* q = acc + (size_t)(s * 2 + chn) * 3;
-                            atomicAdd(q + 0, (unsigned long long)l0);
-                            atomicAdd(q + 1, (unsigned long long)l1);
-                            atomicAdd(q + 2, (unsigned long long)l2);
+                            unsigned long long* q = acc + (size_t)(3u * chn) * KSM + s;
+                            atomicAdd(q, (unsigned long long)l0);
+                            atomicAdd(q + KSM, (unsigned long long)l1);
+                            atomicAdd(q + 2u * KSM, (unsigned long long)l2);
                             atomicMin(&tkey[s], i * nB + j);
                         }
                     }
@@ -460,7 +464,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         uint64_t myor = 0;
         // all reads first (the stores below would otherwise pin every later read behind them: same
         // LDS array), then the arithmetic, then the exchanges and in-place stores
-        ulonglong2 lim[KI][3];
+        uint64_t lim[KI][6];
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
@@ -469,8 +473,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
-            const ulonglong2* q = ksu + (size_t)min(s, KS - 1u) * 3;
-            lim[k][0] = q[0]; lim[k][1] = q[1]; lim[k][2] = q[2];
+            const unsigned long long* q = acc + min(s, KS - 1u);
+#pragma unroll
+            for (int c = 0; c < 6; ++c) lim[k][c] = q[c * KSM];
         }
         PHASE_STAMP_SYNC(12);
 #pragma unroll
@@ -480,8 +485,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             sumP[k] = fp{0, 0};
             sumM[k] = fp{0, 0};
             if (kt[k] != kTInf) {
-                sumP[k] = fp_fold3_lazy(lim[k][0].x, lim[k][0].y, lim[k][1].x);
-                sumM[k] = fp_fold3_lazy(lim[k][1].y, lim[k][2].x, lim[k][2].y);
+                sumP[k] = fp_fold3_lazy(lim[k][0], lim[k][1], lim[k][2]);
+                sumM[k] = fp_fold3_lazy(lim[k][3], lim[k][4], lim[k][5]);
                 eb[k] = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
                 if (eb[k]) myor |= 1ull << SLOT_LP(k);
             }
@@ -497,10 +502,10 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         for (int k = 0; k < KI; ++k) {
             const uint32_t s = tid + (uint32_t)k * BS;
             if (kt[k] != kTInf) {
-                ulonglong2* q = ksu + (size_t)s * 3;
-                q[0] = make_ulonglong2(sumP[k].lo, sumP[k].hi);
-                q[1] = make_ulonglong2(sumM[k].lo, sumM[k].hi);
-                q[2] = make_ulonglong2(0, 0);
+                unsigned long long* q = acc + s;
+                q[0] = sumP[k].lo; q[KSM] = sumP[k].hi;
+                q[2u * KSM] = sumM[k].lo; q[3u * KSM] = sumM[k].hi;
+                q[4u * KSM] = 0; q[5u * KSM] = 0;
             }
         }
         myor = wave_or_u64(myor);
@@ -648,7 +653,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                     const uint32_t lid = ident ? base + SLOT_LP(k) : remap[base + SLOT_LP(k)];
                     uint32_t* sp = gq->salt_pos;
                     if (eb[k] & 1u) {
-                        const ulonglong2 w = ksu[3 * s];
+                        const ulonglong2 w = make_ulonglong2(acc[s], acc[KSM + s]);
                         gq->C.meta[ceo + p] = make_meta(lid, idx, 0);
                         gq->C.w_lo[ceo + p] = w.x;
                         gq->C.w_hi[ceo + p] = w.y;
@@ -656,7 +661,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                         ++p;
                     }
                     if (eb[k] & 2u) {
-                        const ulonglong2 w = ksu[3 * s + 1];
+                        const ulonglong2 w = make_ulonglong2(acc[2u * KSM + s], acc[3u * KSM + s]);
                         gq->C.meta[ceo + p] = make_meta(lid, idx, 1);
                         gq->C.w_lo[ceo + p] = w.x;
                         gq->C.w_hi[ceo + p] = w.y;
@@ -664,8 +669,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                     }
                 }
                 if (own) {
-                    ksu[3 * s] = make_ulonglong2(0, 0);
-                    ksu[3 * s + 1] = make_ulonglong2(0, 0);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[c * KSM + s] = 0;
                 }
             }
         }
@@ -701,9 +706,11 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 uint32_t* ip = inv_at(p);
                 const uint32_t e = *ip;
                 const uint32_t s = e & 0x7FFu, ch = (e >> 11) & 1u, idx = (e >> 12) & 0x7FFu, lid = e >> 23;
-                const ulonglong2 w = ksu[3 * s + ch];
+                unsigned long long* q = acc + (2u * ch) * KSM + s;
+                const ulonglong2 w = make_ulonglong2(q[0], q[KSM]);
                 *ip = 0;
-                ksu[3 * s + ch] = make_ulonglong2(0, 0);
+                q[0] = 0;
+                q[KSM] = 0;
                 gq->C.meta[ceo + p] = make_meta(lid, idx, ch);
                 gq->C.w_lo[ceo + p] = w.x;
                 gq->C.w_hi[ceo + p] = w.y;
@@ -714,7 +721,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 
         // ---- clear bucket heads and G for the next pair (the rest was cleared by its readers)
         for (uint32_t w = tid; w < nbk; w += BS) heads[w] = 0;
-        for (uint32_t q = tid; q < (n + 3u) / 4u; q += BS) *(uint64_t*)(accb + q * 48u + 32u) = 0;   // G
+        for (uint32_t q = tid; q < (n + 3u) / 4u; q += BS) X4[q] = 0;   // G
         PHASE_STAMP(7);
         __syncthreads();
         PHASE_STAMP(9);
