@@ -125,7 +125,7 @@ constexpr uint32_t kFreshKeysMax = 1536;    // |A.L||B.L|B key slots
 constexpr uint32_t kFreshProdMax = 4096;    // |A.E||B.E| products
 constexpr uint32_t kFreshEdgesMax = 256;    // |A.E|, |B.E|
 constexpr uint32_t kFreshLayersMax = 64;    // |C.L| before compaction
-constexpr uint32_t kFreshThreads = 512;     // workgroup of the fresh kernel
+constexpr uint32_t kFreshThreads = 512;     // workgroup of the fresh kernel (8 waves, two per CU)
 
 // One 64-byte header record per pair (written by k_mul_layers_fresh, read by k_ct_mul_fresh with
 // a single scalar load): every per-pair field the aggregation kernel needs, in one cache line.

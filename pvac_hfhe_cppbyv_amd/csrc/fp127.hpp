@@ -158,8 +158,9 @@ __device__ __forceinline__ fp fp_fold3_lazy(uint64_t l0, uint64_t l1, uint64_t l
     const uint32_t t = x3 >> 31;
     x3 &= 0x7FFFFFFFu;
     x0 += t;
-    const bool is_p = (x3 == 0x7FFFFFFFu) & ((x0 & x1 & x2) == 0xFFFFFFFFu);
-    if (is_p) { x0 = 0; x1 = 0; x2 = 0; x3 = 0; }
+    // x == p -> 0, as a mask (no exec branch: folds of several slots interleave)
+    const uint32_t keep = ((x3 == 0x7FFFFFFFu) & ((x0 & x1 & x2) == 0xFFFFFFFFu)) ? 0u : ~0u;
+    x0 &= keep; x1 &= keep; x2 &= keep; x3 &= keep;
     return fp{join32(x0, x1), join32(x2, x3)};
 }
 

@@ -117,6 +117,10 @@ struct fresh_layout {
     uint32_t acc, heads, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total, ks;
 };
 
+// misc u32 word indices
+enum : int { MF_PART = 0 /* <= 16 scan partials */, MF_INVALID = 16, MF_TOTAL = 17, MF_IDENT = 18,
+             MF_KEEP = 20 /* u64 */, MF_WAVELP = 24 /* 16 x u64 */, MF_WORDS = 56 };
+
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
 // Accumulators: six u64 arrays X0..X5 of ks slots (structure of arrays: a slot's u64 words sit
@@ -137,14 +141,11 @@ __host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint
     L.b_inf = o; o = align16(o + nb * 4u);
     L.pm = o;    o = align16(o + kFreshLayersMax * 8u);   // parent masks of C's layers
     L.remap = o; o = align16(o + kFreshLayersMax * 4u);
-    L.misc = o;  o = align16(o + 32u * 4u);
+    L.misc = o;  o = align16(o + MF_WORDS * 4u);
     L.total = o;
     return L;
 }
 
-// misc u32 word indices
-enum : int { MF_PART = 0 /* <= 8 scan partials */, MF_INVALID = 8, MF_TOTAL = 9, MF_IDENT = 10,
-             MF_KEEP = 12 /* u64 */, MF_WAVELP = 16 /* 8 x u64 */ };
 
 // Kernel arguments read through the constant address space: scalar loads (lgkmcnt only), so an
 // argument read never waits on outstanding vector-memory loads.
@@ -275,14 +276,14 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
         if (la >= h.LA || idx >= Bm || ch > 1) misc[MF_INVALID] = 1;
         const fp w = fp_canon(f.al, f.ah);
         a_w[t] = make_ulonglong2(w.lo, w.hi);
-        a_inf[t] = idx | ((la & 0x7FFFu) << 16) | (ch << 31);
+        a_inf[t] = idx | ((la * h.LB * Bm) << 12) | (ch << 24);   // S1 adds A and B records (see there)
     }
     if (t < h.nB) {
         const uint32_t lb = meta_layer(f.bm), idx = meta_idx(f.bm), ch = meta_ch(f.bm);
         if (lb >= h.LB || idx >= Bm || ch > 1) misc[MF_INVALID] = 1;
         const fp w = fp_canon(f.bl, f.bh);
         b_w[t] = make_ulonglong2(w.lo, w.hi);
-        b_inf[t] = idx | ((lb & 0x7FFFu) << 16) | (ch << 31);
+        b_inf[t] = idx | ((lb * Bm) << 12) | (ch << 24);
     }
     const uint32_t base = h.LA + h.LB, Lc = base + h.LA * h.LB;
     uint32_t rule = f.rule;
@@ -306,10 +307,10 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
 
 template <int BS, int MINW>
 __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args* __restrict__ gp, fresh_layout Ls) {
-    constexpr int KI = kFreshKeysMax / BS;               // key slots owned per thread (3): s = tid + k*BS
+    constexpr int KI = (kFreshKeysMax + BS - 1) / BS;    // key slots owned per thread: s = tid + k*BS
     constexpr int NW = BS / 64;
-    constexpr int U = 4;                                 // products in flight per thread in S1
-    static_assert(BS == (int)kFreshThreads && BS >= (int)kFreshEdgesMax && NW <= 8, "fresh geometry");
+    constexpr int U = 4;                                 // unrolled product rounds per thread in S1
+    static_assert(BS == (int)kFreshThreads && BS >= (int)kFreshEdgesMax && NW <= 16, "fresh geometry");
     // Arguments live in a device buffer; the pointer is laundered after every barrier so the
     // compiler re-reads fields from the scalar cache on use instead of pinning ~60 SGPRs of
     // pointers for the whole loop (which spilled into VGPRs and scratch).
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     // one-time clear: accumulators and bucket heads 0, first-insert times INF
     for (uint32_t w = tid; w < (Ls.tkey - Ls.acc) / 16u; w += BS) ((uint4*)lds)[Ls.acc / 16u + w] = make_uint4(0, 0, 0, 0);
     for (uint32_t s = tid; s < gq->ks_max; s += BS) tkey[s] = kTInf;
-    if (tid < 32) misc[tid] = 0;
+    if (tid < MF_WORDS) misc[tid] = 0;
     __syncthreads();
 
 #ifdef PVAC_PHASE_STAMPS
@@ -396,43 +397,45 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         }
 
         // ---- S1: all |A.E||B.E| products into LDS limb accumulators + first-insert times.
-        //      Thread (j, g0) keeps B edge j and reads its <= U A edges g0 + u*groups up front, so
-        //      the U products and their atomics issue back to back.
+        //      Product t = i*|B.E| + j (the reference's loop order) is taken by thread t mod BS,
+        //      so every wave but the first runs ceil(n/BS) - 1 or ceil(n/BS) rounds. Staged
+        //      records: idx | layer-slot base << 12 | ch << 24, so one add of an A and a B record
+        //      gives idx_i + idx_j, the product layer's slot base and ch_i + ch_j (bit 24 = P/M).
         if (n) {
-            const uint32_t groups = BS / nB;
-            const uint32_t j = (uint32_t)tid % nB, g0 = (uint32_t)tid / nB;
-            if (g0 < groups) {
-                const uint32_t bj = b_inf[j];
-                const ulonglong2 y = b_w[j];
-                const fp yb{y.x, y.y};
-                const uint32_t lb = (bj >> 16) & 0x7FFFu, ib = bj & 0xFFFFu;
-                for (uint32_t i0 = g0; i0 < nA; i0 += U * groups) {
-                    uint32_t ai[U];
-                    ulonglong2 x[U];
+            const uint32_t mdiv = (1u << 24) / nB + 1u;   // i = ((t << 8) * mdiv) >> 32, exact for t < 2^12
+            for (uint32_t t0 = (uint32_t)tid; t0 < n; t0 += U * BS) {   // one pass for n <= U*BS
+                // all operand reads first (clamped in-range indices), so their latency is paid once
+                ulonglong2 x[U], y[U];
+                uint32_t sum[U];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t i = min(i0 + (uint32_t)u * groups, nA - 1u);
-                        ai[u] = a_inf[i];
-                        x[u] = a_w[i];
-                    }
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t t = min(t0 + (uint32_t)u * BS, n - 1u);
+                    const uint32_t i = __umulhi(t << 8, mdiv);
+                    const uint32_t j = t - i * nB;
+                    x[u] = a_w[i];
+                    y[u] = b_w[j];
+                    sum[u] = a_inf[i] + b_inf[j];
+                }
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t i = i0 + (uint32_t)u * groups;
-                        if (i < nA) {
-                            const uint32_t lp = ((ai[u] >> 16) & 0x7FFFu) * LB + lb;
-                            uint32_t r = (ai[u] & 0xFFFFu) + ib;
-                            r = r >= Bm ? r - Bm : r;
-                            const uint32_t s = lp * Bm + r;
-                            const uint32_t chn = (ai[u] ^ bj) >> 31;   // 0 = P (same sign), 1 = M
-                            uint64_t x0, x1, l0, l1, l2;
-                            fp_mul_fold1(fp{x[u].x, x[u].y}, yb, x0, x1);
-                            fp_split3_128(x0, x1, l0, l1, l2);
-                            unsigned long long* q = acc + (size_t)(3u * chn) * KSM + s;
-                            atomicAdd(q, (unsigned long long)l0);
-                            atomicAdd(q + KSM, (unsigned long long)l1);
-                            atomicAdd(q + 2u * KSM, (unsigned long long)l2);
-                            atomicMin(&tkey[s], i * nB + j);
-                        }
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t t = t0 + (uint32_t)u * BS;
+                    if (t < n) {
+                        uint32_t r = sum[u] & 0xFFFu;
+                        r = min(r, r - Bm);   // (idx_i + idx_j) mod B: r - B wraps when r < B
+                        const uint32_t s = ((sum[u] >> 12) & 0xFFFu) + r;
+                        const uint32_t chn = (sum[u] >> 24) & 1u;   // 0 = P (same sign), 1 = M
+                        uint64_t x0, x1, l0, l1, l2;
+#ifdef PVAC_EXP_NOMUL
+                        x0 = x[u].x ^ y[u].x; x1 = (x[u].y ^ y[u].y) & 0x7FFFFFFFFFFFFFFFull;
+#else
+                        fp_mul_fold1(fp{x[u].x, x[u].y}, fp{y[u].x, y[u].y}, x0, x1);
+#endif
+                        fp_split3_128(x0, x1, l0, l1, l2);
+                        unsigned long long* q = acc + chn * (3u * KSM) + s;
+                        atomicAdd(q, (unsigned long long)l0);
+                        atomicAdd(q + KSM, (unsigned long long)l1);
+                        atomicAdd(q + 2u * KSM, (unsigned long long)l2);
+                        atomicMin(&tkey[s], t);
                     }
                 }
             }
@@ -478,18 +481,25 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             for (int c = 0; c < 6; ++c) lim[k][c] = q[c * KSM];
         }
         PHASE_STAMP_SYNC(12);
+        // branch-free: empty slots hold zero limbs (slots past KS are masked by kt), so the six
+        // folds form one block the scheduler interleaves (their carry chains hide each other's
+        // VALU hazards)
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            eb[k] = 0;
             bk[k] = SLOT_BK(k);
-            sumP[k] = fp{0, 0};
-            sumM[k] = fp{0, 0};
-            if (kt[k] != kTInf) {
-                sumP[k] = fp_fold3_lazy(lim[k][0], lim[k][1], lim[k][2]);
-                sumM[k] = fp_fold3_lazy(lim[k][3], lim[k][4], lim[k][5]);
-                eb[k] = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
-                if (eb[k]) myor |= 1ull << SLOT_LP(k);
-            }
+#ifdef PVAC_EXP_NOFOLD
+            sumP[k] = fp{lim[k][0] ^ lim[k][2], lim[k][1] & 0x7FFFFFFFFFFFFFFFull};
+            sumM[k] = fp{lim[k][3] ^ lim[k][5], lim[k][4] & 0x7FFFFFFFFFFFFFFFull};
+#else
+            sumP[k] = fp_fold3_lazy(lim[k][0], lim[k][1], lim[k][2]);
+            sumM[k] = fp_fold3_lazy(lim[k][3], lim[k][4], lim[k][5]);
+#endif
+        }
+#pragma unroll
+        for (int k = 0; k < KI; ++k) {
+            const uint32_t e = (fp_nonzero(sumP[k]) ? 1u : 0u) | (fp_nonzero(sumM[k]) ? 2u : 0u);
+            eb[k] = kt[k] != kTInf ? e : 0u;
+            myor |= eb[k] ? 1ull << SLOT_LP(k) : 0ull;
         }
         PHASE_STAMP(13);
         // bucket chains: exchanges back to back, one wait for all (heads has its own region)
@@ -529,9 +539,16 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             cE[k] = 0;
             cq[k] = kt[k] != kTInf ? heads[bk[k]] : 0u;
         }
+#ifdef PVAC_EXP_NOWALK
+#pragma unroll
+        for (int k = 0; k < KI; ++k) { cE[k] = __popc(eb[k]); cq[k] = 0; }
+#endif
         // the three walks advance together: one LDS round trip per step for all of them
-        while (cq[0] | cq[1] | cq[2]) {
-            static_assert(KI == 3, "walk interleave assumes three slots per thread");
+        for (;;) {
+            uint32_t any = 0;
+#pragma unroll
+            for (int k = 0; k < KI; ++k) any |= cq[k];
+            if (!any) break;
             uint32_t v[KI];
 #pragma unroll
             for (int k = 0; k < KI; ++k) v[k] = tkey[(cq[k] ? cq[k] : 1u) - 1u];
@@ -577,36 +594,50 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         gq = launder(gq);
         PHASE_STAMP(4);
 
-        // ---- S3: exclusive SUFFIX scan of G over t in [0, n): emit offset of each bucket group
-        {
-            const uint32_t per = (n + BS - 1) / BS;
-            const uint32_t r0 = tid * per;   // reversed positions r in [r0, r0 + per), t = n-1-r
+        // ---- S3: exclusive SUFFIX scan of G over t in [0, n): emit offset of each bucket group.
+        //      One wave (the last: it holds no input records, edges <= 256) scans with no barrier:
+        //      lane l owns the aligned t-chunk [(63 - l) c, (64 - l) c) (c a multiple of 8; only
+        //      8-groups that start below n are touched, and their entries at t >= n - which lie in
+        //      G's zero tail or the zero writer map - stay zero), so lane order is suffix order. Meanwhile the
+        //      other waves stage the next pair: a_w/a_inf/b_w/b_inf were last read in S1 and pm in
+        //      the S2c closure, and the prefetched loads have had S2a and S2c to land.
+        if (wave == NW - 1) {
+            const uint32_t c8 = (n + 511u) / 512u;   // b128 chunks (8 times) per lane
+            uint4* gv = (uint4*)X4;
+            const uint32_t q0 = (63u - (uint32_t)lane) * c8;
             uint32_t local = 0;
-            for (uint32_t r = r0; r < r0 + per && r < n; ++r) local += *G_at(n - 1 - r);
-            uint32_t total;
-            uint32_t run = block_exclusive_scan<BS>(local, misc + MF_PART, total);
-            for (uint32_t r = r0; r < r0 + per && r < n; ++r) {
-                uint16_t* g = G_at(n - 1 - r);
-                const uint32_t v = *g;
-                *g = (uint16_t)run;
-                run += v;
+            const uint32_t qn = min(c8, ((n + 7u) >> 3) > q0 ? ((n + 7u) >> 3) - q0 : 0u);   // chunks with t < n
+            for (uint32_t q = 0; q < qn; ++q) {
+                const uint4 v = gv[q0 + q];
+                local += (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) +
+                         (v.z >> 16) + (v.w & 0xFFFFu) + (v.w >> 16);
             }
-            if (tid == 0) misc[MF_TOTAL] = total;
+            const uint32_t incl = wave_incl_scan_u32(local);
+            uint32_t run = incl - local;
+            for (uint32_t q = qn; q-- > 0;) {   // t descending inside the chunk
+                const uint4 v = gv[q0 + q];
+                uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                const uint32_t tq = (q0 + q) * 8u;
+#pragma unroll
+                for (int h = 3; h >= 0; --h) {
+                    const uint32_t hi = w[h] >> 16, lo = w[h] & 0xFFFFu;
+                    const uint32_t ohi = run;
+                    run += hi;
+                    const uint32_t olo = run;
+                    run += lo;
+                    const uint32_t t = tq + 2u * (uint32_t)h;
+                    w[h] = (t < n ? olo : 0u) | ((t + 1u < n ? ohi : 0u) << 16);
+                }
+                gv[q0 + q] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            if (lane == 63) misc[MF_TOTAL] = run;   // lane 63 owns t = 0: its running sum is the total
         }
+        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(5);
 
         // ---- S4: emit positions
-        // Stage the next pair first: its prefetched loads are the only vector-memory operations in
-        // flight here, so their wait does not also wait for this pair's output stores (S4/S5).
-        // a_w/a_inf/b_w/b_inf and pm are free (last read in S1 / S2c).
-#ifdef PVAC_PHASE_STAMPS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PHASE_STAMP(16);
-#endif
-        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
-        PHASE_STAMP_SYNC(17);
         const uint32_t total = misc[MF_TOTAL];
         // guard_budget (encrypt.hpp:106-111): above edge_budget the reference runs compact_edges,
         // whose output is (layer, idx, P before M) order; product edges are already unique per
@@ -711,10 +742,14 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 *ip = 0;
                 q[0] = 0;
                 q[KSM] = 0;
+#ifndef PVAC_EXP_NOWRITE
                 gq->C.meta[ceo + p] = make_meta(lid, idx, ch);
                 gq->C.w_lo[ceo + p] = w.x;
                 gq->C.w_hi[ceo + p] = w.y;
                 if (sp) sp[ceo + p] = p;   // hash order == emit order here
+#else
+                if (w.x == 0x1234567 && lid == 77) gq->C.w_hi[ceo + p] = w.y + idx;
+#endif
             }
         }
         PHASE_STAMP(8);
