@@ -186,6 +186,12 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(eng, A, B, out, n, args)
+    # the cfg-3 batch (~35 GB of inputs, outputs and nonces) is done with: release it so the side
+    # measurements (chains size their sub-batches from free HBM) run on an empty device
+    A = B = out = nonces = plan = None
+    placement.clear()
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
     if rank == 0 and not args.no_extras:
         try:
             result["extras"] = extras(eng, args, world == 1 and not args.no_cpu)
