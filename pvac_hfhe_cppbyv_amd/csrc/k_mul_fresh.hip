@@ -114,12 +114,13 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
 // ---------------------------------------------------------------- aggregation + emit
 struct fresh_layout {
     // byte offsets into dynamic LDS; ks = slots per accumulator array
-    uint32_t acc, heads, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total, ks;
+    uint32_t acc, boff, members, tkey, a_w, a_inf, b_w, b_inf, pm, remap, misc, total, ks;
 };
 
 // misc u32 word indices
 enum : int { MF_PART = 0 /* <= 16 scan partials */, MF_INVALID = 16, MF_TOTAL = 17, MF_IDENT = 18,
-             MF_KEEP = 20 /* u64 */, MF_WAVELP = 24 /* 16 x u64 */, MF_WORDS = 56 };
+             MF_KEEP = 20 /* u64 */, MF_WAVELP = 24 /* 16 x u64 */,
+             MF_HDR = 56 /* 16: next pair's header record */, MF_WORDS = 72 };
 
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
@@ -127,13 +128,15 @@ __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15
 // 8 bytes apart across lanes, so random-slot atomics spread over 32 bank pairs and owner reads are
 // contiguous). S1: X0..X2 = P limbs, X3..X5 = M limbs. From S2 on: P sum (X0 lo, X1 hi), M sum
 // (X2, X3), X4 = G (u16 per product time), X5 = the writer map inv (u32 per emit position), both
-// zero outside their use. heads: bucket chain heads (u32).
+// zero outside their use. boff / members: the slots of every libstdc++ bucket as a CSR (bucket
+// offsets u32, slot ids u16), rebuilt when the bucket count changes (see k_ct_mul_fresh).
 __host__ __device__ inline fresh_layout fresh_lds(uint32_t ks, uint32_t na, uint32_t nb, uint32_t nbk) {
     fresh_layout L;
     uint32_t o = 0;
     L.ks = ks;
     L.acc = o;   o = align16(o + ks * 48u);           // 2 channels x 3 u64 limbs per key slot
-    L.heads = o; o = align16(o + nbk * 4u);
+    L.boff = o;  o = align16(o + nbk * 4u);
+    L.members = o; o = align16(o + ks * 2u);
     L.tkey = o;  o = align16(o + ks * 4u);
     L.a_w = o;   o = align16(o + na * 16u);
     L.a_inf = o; o = align16(o + na * 4u);
@@ -240,26 +243,33 @@ struct fresh_pref {
 };
 
 __device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h) {
-    // branch-free: every lane loads a clamped (valid) index, so no divergent block ends in a
-    // wait; lanes past the counts simply ignore what they loaded
-    fresh_pref f{};
+    // branch-free and unconditional: every lane loads a valid address (a clamped index, or the
+    // argument block itself when there is no pair / no edge), so the waitcnt pass never has to
+    // drain earlier loads (or the previous pair's output stores) before issuing these; lanes past
+    // the counts ignore what they loaded
     const uint32_t t = threadIdx.x;
-    if (h.pr == kNoPair) return f;
-    if (h.nA) {
-        const uint64_t e = h.aeo + min(t, h.nA - 1);
-        f.am = g->A.meta[e]; f.al = g->A.w_lo[e]; f.ah = g->A.w_hi[e];
-    }
-    if (h.nB) {
-        const uint64_t e = h.beo + min(t, h.nB - 1);
-        f.bm = g->B.meta[e]; f.bl = g->B.w_lo[e]; f.bh = g->B.w_hi[e];
-    }
+    const bool live = h.pr != kNoPair;
+    using gp64 = const __attribute__((address_space(1))) uint64_t*;   // global: never a flat load
+    using gpl = const __attribute__((address_space(1))) uint32_t*;
+    const gp64 dummy = (gp64)(uint64_t)g;
+    const bool okA = live && h.nA, okB = live && h.nB;
+    const uint64_t ea = okA ? h.aeo + min(t, h.nA - 1u) : 0ull;
+    const uint64_t eb = okB ? h.beo + min(t, h.nB - 1u) : 0ull;
+    const gp64 am = okA ? (gp64)g->A.meta : dummy;
+    const gp64 al = okA ? (gp64)g->A.w_lo : dummy;
+    const gp64 ah = okA ? (gp64)g->A.w_hi : dummy;
+    const gp64 bm = okB ? (gp64)g->B.meta : dummy;
+    const gp64 bl = okB ? (gp64)g->B.w_lo : dummy;
+    const gp64 bh = okB ? (gp64)g->B.w_hi : dummy;
     const uint32_t nl = h.LA + h.LB;
-    if (nl) {
-        const uint32_t l = min(t, nl - 1);
-        const pvac_layer* rec = l < h.LA ? g->A.layers + h.alo + l : g->B.layers + h.blo + (l - h.LA);
-        const uint3 w3 = *(const uint3*)rec;
-        f.rule = w3.x; f.pa = w3.y; f.pb = w3.z;
-    }
+    const uint32_t l = min(t, nl - 1u);
+    const gpl rec = !(live && nl) ? (gpl)dummy
+                    : l < h.LA    ? (gpl)(g->A.layers + h.alo + l)
+                                  : (gpl)(g->B.layers + h.blo + (l - h.LA));
+    fresh_pref f;
+    f.am = am[ea]; f.al = al[ea]; f.ah = ah[ea];
+    f.bm = bm[eb]; f.bl = bl[eb]; f.bh = bh[eb];
+    f.rule = rec[0]; f.pa = rec[1]; f.pb = rec[2];
     return f;
 }
 
@@ -320,7 +330,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     const uint32_t KSM = Ls.ks;                           // accumulator array stride (slots)
     unsigned long long* X4 = acc + 4u * KSM;
     unsigned long long* X5 = acc + 5u * KSM;
-    uint32_t* heads = (uint32_t*)(lds + Ls.heads);
+    uint32_t* boff = (uint32_t*)(lds + Ls.boff);
+    uint16_t* members = (uint16_t*)(lds + Ls.members);
     uint32_t* tkey = (uint32_t*)(lds + Ls.tkey);
     ulonglong2* a_w = (ulonglong2*)(lds + Ls.a_w);
     uint32_t* a_inf = (uint32_t*)(lds + Ls.a_inf);
@@ -346,11 +357,17 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         const uint32_t lp = s / Bm;
         sinfo[k] = ((s - lp * Bm) << 15) | (min(lp, 63u) << 26);
     }
+    // The other slots of each owned slot's bucket (a static property of the bucket count and B):
+    // up to 4 cached as packed u16 pairs; gcnt = their number | CSR start << 16 (more than 4 are
+    // read from `members`).
+    uint32_t gmem[KI][2], gcnt[KI];
+#pragma unroll
+    for (int k = 0; k < KI; ++k) { gmem[k][0] = gmem[k][1] = 0; gcnt[k] = 0; }
 #define SLOT_LP(k) (sinfo[k] >> 26)
 #define SLOT_R(k) ((sinfo[k] >> 15) & 0x7FFu)
 #define SLOT_BK(k) (sinfo[k] & 0x7FFFu)
 
-    // one-time clear: accumulators and bucket heads 0, first-insert times INF
+    // one-time clear: accumulators 0, first-insert times INF
     for (uint32_t w = tid; w < (Ls.tkey - Ls.acc) / 16u; w += BS) ((uint4*)lds)[Ls.acc / 16u + w] = make_uint4(0, 0, 0, 0);
     for (uint32_t s = tid; s < gq->ks_max; s += BS) tkey[s] = kTInf;
     if (tid < MF_WORDS) misc[tid] = 0;
@@ -370,7 +387,13 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
     while (cur.pr != kNoPair) {
         gq = launder(gq);
         const uint64_t qn = cur.pr + gridDim.x;
-        const uint32_t hv = hdr_issue(recs, n_pairs, qn);   // decoded after S1
+        // The last wave is the control wave: it issues no global stores (it skips the S5 writer),
+        // so waiting for its header load never waits for output stores (vmcnt counts both, in
+        // order). It loads the next pair's record now and relays it through LDS after S1.
+        const uint32_t hv = wave == NW - 1 ? hdr_issue(recs, n_pairs, qn) : 0u;
+        auto hdr_publish = [&]() {
+            if (wave == NW - 1 && lane < 16) misc[MF_HDR + lane] = hv;
+        };
         const uint64_t pr = cur.pr;
         const uint32_t LA = cur.LA, LB = cur.LB, nA = cur.nA, nB = cur.nB;
         const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
@@ -388,12 +411,74 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 gq->C.e_cnt[pr] = 0;
                 misc[MF_INVALID] = 0;
             }
+            hdr_publish();
             __syncthreads();
-            const fresh_hdr nx = hdr_next(gq, hv, qn, n_pairs);
+            const fresh_hdr nx = hdr_next(gq, misc[MF_HDR + (lane & 15)], qn, n_pairs);
             stage_pair(prefetch_pair(gq, nx), nx, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
             __syncthreads();
             cur = nx;
             continue;
+        }
+
+        // ---- bucket groups: on a new reserve() size (workgroup-uniform), hash every slot
+        //      s < ks_max to its libstdc++ bucket and group the slots by bucket (counting sort in
+        //      LDS). Each thread caches the other slots of its own slots' buckets, so S2c reads their
+        //      keys directly instead of discovering them through per-pair bucket chains.
+        if (nbk != nbk_c) {
+            const uint32_t ksa = gq->ks_max;
+            const fastmod64 fm{nbk, cur.nb_magic};
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t b = (uint32_t)fmod64((((uint64_t)SLOT_LP(k) << 32) | SLOT_R(k)) * kGolden, fm);
+                sinfo[k] = (sinfo[k] & ~0x7FFFu) | b;   // std::hash -> bucket
+            }
+            for (uint32_t w = tid; w < nbk; w += BS) boff[w] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KI; ++k)
+                if (tid + (uint32_t)k * BS < ksa) atomicAdd(&boff[SLOT_BK(k)], 1u);
+            __syncthreads();
+            {   // exclusive scan of the bucket sizes in place
+                const uint32_t per = (nbk + BS - 1) / BS, b0 = tid * per;
+                uint32_t local = 0;
+                for (uint32_t b = b0; b < b0 + per && b < nbk; ++b) local += boff[b];
+                uint32_t tot;
+                uint32_t run = block_exclusive_scan<BS>(local, misc + MF_PART, tot);
+                for (uint32_t b = b0; b < b0 + per && b < nbk; ++b) {
+                    const uint32_t v = boff[b];
+                    boff[b] = run;
+                    run += v;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                if (s < ksa) members[atomicAdd(&boff[SLOT_BK(k)], 1u)] = (uint16_t)s;
+            }
+            __syncthreads();   // boff[b] is now the END of bucket b's slots
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                const uint32_t b = SLOT_BK(k);
+                uint32_t g0 = 0, g1 = 0, c = 0, start = 0;
+                if (s < ksa) {
+                    const uint32_t end = boff[b];
+                    start = b ? boff[b - 1] : 0u;
+                    for (uint32_t q = start; q < end; ++q) {
+                        const uint32_t m = members[q];
+                        if (m == s) continue;
+                        g0 |= c == 0 ? m : (c == 1 ? m << 16 : 0u);
+                        g1 |= c == 2 ? m : (c == 3 ? m << 16 : 0u);
+                        ++c;
+                    }
+                }
+                gmem[k][0] = g0;
+                gmem[k][1] = g1;
+                gcnt[k] = c | (start << 16);
+            }
+            nbk_c = nbk;
+            __syncthreads();   // boff is rebuilt in place by the next change
         }
 
         // ---- S1: all |A.E||B.E| products into LDS limb accumulators + first-insert times.
@@ -441,29 +526,20 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             }
         }
         PHASE_STAMP_SYNC(11);
-        // next pair's header (its load has had S1 to land) and raw inputs: the pointer reads are
-        // scalar loads whose wait the barrier below pays anyway; the data loads stay in flight
-        // until stage_pair in S4
-        const fresh_hdr nxt = hdr_next(gq, hv, qn, n_pairs);
-        const fresh_pref pf = prefetch_pair(gq, nxt);
+        hdr_publish();   // its load has had S1 to land
         PHASE_STAMP(10);
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(1);
+        // next pair's header (from the control wave) and raw inputs: the data loads stay in
+        // flight until stage_pair in S3
+        const fresh_hdr nxt = hdr_next(gq, misc[MF_HDR + (lane & 15)], qn, n_pairs);
+        const fresh_pref pf = prefetch_pair(gq, nxt);
 
         // ---- S2a: every thread owns key slots s = tid + k*BS: fold the limbs, clear them, hash
         //      the key to its libstdc++ bucket
-        if (nbk != nbk_c) {   // workgroup-uniform: a new reserve() size
-            const fastmod64 fm{nbk, cur.nb_magic};
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t b = (uint32_t)fmod64((((uint64_t)SLOT_LP(k) << 32) | SLOT_R(k)) * kGolden, fm);
-                sinfo[k] = (sinfo[k] & ~0x7FFFu) | b;   // std::hash -> bucket
-            }
-            nbk_c = nbk;
-        }
         fp sumP[KI], sumM[KI];
-        uint32_t kt[KI], eb[KI], bk[KI];
+        uint32_t kt[KI], eb[KI];
         uint64_t myor = 0;
         // all reads first (the stores below would otherwise pin every later read behind them: same
         // LDS array), then the arithmetic, then the exchanges and in-place stores
@@ -486,7 +562,6 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         // VALU hazards)
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            bk[k] = SLOT_BK(k);
 #ifdef PVAC_EXP_NOFOLD
             sumP[k] = fp{lim[k][0] ^ lim[k][2], lim[k][1] & 0x7FFFFFFFFFFFFFFFull};
             sumM[k] = fp{lim[k][3] ^ lim[k][5], lim[k][4] & 0x7FFFFFFFFFFFFFFFull};
@@ -502,11 +577,6 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
             myor |= eb[k] ? 1ull << SLOT_LP(k) : 0ull;
         }
         PHASE_STAMP(13);
-        // bucket chains: exchanges back to back, one wait for all (heads has its own region)
-        uint32_t prev[KI];
-#pragma unroll
-        for (int k = 0; k < KI; ++k)
-            prev[k] = kt[k] != kTInf ? atomicExch(&heads[bk[k]], tid + (uint32_t)k * BS + 1u) : 0u;
         // key sums in place over the slot's own limbs (a zero sum is the zero unit), tail zeroed
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
@@ -520,46 +590,55 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         }
         myor = wave_or_u64(myor);
         if (lane == 0) wave_lp[wave] = myor;
-        // chain entry: time (12 bits) | next slot + 1 (11 bits) << 12 | channels present << 23
+        // key entry: first-insert time (12 bits) | channels present << 23 (empty slots keep INF)
 #pragma unroll
         for (int k = 0; k < KI; ++k)
-            if (kt[k] != kTInf) tkey[tid + (uint32_t)k * BS] = kt[k] | (prev[k] << 12) | (eb[k] << 23);
+            if (kt[k] != kTInf) tkey[tid + (uint32_t)k * BS] = kt[k] | (eb[k] << 23);
         PHASE_STAMP_SYNC(14);
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(2);
 
-        // ---- S2c: walk chains -> bucket first-insert time, rank inside the bucket, group sizes;
-        //      wave 0 then runs compact_layers (encrypt.hpp:73-104) as a bitmask closure
-        uint32_t tb[KI], within[KI], cq[KI], cE[KI];
-#pragma unroll
-        for (int k = 0; k < KI; ++k) {
-            tb[k] = kt[k];
-            within[k] = 0;
-            cE[k] = 0;
-            cq[k] = kt[k] != kTInf ? heads[bk[k]] : 0u;
-        }
-#ifdef PVAC_EXP_NOWALK
-#pragma unroll
-        for (int k = 0; k < KI; ++k) { cE[k] = __popc(eb[k]); cq[k] = 0; }
-#endif
-        // the three walks advance together: one LDS round trip per step for all of them
-        for (;;) {
-            uint32_t any = 0;
-#pragma unroll
-            for (int k = 0; k < KI; ++k) any |= cq[k];
-            if (!any) break;
-            uint32_t v[KI];
-#pragma unroll
-            for (int k = 0; k < KI; ++k) v[k] = tkey[(cq[k] ? cq[k] : 1u) - 1u];
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                if (cq[k]) {
-                    const uint32_t t2 = v[k] & 0xFFFu, e2 = __popc(v[k] >> 23);
+        // ---- S2c: bucket first-insert time, rank inside the bucket and bucket edge count from the
+        //      keys of the other slots of the bucket (one LDS round trip: their entries are read
+        //      together); wave 0 then runs compact_layers (encrypt.hpp:73-104) as a bitmask closure
+        uint32_t tb[KI], within[KI], cE[KI];
+        {
+            auto take = [&](int k, uint32_t x) {   // another slot's key entry (INF: empty slot)
+                if (x != kTInf) {
+                    const uint32_t t2 = x & 0xFFFu, e2 = __popc(x >> 23);
                     tb[k] = t2 < tb[k] ? t2 : tb[k];
                     within[k] += t2 > kt[k] ? e2 : 0u;
                     cE[k] += e2;
-                    cq[k] = (v[k] >> 12) & 0x7FFu;
+                }
+            };
+            uint32_t v[KI][4];
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                tb[k] = kt[k];
+                within[k] = 0;
+                cE[k] = __popc(eb[k]);
+                const uint32_t g = gcnt[k] & 0xFFFFu;
+                const uint32_t c = (kt[k] != kTInf && g <= 4u) ? g : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t m = (gmem[k][j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    v[k][j] = (uint32_t)j < c ? tkey[m] : kTInf;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KI; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) take(k, v[k][j]);
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {   // buckets of more than five slots: the whole group from LDS
+                const uint32_t g = gcnt[k] & 0xFFFFu;
+                if (kt[k] != kTInf && g > 4u) {
+                    const uint32_t s = tid + (uint32_t)k * BS, q0 = gcnt[k] >> 16;
+                    for (uint32_t q = q0; q <= q0 + g; ++q) {
+                        const uint32_t m = members[q];
+                        if (m != s) take(k, tkey[m]);
+                    }
                 }
             }
         }
@@ -733,7 +812,8 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         // ---- S5 (reference order): coalesced writer over emit positions; clears what it read
         if (gather) {
             uint32_t* sp = gq->salt_pos;
-            for (uint32_t p = tid; p < total; p += BS) {
+            // waves 0..NW-2 only: the control wave keeps its vector-memory queue free of stores
+            for (uint32_t p = tid; p < total && wave != NW - 1; p += BS - 64) {
                 uint32_t* ip = inv_at(p);
                 const uint32_t e = *ip;
                 const uint32_t s = e & 0x7FFu, ch = (e >> 11) & 1u, idx = (e >> 12) & 0x7FFu, lid = e >> 23;
@@ -754,8 +834,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         }
         PHASE_STAMP(8);
 
-        // ---- clear bucket heads and G for the next pair (the rest was cleared by its readers)
-        for (uint32_t w = tid; w < nbk; w += BS) heads[w] = 0;
+        // ---- clear G for the next pair (the rest was cleared by its readers)
         for (uint32_t q = tid; q < (n + 3u) / 4u; q += BS) X4[q] = 0;   // G
         PHASE_STAMP(7);
         __syncthreads();
