@@ -198,18 +198,29 @@ struct sig_args {
     uint32_t sub_blocks;
 };
 
-// per-wave LDS: sigma [m_bits/32] | bmX [n_bits/32] | bmN [m_bits/32] | cols [x_col_wt] u16
+// per-wave LDS: sigma [m_bits/32] | bmX [n_bits/32] | bmN [m_bits/32] | cols [x_col_wt] u16 |
+// midstates [32 edges][2 streams][8] u32
 // 6 blocks per CU (6 waves per SIMD): the compiler keeps the pass loop within 80 VGPRs without
 // spills instead of hoisting the whole SHA-256 message schedule (149 VGPRs, 3 waves per SIMD)
+constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compression per lane covers
+__host__ __device__ inline uint32_t sigma_wave_words(uint32_t m_bits, uint32_t n_bits, uint32_t x_col_wt) {
+    const uint32_t w = m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2;
+    return ((w + 3) & ~3u) + kMidBatch * 2 * 8;
+}
+
+// POW2: n_bits and m_bits are powers of two (default Params), so the rejection bound is
+// 2^64 - N and x mod N is a mask instead of a 64-bit software division per draw
+template <bool POW2>
 __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t slds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t sw32 = a.m_bits / 32, bx32 = a.n_bits / 32, bn32 = a.m_bits / 32;
     const uint32_t per_wave = sw32 + bx32 + bn32 + (a.x_col_wt + 1) / 2;
-    uint32_t* sig = slds + (size_t)wave * ((per_wave + 3) & ~3u);
+    uint32_t* sig = slds + (size_t)wave * sigma_wave_words(a.m_bits, a.n_bits, a.x_col_wt);
     uint32_t* bmX = sig + sw32;
     uint32_t* bmN = bmX + bx32;
     uint16_t* cols = (uint16_t*)(bmN + bn32);
+    uint32_t* mids = sig + ((per_wave + 3) & ~3u);   // [edge j][stream][8]
     for (uint32_t w = lane; w < sw32 + bx32 + bn32; w += 64) sig[w] = 0;
 
     const bool isX = lane < 32;
@@ -220,29 +231,53 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     const uint64_t words_per_sigma = a.X.sigma_words;
     const uint32_t sub = blockIdx.y * 4 + wave, nsub = a.sub_blocks * 4;
 
+    // the salt-independent words of an edge (salt last: it is the only word in both blocks)
+    auto edge_words = [&](uint64_t eo, uint64_t lo, uint64_t nl, uint64_t e, uint64_t (&words)[7]) {
+        const uint64_t m = a.X.meta[e];
+        const uint32_t lid = meta_layer(m);
+        pvac_layer L{};
+        if (lid < nl) L = a.X.layers[lo + lid];
+        const uint64_t salt = a.salt_pos ? a.salts[eo + a.salt_pos[e]] : a.salts[e];
+        words[0] = a.canon; words[1] = L.ztag; words[2] = L.nonce_lo; words[3] = L.nonce_hi;
+        words[4] = (uint64_t)meta_idx(m); words[5] = (uint64_t)meta_ch(m); words[6] = salt;
+    };
     for (uint64_t ci = blockIdx.x; ci < a.X.n; ci += gridDim.x) {
         const uint64_t eo = a.X.e_off[ci], ne = a.X.e_cnt[ci], lo = a.X.l_off[ci], nl = a.X.l_cnt[ci];
-        for (uint64_t k = sub; k < ne; k += nsub) {
+        for (uint64_t kb = sub; kb < ne; kb += (uint64_t)kMidBatch * nsub) {
+          // block-0 midstates of the wave's next kMidBatch edges: lane j computes edge j's X-stream
+          // midstate, lane 32 + j its noise-stream midstate (block 0 holds the label, the first six
+          // words and the salt's low byte(s); it does not depend on the counter)
+          {
+            const uint64_t kk = kb + (uint64_t)(lane & 31) * nsub;
+            if (kk < ne) {
+                uint64_t words[7];
+                edge_words(eo, lo, nl, eo + kk, words);
+                uint32_t b0[16];
+                if (isX) build_block<15, 7>(b0, 0, kLabX, words, 0);
+                else build_block<14, 7>(b0, 0, kLabN, words, 0);
+                sha_state ms;
+                sha_init(ms);
+                sha_compress(ms, b0);
+                uint32_t* dst = mids + ((lane & 31) * 2 + (isX ? 0 : 1)) * 8;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) dst[i] = ms.h[i];
+            }
+            __builtin_amdgcn_wave_barrier();
+          }
+          for (uint32_t jb = 0; jb < kMidBatch; ++jb) {
+            const uint64_t k = kb + (uint64_t)jb * nsub;
+            if (k >= ne) break;
             const uint64_t e = eo + k;
-            const uint64_t m = a.X.meta[e];
-            const uint32_t lid = meta_layer(m);
-            pvac_layer L{};
-            if (lid < nl) L = a.X.layers[lo + lid];
-            const uint64_t salt = a.salt_pos ? a.salts[eo + a.salt_pos[e]] : a.salts[e];
-            const uint64_t words[7] = {a.canon, L.ztag, L.nonce_lo, L.nonce_hi, (uint64_t)meta_idx(m),
-                                       (uint64_t)meta_ch(m), salt};
-            // midstates: block 0 of both messages, selected per lane group
+            uint64_t words[7];
+            edge_words(eo, lo, nl, e, words);
             uint32_t tm[16];
             sha_state mid;
             {
-                uint32_t bx[16], bn[16];
-                build_block<15, 7>(bx, 0, kLabX, words, 0);
-                build_block<14, 7>(bn, 0, kLabN, words, 0);
+                const uint32_t* src = mids + (jb * 2 + (isX ? 0 : 1)) * 8;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) tm[i] = isX ? bx[i] : bn[i];
-                sha_init(mid);
-                sha_compress(mid, tm);
+                for (int i = 0; i < 8; ++i) mid.h[i] = src[i];
                 // block 1 template (counter 0); each pass ORs its counter in below
+                uint32_t bx[16], bn[16];
                 build_block<15, 7>(bx, 1, kLabX, words, 0);
                 build_block<14, 7>(bn, 1, kLabN, words, 0);
 #pragma unroll
@@ -267,7 +302,8 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint64_t x = (uint64_t)bswap32(s.h[2 * q]) | ((uint64_t)bswap32(s.h[2 * q + 1]) << 32);
-                    val[q] = (have < K && x <= lim) ? (uint32_t)(x % Nmod) : 0xFFFFFFFFu;
+                    val[q] = (have < K && x <= lim) ? (uint32_t)(POW2 ? (x & (uint64_t)(Nmod - 1u)) : x % Nmod)
+                                                    : 0xFFFFFFFFu;
                 }
                 int rank[4];
                 select_pass2x32(val, bm, K, have, rank);
@@ -283,34 +319,70 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                 if (doneX && doneN) break;
             }
             // XOR the selected H columns: every lane takes whole columns and reads their row lists
-            // with 16-byte loads (width is a multiple of 8), flipping bits with LDS atomic XOR
+            // with 16-byte loads (width is a multiple of 8), flipping bits with LDS atomic XOR. The
+            // selection bitmaps are dead now and sit right after the sigma image, so each 16-lane
+            // group flips into its own copy of the image (group g: words sig[256 g + (w + 16 g) mod
+            // 256]; the skew puts the groups' equal word indices on different banks): lanes of
+            // different groups never contend for a word. Copy 0 already holds the noise bits.
             const uint32_t W = a.width;
+            const bool split = sw32 == 256u && bx32 + bn32 >= 768u;   // default Params: 4 copies fit
+            if (split) {
+                for (uint32_t w4 = lane; w4 < 192u; w4 += 64) ((uint4*)(sig + 256))[w4] = make_uint4(0, 0, 0, 0);
+                __builtin_amdgcn_wave_barrier();
+            }
+            const uint32_t grp = split ? (uint32_t)lane >> 4 : 0u;
+            uint32_t* img = sig + 256u * grp;
+            const uint32_t skew = 16u * grp;
+#ifdef PVAC_EXP_SIG_NOXOR
+            if (a.width == 0x7FFFFFFFu)   // timing experiment: no column expansion at all
+#endif
             for (uint32_t c = lane; c < a.x_col_wt; c += 64) {
                 const uint32_t col = cols[c];
                 const uint32_t cnt = a.counts[col];
                 const uint4* rp = (const uint4*)(a.rows + (size_t)col * W);
-                for (uint32_t k8 = 0; k8 < cnt; k8 += 8) {
-                    const uint4 v = rp[k8 >> 3];
-                    const uint32_t rr[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
-                                            v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
-                    if (k8 + 8 <= cnt) {   // full group (always, for gen_H tables)
+                // eight 16-byte row loads in flight per lane, then their 64 flips: the row lists live
+                // in L2/MALL, so one load at a time would expose ~24 load latencies per column
+                constexpr uint32_t kB = 8;
+                for (uint32_t k8 = 0; k8 < cnt; k8 += 8 * kB) {
+                    uint4 v[kB];
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) atomicXor(&sig[rr[j] >> 5], 1u << (rr[j] & 31));
-                    } else {
+                    for (uint32_t b = 0; b < kB; ++b)
+                        v[b] = k8 + 8 * b < cnt ? rp[(k8 >> 3) + b] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                    for (uint32_t b = 0; b < kB; ++b) {
+                        const uint32_t kb = k8 + 8 * b;
+                        const uint32_t rr[8] = {v[b].x & 0xFFFFu, v[b].x >> 16, v[b].y & 0xFFFFu, v[b].y >> 16,
+                                                v[b].z & 0xFFFFu, v[b].z >> 16, v[b].w & 0xFFFFu, v[b].w >> 16};
+#ifdef PVAC_EXP_SIG_NOLDSXOR
+                        // timing experiment: rows read, no LDS atomics
+                        if ((rr[0] ^ rr[3] ^ rr[7]) == 0xFFFFFFFFu) sig[0] = rr[1];
+#else
 #pragma unroll
                         for (int j = 0; j < 8; ++j)
-                            if (k8 + j < cnt) atomicXor(&sig[rr[j] >> 5], 1u << (rr[j] & 31));
+                            if (kb + j < cnt)
+                                atomicXor(&img[split ? ((rr[j] >> 5) + skew) & 255u : rr[j] >> 5], 1u << (rr[j] & 31));
+#endif
                     }
                 }
             }
-            // write 8192 bits: one 16-byte store per lane, then clear the wave's LDS
+            __builtin_amdgcn_wave_barrier();
+            // write 8192 bits: one 16-byte store per lane (the XOR of the copies), then clear the
+            // wave's LDS
             uint64_t* out = a.X.sigma + e * words_per_sigma;
             for (uint32_t w4 = lane; w4 * 4 < sw32; w4 += 64) {
-                const uint4 v = *(const uint4*)(sig + w4 * 4);
+                uint4 v = *(const uint4*)(sig + w4 * 4);
+                if (split) {
+#pragma unroll
+                    for (uint32_t g = 1; g < 4; ++g) {
+                        const uint4 u = *(const uint4*)(sig + 256u * g + ((w4 * 4 + 16u * g) & 255u));
+                        v.x ^= u.x; v.y ^= u.y; v.z ^= u.z; v.w ^= u.w;
+                    }
+                }
                 ((ulonglong2*)out)[w4] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
                                                          (uint64_t)v.z | ((uint64_t)v.w << 32));
             }
             for (uint32_t w = lane; w < sw32 + bx32 + bn32; w += 64) sig[w] = 0;
+          }
         }
     }
 }
@@ -483,15 +555,18 @@ hipError_t launch_sigma(const sigma_tables& T, const pvac_hip_params& prm, const
     a.m_bits = prm.m_bits;
     a.x_col_wt = prm.x_col_wt;
     a.err_wt = prm.err_wt;
-    const uint32_t per_wave = prm.m_bits / 32 + prm.n_bits / 32 + prm.m_bits / 32 + (prm.x_col_wt + 1) / 2;
-    const size_t lds = (size_t)4 * ((per_wave + 3) & ~3u) * 4;
+    const size_t lds = (size_t)4 * sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) * 4;
     uint64_t gx = X.n < 4096 ? X.n : 4096;
     uint64_t sub = 1;
     const uint64_t want = (uint64_t)num_cus * 8;
     if (gx < want) sub = (want + gx - 1) / gx;
     if (sub > 64) sub = 64;
     a.sub_blocks = (uint32_t)sub;
-    hipLaunchKernelGGL(k_sigma, dim3((unsigned)gx, (unsigned)sub), dim3(kSigBlock), lds, st, a);
+    const bool pow2 = (prm.n_bits & (prm.n_bits - 1)) == 0 && (prm.m_bits & (prm.m_bits - 1)) == 0;
+    if (pow2)
+        hipLaunchKernelGGL(k_sigma<true>, dim3((unsigned)gx, (unsigned)sub), dim3(kSigBlock), lds, st, a);
+    else
+        hipLaunchKernelGGL(k_sigma<false>, dim3((unsigned)gx, (unsigned)sub), dim3(kSigBlock), lds, st, a);
     return hipGetLastError();
 }
 

@@ -12,6 +12,18 @@ namespace pvhip {
 
 PVH_HD uint32_t rotr32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
 
+// a ^ b ^ c in one VALU instruction on gfx950 (v_bitop3_b32, truth table 0x96); the compiler
+// emits two v_xor_b32 for the expression. Host passes keep the plain expression.
+PVH_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 struct sha_state { uint32_t h[8]; };
 
 PVH_HD void sha_init(sha_state& s) {
@@ -42,15 +54,15 @@ PVH_HD void sha_compress(sha_state& s, const uint32_t blk[16]) {
             wi = w[i];
         } else {
             const uint32_t x15 = w[(i - 15) & 15], x2 = w[(i - 2) & 15];
-            const uint32_t s0 = rotr32(x15, 7) ^ rotr32(x15, 18) ^ (x15 >> 3);
-            const uint32_t s1 = rotr32(x2, 17) ^ rotr32(x2, 19) ^ (x2 >> 10);
+            const uint32_t s0 = xor3(rotr32(x15, 7), rotr32(x15, 18), x15 >> 3);
+            const uint32_t s1 = xor3(rotr32(x2, 17), rotr32(x2, 19), x2 >> 10);
             wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
             w[i & 15] = wi;
         }
-        const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+        const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
         const uint32_t ch = (e & f) ^ (~e & g);
         const uint32_t t1 = h + S1 + ch + kSHA_K[i] + wi;
-        const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+        const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
         const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
         const uint32_t t2 = S0 + mj;
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
