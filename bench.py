@@ -2,13 +2,15 @@
 """bench.py — headline benchmark of the MI355X pvac-hfhe engine (driver contract).
 
 Workload (BASELINE.json cfg 3): batched weights-only ct_mul over fresh-shaped Cipher pairs
-(2 BASE layers x 20 distinct (idx, ch) edges per layer, default Params B=337), 2^20 pairs per
-GPU, inputs resident in HBM. One step = plan (sizing) + exec over the whole batch. Multi-GPU:
-one process per GPU; each rank owns an independent shard (weak scaling); the only collective
-is the gather of per-rank output totals (global CSR offsets), over RCCL.
+(2 BASE layers x 20 distinct (idx, ch) edges per layer, default Params B=337), 2^20 pairs on
+one GPU, inputs resident in HBM. One step = plan (sizing) + exec over the whole batch.
+Multi-GPU (cfg 5): one process per GPU, 2^21 pairs per rank (2^24 at N=8); each rank owns an
+independent shard (weak scaling); the only collective is the gather of per-rank output totals
+(global CSR offsets), over RCCL.
 
-Also reported (side fields): cfg 2 element-wise Fp127 add/mul at 2^24, and full ct_mul WITH
-sigma (the reference's complete ct_mul) on a smaller batch, each with its CPU baseline.
+Also reported (side fields, rank 0): cfg 2 element-wise Fp127 add/mul at 2^24, full ct_mul WITH
+sigma (the reference's complete ct_mul) on a smaller batch, cfg 4 (GPU enc_value + depth-8
+chains over 2^16 inputs) and batched enc_value, each with its CPU baseline where one exists.
 """
 import argparse
 import json
@@ -29,12 +31,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU")
+    ap.add_argument("--pairs", type=int, default=None,
+                    help="pairs per GPU (default 2^20 = cfg 3 at N=1; 2^21 at N>1, so N=8 is cfg 5's 2^24 pairs)")
     ap.add_argument("--epl", type=int, default=20, help="edges per BASE layer")
     ap.add_argument("--cpu-pairs", type=int, default=1 << 17)
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--sigma-pairs", type=int, default=1 << 12)
-    ap.add_argument("--chain-inputs", type=int, default=1 << 12, help="cfg 4 chain inputs timed (per chunk run)")
+    ap.add_argument("--chain-inputs", type=int, default=1 << 16, help="cfg 4 chain inputs (enc_value outputs)")
     ap.add_argument("--chain-chunk", type=int, default=1 << 10)
     ap.add_argument("--chain-depth", type=int, default=8)
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
@@ -71,7 +74,7 @@ def main():
         print(json.dumps(enc_bench(eng, args, False)), flush=True)
         return
     from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks
-    n = args.pairs
+    n = args.pairs if args.pairs else (1 << 20 if world == 1 else 1 << 21)
     # weak scaling: rank r owns global pairs [r*n, (r+1)*n); inputs and nonces are keyed by the
     # global pair index, so the N-GPU result is the 1-GPU result of the same global batch, sharded
     first = rank * n
@@ -92,7 +95,9 @@ def main():
         placement.update(offset=off, total_edge_slots=total)
         return out, plan
 
+    out = plan = None
     for _ in range(args.warmup):
+        out = plan = None   # release the previous output first: its cached block is reused
         out, plan = step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -104,6 +109,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        out = plan = None   # (at 2^21 pairs two outputs do not fit in HBM together)
         out, plan = step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -146,8 +152,9 @@ def main():
         "dtype": "u64",
         "data": "synthetic (device splitmix64 generator, cfg-3 fresh-shaped ciphers)",
         "config": {
-            "workload": "cfg3: 2^20 fresh-shaped Cipher pairs per GPU, batched ct_mul (weights + layers + "
-                        "reference emit order; sigma in side field), default Params B=337",
+            "workload": ("cfg3" if world == 1 else "cfg5") + f": {n} fresh-shaped Cipher pairs per GPU, "
+                        "batched ct_mul (weights + layers + reference emit order; sigma in side field), "
+                        "default Params B=337",
             "pairs_per_gpu": n,
             "edges_per_layer": args.epl,
             "global_pairs": world * n,
@@ -350,12 +357,13 @@ def sigma_bench(eng, args, with_cpu):
     return full
 
 
-def enc_bench(eng, args, with_cpu):
-    """f2: batched enc_value (LPN PRF + signal/noise equations + sigma), synthetic key material
-    (random prf_k / LPN secret, powg_B = powers of a random element), draws from a device stream."""
+ENC_STRIDE = 256   # random words per enc_value (the reference draws ~170; status 1 if short)
+
+
+def _enc_keys(eng):
+    """Synthetic key material for enc_value: random prf_k / LPN secret, H from canon_tag,
+    powg_B = powers of a random element."""
     import numpy as np
-    import torch
-    dev = eng.device
     P = (1 << 127) - 1
     rng = np.random.default_rng(0xE1C)
     eng.gen_H()
@@ -367,7 +375,16 @@ def enc_bench(eng, args, with_cpu):
         pg[2 * i], pg[2 * i + 1] = x & (2**64 - 1), x >> 64
         x = x * g % P
     eng.set_powg(pg)
-    n, stride = args.enc_values, 256
+
+
+def enc_bench(eng, args, with_cpu):
+    """f2: batched enc_value (LPN PRF + signal/noise equations + sigma), synthetic key material
+    (random prf_k / LPN secret, powg_B = powers of a random element), draws from a device stream."""
+    import numpy as np
+    import torch
+    dev = eng.device
+    _enc_keys(eng)
+    n, stride = args.enc_values, ENC_STRIDE
     vals = torch.empty(n, dtype=torch.int64, device=dev)
     rnd = torch.empty(n * stride, dtype=torch.int64, device=dev)
     eng.fill_random(vals, 0xE1)
@@ -411,19 +428,33 @@ def _ref_enc_baseline():
 
 
 def chain_bench(eng, args):
-    """cfg 4 (SURVEY 8(d) restatement of test_depth): c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) to depth
-    8 over fresh-shaped x_i, in chunks; every step is plan + exec on the general path."""
+    """cfg 4 (SURVEY 8(d) restatement of test_depth): x_i = enc_value(v_i) on the GPU, c_0 = x_i,
+    c_k = ct_mul(c_{k-1}, x_i) to depth 8, over 2^16 inputs in chunks; every ct_mul step is
+    plan + exec on the general path. Reports the chain alone and enc_value + chain."""
     import torch
     dev = eng.device
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
+    _enc_keys(eng)
     step_ms = [0.0] * depth
     step_edges = [0.0] * depth
+    last_ms = []   # deepest step per chunk
     products = 0.0
+    enc_s = 0.0
+    in_edges = 0.0
+    bad = 0
+    vals = torch.empty(chunk, dtype=torch.int64, device=dev)
+    rnd = torch.empty(chunk * ENC_STRIDE, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for c0 in range(0, n, chunk):
         k = min(chunk, n - c0)
-        X = eng.gen_fresh(k, 0x5EED0004 + c0, args.epl)
+        ts = time.perf_counter()
+        eng.fill_random(vals[:k], 0x5EED0004 + c0)
+        eng.fill_random(rnd[:k * ENC_STRIDE], 0x5EED1004 + c0)
+        X, st = eng.enc_value(vals[:k], rnd[:k * ENC_STRIDE])   # status read back = synchronised
+        enc_s += time.perf_counter() - ts
+        bad += int((st != 0).sum())
+        in_edges += float(X.e_cnt[:k].sum().item())
         cur = X
         for d in range(depth):
             ts = time.perf_counter()
@@ -433,16 +464,24 @@ def chain_bench(eng, args):
             out = eng.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
             torch.cuda.synchronize(dev)
             step_ms[d] += 1000.0 * (time.perf_counter() - ts)
+            if d == depth - 1:
+                last_ms.append(round(1000.0 * (time.perf_counter() - ts), 1))
             products += float((cur.e_cnt[:k].to(torch.float64) * X.e_cnt[:k].to(torch.float64)).sum().item())
             step_edges[d] += float(out.e_cnt[:k].sum().item())
-            del Cb, nonces
+            del Cb, nonces, plan
             cur = out
-        del cur, X
-        torch.cuda.empty_cache()
+        # no empty_cache() here: chunks reuse torch's cached blocks (the driver clears freshly
+        # mapped VRAM, so re-allocating ~10 GB per chunk stalled single steps for seconds)
+        del cur, X, out
     el = time.perf_counter() - t0
-    return {"inputs": n, "depth": depth, "chunk": chunk, "seconds": el, "chains_per_s": n / el,
-            "ct_mul_per_s": n * depth / el, "products": products, "Gfp_mul_per_s": products / el / 1e9,
-            "edges_per_input_by_step": [e / n for e in step_edges], "ms_by_step": step_ms}
+    chain_s = sum(step_ms) / 1000.0
+    return {"inputs": n, "depth": depth, "chunk": chunk, "producer": "GPU enc_value (weights-only)",
+            "seconds": el, "enc_seconds": enc_s, "chain_seconds": chain_s,
+            "chains_per_s": n / el, "ct_mul_per_s": n * depth / chain_s, "ct_mul_per_s_incl_enc": n * depth / el,
+            "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
+            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
+            "edges_per_input_by_step": [e / n for e in step_edges], "ms_by_step": step_ms,
+            "last_step_ms_by_chunk": last_ms}
 
 
 def _ref_full_baseline():

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -499,13 +501,21 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             ++j;
         }
         if (words > c->arena_words) {
+            // grow with 1/8 headroom (within the budget): batches of similar pairs differ by a few
+            // words, and a free + re-malloc of tens of GB stalls for seconds
+            const uint64_t grown = std::max<uint64_t>(words, std::min<uint64_t>(words + words / 8, budget));
             hipStreamSynchronize(c->stream);
+            const auto t0 = std::chrono::steady_clock::now();
             hipFree(c->arena);
             c->arena = nullptr;
             c->arena_words = 0;
-            hipError_t e = hipMalloc(&c->arena, words * 4);
+            hipError_t e = hipMalloc(&c->arena, grown * 4);
             if (e != hipSuccess) return hip_fail(c, e, "alloc ct_mul scratch arena");
-            c->arena_words = words;
+            c->arena_words = grown;
+            if (std::getenv("PVAC_DEBUG_ARENA"))
+                std::fprintf(stderr, "[pvac] arena -> %.2f GB (free %.1f GB, sub-batch %zu pairs): %.1f ms\n",
+                             grown * 4e-9, free_b * 1e-9, j - i,
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         }
         hipError_t e = hipMemcpyAsync(c->desc_dev + i, c->large_exec.data() + i, (j - i) * sizeof(large_desc),
                                       hipMemcpyHostToDevice, c->stream);
