@@ -148,6 +148,7 @@ struct mul_fresh_args {
     const uint32_t* nb_table;    // libstdc++ bucket count after reserve(n), n <= kFreshProdMax
     const uint64_t* nb_magic;    // fastmod64 multipliers for nb_table
     uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
+    const uint32_t* grp;         // static bucket-group tables (large_desc::g_head / g_next)
     uint64_t canon_tag;
     uint64_t edge_budget;
     uint32_t Bm;
@@ -243,7 +244,10 @@ struct large_desc {
     uint64_t capE;               // 2 min(n, S) output edge capacity
     fastmod64 nbm;               // libstdc++ bucket count after reserve(n)
     uint32_t LA, LB, nA, nB;
-    uint32_t hbits, pad;         // bucket hash table capacity = 2^hbits >= 2 S
+    uint32_t hbits, pad;         // bucket hash table capacity = 2^hbits >= 2 S (dynamic chains only)
+    // static bucket groups (bucket_count >= 2 S): per-slot chain head / next of the slots sharing
+    // a libstdc++ bucket, word offsets into mul_large_args::grp (kNoGrp: dynamic chains via link)
+    uint64_t g_head, g_next;
     // zero-initialised block [o_zero, o_zero + zero_words): cnt | hkey | hhead | bmask | bcnt | used
     uint64_t o_zero, zero_words;
     uint64_t o_cnt;              // [8] neA, neB, invalid, total edges, canonical
@@ -282,10 +286,17 @@ struct mul_large_args {
     uint32_t flags;
     uint32_t pad;
     uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
+    const uint32_t* grp;         // static bucket-group tables (large_desc::g_head / g_next)
     // launch sizing (maxima over the nl descriptors)
     uint64_t max_S, max_zero, max_tasks, max_capE, max_lay;
 };
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
+constexpr uint64_t kNoGrp = ~0ull;
+// static bucket groups of key slots [0, S) for one bucket count: head[s] = 0 when s is alone in
+// its bucket, else the first slot + 1 of the bucket's chain; next[s] = the following slot + 1
+// (0 ends). tmp_key / tmp_head: 2^hbits entries, zeroed by the caller.
+hipError_t launch_grp_build(fastmod64 nbm, uint32_t Bm, uint64_t S, uint32_t hbits, uint32_t* head, uint32_t* next,
+                            unsigned long long* tmp_key, uint32_t* tmp_head, hipStream_t st);
 
 hipError_t launch_ct_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, int negate_b,
                          uint32_t max_layers, const uint8_t* pair_class, hipStream_t st);

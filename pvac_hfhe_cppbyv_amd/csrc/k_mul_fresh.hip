@@ -47,6 +47,9 @@ __device__ unsigned long long g_fresh_stamps[4096 * kStampPhases];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
         PHASE_STAMP(ph);                                       \
     } while (0)
+#elif defined(PVAC_ASM_MARKS)   // static instruction counts per phase (tools/asm_phases.py)
+#define PHASE_STAMP(ph) asm volatile("; PVAC_MARK " #ph ::: "memory")
+#define PHASE_STAMP_SYNC(ph) PHASE_STAMP(ph)
 #else
 #define PHASE_STAMP(ph) \
     do {                \

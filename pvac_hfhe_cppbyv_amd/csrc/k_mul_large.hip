@@ -398,6 +398,7 @@ __global__ __launch_bounds__(kLB) void k_large_link(mul_large_args g) {
     unsigned long long* hkey = (unsigned long long*)w64(S, d.o_hkey);
     uint32_t* hhead = S + d.o_hhead;
     const uint64_t hmask = (1ull << d.hbits) - 1;
+    if (d.g_head != kNoGrp) return;   // static bucket groups: no per-pair chains
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
         if (tkey[s] == kInf) continue;
         const uint64_t lp = s / Bm, r = s - lp * Bm;
@@ -427,18 +428,40 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     uint32_t* etot = S + d.o_etot;
     unsigned long long* bmask = (unsigned long long*)w64(S, d.o_bmask);
     uint32_t* bcnt = S + d.o_bcnt;
+    const bool stat = d.g_head != kNoGrp;
+    const uint32_t* ghead = g.grp + (stat ? d.g_head : 0);
+    const uint32_t* gnext = g.grp + (stat ? d.g_next : 0);
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
         const uint32_t t = tkey[s];
         if (t == kInf) continue;
-        uint32_t q = hhead[info[s] >> 2], tmin = t, w = 0, E = 0;
-        while (q) {
-            const uint32_t s2 = q - 1;
-            const uint32_t t2 = tkey[s2];
-            const uint32_t e2 = __popc(info[s2] & 3u);
-            tmin = t2 < tmin ? t2 : tmin;
-            w += t2 > t ? e2 : 0u;
-            E += e2;
-            q = nxt[s2];
+        uint32_t tmin = t, w = 0, E = 0;
+        if (stat) {
+            // the bucket's slots are a static property of (bucket count, B): walk them, keep the
+            // ones present in this pair (a lone slot, the common case, reads nothing more)
+            uint32_t q = ghead[s];
+            if (!q) E = __popc(info[s] & 3u);
+            while (q) {
+                const uint32_t s2 = q - 1;
+                q = gnext[s2];
+                if (s2 >= d.S) continue;
+                const uint32_t t2 = tkey[s2];
+                if (t2 == kInf) continue;
+                const uint32_t e2 = __popc(info[s2] & 3u);
+                tmin = t2 < tmin ? t2 : tmin;
+                w += t2 > t ? e2 : 0u;
+                E += e2;
+            }
+        } else {
+            uint32_t q = hhead[info[s] >> 2];
+            while (q) {
+                const uint32_t s2 = q - 1;
+                const uint32_t t2 = tkey[s2];
+                const uint32_t e2 = __popc(info[s2] & 3u);
+                tmin = t2 < tmin ? t2 : tmin;
+                w += t2 > t ? e2 : 0u;
+                E += e2;
+                q = nxt[s2];
+            }
         }
         tb[s] = tmin;
         within[s] = w;
@@ -569,6 +592,33 @@ __global__ __launch_bounds__(kLB) void k_large_write(mul_large_args g) {
     }
 }
 
+// ---------------------------------------------------------------- static bucket groups
+__global__ __launch_bounds__(kLB) void k_grp_insert(fastmod64 nbm, uint32_t Bm, uint64_t S, uint32_t hbits,
+                                                    uint32_t* head, uint32_t* next, unsigned long long* tkeyb,
+                                                    uint32_t* thead) {
+    const uint64_t hmask = (1ull << hbits) - 1;
+    for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < S; s += (uint64_t)gridDim.x * kLB) {
+        const uint64_t lp = s / Bm, r = s - lp * Bm;
+        const uint64_t b = fmod64(((lp << 32) | r) * kGolden, nbm);   // std::hash -> bucket
+        uint64_t h = ((b + 1) * kGolden) >> (64 - hbits);
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&tkeyb[h], 0ull, (unsigned long long)(b + 1));
+            if (prev == 0ull || prev == b + 1) break;
+            h = (h + 1) & hmask;
+        }
+        next[s] = atomicExch(&thead[h], (uint32_t)(s + 1));
+        head[s] = (uint32_t)h;
+    }
+}
+
+__global__ __launch_bounds__(kLB) void k_grp_finish(uint64_t S, uint32_t* head, const uint32_t* next,
+                                                    const uint32_t* thead) {
+    for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < S; s += (uint64_t)gridDim.x * kLB) {
+        const uint32_t h0 = thead[head[s]];
+        head[s] = (h0 == (uint32_t)(s + 1) && next[s] == 0u) ? 0u : h0;   // 0: alone in its bucket
+    }
+}
+
 unsigned grid_x(uint64_t work, uint64_t per_block, uint64_t cap) {
     uint64_t b = (work + per_block - 1) / per_block;
     if (b < 1) b = 1;
@@ -577,6 +627,16 @@ unsigned grid_x(uint64_t work, uint64_t per_block, uint64_t cap) {
 }
 
 }  // namespace
+
+hipError_t launch_grp_build(fastmod64 nbm, uint32_t Bm, uint64_t S, uint32_t hbits, uint32_t* head, uint32_t* next,
+                            unsigned long long* tmp_key, uint32_t* tmp_head, hipStream_t st) {
+    if (!S) return hipSuccess;
+    const unsigned gs = grid_x(S, kLB * 2, 4096);
+    hipLaunchKernelGGL(k_grp_insert, dim3(gs), dim3(kLB), 0, st, nbm, Bm, S, hbits, head, next, tmp_key, tmp_head);
+    hipLaunchKernelGGL(k_grp_finish, dim3(gs), dim3(kLB), 0, st, S, head, (const uint32_t*)next,
+                       (const uint32_t*)tmp_head);
+    return hipGetLastError();
+}
 
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     if (!a.nl) return hipSuccess;

@@ -82,6 +82,11 @@ struct pvac_hip_ctx {
     size_t desc_cap = 0;
     uint32_t* arena = nullptr;
     size_t arena_words = 0;
+    // static bucket-group tables of the last plan (one per distinct bucket count) + build scratch
+    uint32_t* grp = nullptr;
+    size_t grp_cap = 0;
+    uint32_t* grp_tmp = nullptr;
+    size_t grp_tmp_cap = 0;
     uint32_t* salt_pos = nullptr;
     size_t salt_cap = 0;
     mul_fresh_args* fresh_args = nullptr;   // device copy of the fresh kernel's arguments
@@ -210,7 +215,7 @@ uint32_t ceil_log2(uint64_t x) {
 // executor rebases them into the arena. 64-bit arrays on even words, 16-byte arrays on
 // multiples of four.
 int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uint64_t nA, uint64_t nB, uint32_t Bm,
-                     std::string& why) {
+                     std::string& why, bool static_grp = false) {
     d = large_desc{};
     d.pair = pair;
     d.n = nA * nB;
@@ -235,7 +240,8 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.capE = 2 * keys;
     d.nbm = make_fastmod64(bucket_count_after_reserve(d.n));
     d.hbits = std::max<uint32_t>(1, ceil_log2(2 * std::max<uint64_t>(keys, 1)));
-    const uint64_t hcap = 1ull << d.hbits;
+    d.g_head = d.g_next = kNoGrp;
+    const uint64_t hcap = static_grp ? 0 : 1ull << d.hbits;   // static groups: no bucket table / chains
     uint64_t o = 0;
     auto even = [&]() { o = (o + 1) & ~1ull; };
     auto quad = [&]() { o = (o + 3) & ~3ull; };
@@ -257,7 +263,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.o_info = o; o += d.S;
     quad();
     d.o_sums = o; o += 8 * d.S;
-    d.o_nxt = o; o += d.S;
+    d.o_nxt = o; o += static_grp ? 0 : d.S;
     d.o_tb = o; o += d.S;
     d.o_within = o; o += d.S;
     d.o_etot = o; o += d.S;
@@ -331,6 +337,8 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->large_info);
     hipFree(c->desc_dev);
     hipFree(c->arena);
+    hipFree(c->grp);
+    hipFree(c->grp_tmp);
     hipFree(c->salt_pos);
     hipFree(c->fresh_args);
     hipFree(c->merge_scratch);
@@ -409,6 +417,63 @@ int pvac_hip_fp_binop(pvac_hip_ctx* c, int op, const uint64_t* a_lo, const uint6
 }
 
 // ---------------------------------------------------------------- ct_mul
+namespace {
+
+// Pairs whose bucket count is at least twice their key-slot space (dense chain steps: reserve(|A.E||B.E|)
+// buckets for |A.L||B.L|B slots) share their bucket groups with every pair of the same bucket count:
+// the group of a slot depends only on (slot, B, bucket count). One static table per distinct bucket
+// count replaces the per-pair bucket table + chains (k_large_link) and its zeroing; rank walks the
+// static group and keeps the slots present in the pair (almost every slot is alone in its bucket).
+int plan_static_groups(pvac_hip_ctx* c) {
+    constexpr size_t kMaxCfg = 64;
+    constexpr uint64_t kMaxWords = 1ull << 28;   // <= 1 GiB of tables
+    std::map<uint64_t, uint64_t> cfg;             // bucket count -> max S
+    for (const large_desc& d : c->large_host)
+        if (d.nbm.d >= 2 * d.S && d.S) {
+            uint64_t& m = cfg[d.nbm.d];
+            m = std::max(m, d.S);
+        }
+    uint64_t words = 0, tmp_max = 0;
+    for (auto& kv : cfg) {
+        words += 2 * kv.second;
+        tmp_max = std::max<uint64_t>(tmp_max, 1ull << std::max<uint32_t>(1, ceil_log2(2 * kv.second)));
+    }
+    if (cfg.empty() || cfg.size() > kMaxCfg || words > kMaxWords) return PVAC_OK;   // dynamic chains
+    int rc = ensure_dev(c, c->grp, c->grp_cap, words, "alloc bucket-group tables");
+    if (!rc) rc = ensure_dev(c, c->grp_tmp, c->grp_tmp_cap, 3 * tmp_max, "alloc bucket-group scratch");
+    if (rc) return rc;
+    std::map<uint64_t, uint64_t> off;   // bucket count -> head offset (next = head + S_max)
+    uint64_t o = 0;
+    for (auto& kv : cfg) {
+        const uint64_t Sm = kv.second;
+        const uint32_t hb = std::max<uint32_t>(1, ceil_log2(2 * Sm));
+        const uint64_t hcap = 1ull << hb;
+        unsigned long long* tk = (unsigned long long*)c->grp_tmp;   // [hcap] u64 keys, then [hcap] u32 heads
+        uint32_t* th = c->grp_tmp + 2 * hcap;
+        hipError_t e = hipMemsetAsync(c->grp_tmp, 0, 3 * hcap * 4, c->stream);
+        if (e == hipSuccess)
+            e = launch_grp_build(make_fastmod64(kv.first), c->prm.B, Sm, hb, c->grp + o, c->grp + o + Sm, tk, th,
+                                 c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "build bucket-group tables");
+        off[kv.first] = o;
+        o += 2 * Sm;
+    }
+    for (large_desc& d : c->large_host) {
+        auto it = off.find(d.nbm.d);
+        if (it == off.end() || d.nbm.d < 2 * d.S || !d.S) continue;
+        std::string why;
+        large_desc x;
+        rc = build_large_desc(x, d.pair, d.LA, d.LB, d.nA, d.nB, c->prm.B, why, true);
+        if (rc) return fail(c, rc, why);
+        x.g_head = it->second;
+        x.g_next = it->second + cfg[d.nbm.d];
+        d = x;
+    }
+    return PVAC_OK;
+}
+
+}  // namespace
+
 int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
                          pvac_hip_plan* plan) {
     if (!c || !plan || !batch_ok(A) || !batch_ok(B) || !C || !C->l_off || !C->e_off)
@@ -466,6 +531,8 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
         // deterministic launch order (the plan kernel appends in arrival order)
         std::sort(c->large_host.begin(), c->large_host.end(),
                   [](const large_desc& x, const large_desc& y) { return x.pair < y.pair; });
+        rc = plan_static_groups(c);
+        if (rc) return rc;
     }
     return PVAC_OK;
 }
@@ -532,6 +599,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.edge_budget = c->prm.edge_budget;
         a.flags = flags;
         a.salt_pos = salt_pos;
+        a.grp = c->grp;
         a.max_S = mS; a.max_zero = mZ; a.max_tasks = mT; a.max_capE = mE; a.max_lay = mL;
         e = launch_ct_mul_large(a, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "ct_mul_large");
