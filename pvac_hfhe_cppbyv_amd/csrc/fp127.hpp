@@ -220,6 +220,40 @@ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
     return fp{join32(y0, y1), join32(y2, y3)};
 }
 
+// ---- lazy register accumulators ---------------------------------------------------------
+// Sum of lazy products x < 2^128 (fp_mul_fold1 of canonical operands) as 128 bits + a carry
+// count: up to 2^32 addends, 5 VALU ops per add. acc_fold returns the canonical residue, equal to
+// the reference's fp_add chain of canonical fp_mul results (exact sum mod p).
+struct acc128c { uint32_t w[4]; uint32_t c; };
+__device__ __forceinline__ void acc_zero(acc128c& a) { a.w[0] = a.w[1] = a.w[2] = a.w[3] = 0; a.c = 0; }
+__device__ __forceinline__ void acc_add(acc128c& a, uint64_t x0, uint64_t x1) {
+    uint32_t c;
+    a.w[0] = addc(a.w[0], lo32(x0), 0u, c);
+    a.w[1] = addc(a.w[1], hi32(x0), c, c);
+    a.w[2] = addc(a.w[2], lo32(x1), c, c);
+    a.w[3] = addc(a.w[3], hi32(x1), c, c);
+    a.c += c;
+}
+__device__ __forceinline__ fp acc_fold(const acc128c& a) {
+    // V = c 2^128 + W, 2^128 == 2 (mod p): x = (W mod 2^127) + (W >> 127) + 2c < 2^127 + 2^34
+    uint32_t c;
+    const uint32_t add = (a.w[3] >> 31) + 2u * a.c;   // < 2^34 only when c >= 2^31: kept below
+    uint32_t x0 = addc(a.w[0], add, 0u, c);
+    uint32_t x1 = addc(a.w[1], 0u, c, c);
+    uint32_t x2 = addc(a.w[2], 0u, c, c);
+    uint32_t x3 = (a.w[3] & 0x7FFFFFFFu) + c;
+    // x < 2^127 + 2^32: one conditional subtract of p = (x - 2^127) + 1, then x == p -> 0
+    const uint32_t t = x3 >> 31;
+    x3 &= 0x7FFFFFFFu;
+    x0 = addc(x0, t, 0u, c);
+    x1 = addc(x1, 0u, c, c);
+    x2 = addc(x2, 0u, c, c);
+    x3 += c;
+    const bool is_p = (x3 == 0x7FFFFFFFu) & ((x0 & x1 & x2) == 0xFFFFFFFFu);
+    if (is_p) { x0 = 0; x1 = 0; x2 = 0; x3 = 0; }
+    return fp{join32(x0, x1), join32(x2, x3)};
+}
+
 // field.hpp:229-273 fp_inv = a^(p-2) (fp_inv_ct's windowed ladder). The power is unique, so any
 // exact chain is bit-identical: a Mersenne addition chain x_k = a^(2^k - 1),
 // a^(p-2) = a^(2^127 - 3) = (x_125)^4 * a: 126 squarings + 11 multiplies; fp_inv(0) = 0.

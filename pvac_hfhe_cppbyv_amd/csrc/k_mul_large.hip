@@ -190,8 +190,12 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
             const uint32_t e = dids[k];
             const uint64_t m = D.meta[deo + e];
             const uint32_t sl = meta_idx(m) * 2 + meta_ch(m);
-            if (atomicCAS(&di[sl], kInf, e) != kInf) *dup = 1;
-            else dw[sl] = make_ulonglong2(D.w_lo[deo + e], D.w_hi[deo + e]);
+            if (atomicCAS(&di[sl], kInf, e) != kInf) {
+                *dup = 1;
+            } else {   // canonical operands: the lazy product below needs a, b < 2^127
+                const fp w = fp_canon(D.w_lo[deo + e], D.w_hi[deo + e]);
+                dw[sl] = make_ulonglong2(w.lo, w.hi);
+            }
         }
         __syncthreads();
         dense = *dup == 0;   // duplicate (layer, idx, ch) edges: use the scatter mode instead
@@ -199,18 +203,20 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
             const uint32_t* sids = denseA ? idsB : idsA;
             const pvac_ct_batch& Sp = denseA ? g.B : g.A;
             const uint64_t seo = denseA ? beo : aeo;
-            // lanes own output indices r (at most kLPRows per lane)
-            fp P[kLPRows], M[kLPRows];
+            // lanes own output indices r (at most kLPRows per lane); P/M sums are lazy 128-bit
+            // register accumulators (acc128c), reduced once at the end
+            acc128c P[kLPRows], M[kLPRows];
             uint32_t tmin[kLPRows];
 #pragma unroll
-            for (int u = 0; u < kLPRows; ++u) { P[u] = fp{0, 0}; M[u] = fp{0, 0}; tmin[u] = kInf; }
+            for (int u = 0; u < kLPRows; ++u) { acc_zero(P[u]); acc_zero(M[u]); tmin[u] = kInf; }
             for (uint32_t c0 = 0; c0 < ns; c0 += kChunk) {
                 const uint32_t cn = min(kChunk, ns - c0);
                 __syncthreads();
                 for (uint32_t k = tid; k < cn; k += kLP) {
                     const uint32_t e = sids[c0 + k];
                     const uint64_t m = Sp.meta[seo + e];
-                    swv[k] = make_ulonglong2(Sp.w_lo[seo + e], Sp.w_hi[seo + e]);
+                    const fp w = fp_canon(Sp.w_lo[seo + e], Sp.w_hi[seo + e]);
+                    swv[k] = make_ulonglong2(w.lo, w.hi);
                     sinf[k] = meta_idx(m) | (meta_ch(m) << 16);
                     sidv[k] = e;
                 }
@@ -230,9 +236,10 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                             const uint32_t e = di[2 * dd + c];
                             if (e != kInf) {
                                 const ulonglong2 dv = dw[2 * dd + c];
-                                const fp pv = fp_mul(fp{dv.x, dv.y}, fp{sw.x, sw.y});
-                                if (c == sch) P[u] = fp_add(P[u], pv);
-                                else M[u] = fp_add(M[u], pv);
+                                uint64_t x0, x1;
+                                fp_mul_fold1(fp{dv.x, dv.y}, fp{sw.x, sw.y}, x0, x1);
+                                if (c == sch) acc_add(P[u], x0, x1);
+                                else acc_add(M[u], x0, x1);
                                 const uint32_t t = denseA ? e * nB + se : se * nB + e;
                                 tmin[u] = t < tmin[u] ? t : tmin[u];
                             }
@@ -247,10 +254,11 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                 const uint64_t s = slot0 + r;
                 tkey[s] = tmin[u];
                 if (tmin[u] != kInf) {
-                    const uint32_t eb = (fp_nonzero(P[u]) ? 1u : 0u) | (fp_nonzero(M[u]) ? 2u : 0u);
+                    const fp ps = acc_fold(P[u]), ms = acc_fold(M[u]);
+                    const uint32_t eb = (fp_nonzero(ps) ? 1u : 0u) | (fp_nonzero(ms) ? 2u : 0u);
                     info[s] = eb;
-                    sums[2 * s] = make_ulonglong2(P[u].lo, P[u].hi);
-                    sums[2 * s + 1] = make_ulonglong2(M[u].lo, M[u].hi);
+                    sums[2 * s] = make_ulonglong2(ps.lo, ps.hi);
+                    sums[2 * s + 1] = make_ulonglong2(ms.lo, ms.hi);
                     any |= eb != 0;
                 }
             }
