@@ -240,7 +240,7 @@ struct large_desc {
     uint64_t n;                  // |A.E| * |B.E|  (< 2^32)
     uint64_t S;                  // |A.L| |B.L| B dense key slots
     uint64_t Lc;                 // |A.L| + |B.L| + |A.L||B.L|  (layers before compaction)
-    uint64_t nblk;               // ceil(n / 64) first-insert-time blocks
+    uint64_t nblk;               // ceil(n / 16) first-insert-time blocks
     uint64_t capE;               // 2 min(n, S) output edge capacity
     fastmod64 nbm;               // libstdc++ bucket count after reserve(n)
     uint32_t LA, LB, nA, nB;
@@ -253,8 +253,10 @@ struct large_desc {
     uint64_t o_cnt;              // [8] neA, neB, invalid, total edges, canonical
     uint64_t o_hkey;             // [2^hbits] u64 bucket ids + 1
     uint64_t o_hhead;            // [2^hbits] chain heads (slot + 1)
-    uint64_t o_bmask;            // [nblk] u64 bucket-leader masks over first-insert times
-    uint64_t o_bcnt;             // [nblk + 1] emitted edges per block -> exclusive suffix offsets
+    uint64_t o_bmask;            // [nblk] u64 per 16 first-insert times: bucket-leader edge codes (2 bits
+                                 // per time: 0 none, 1/2 edges, 3 more) | block edges << 32, then the
+                                 // block's exclusive suffix offset << 32 (k_large_rank / scan / order)
+    uint64_t o_bcnt;             // (unused, empty)
     uint64_t o_used;             // [Lc] product-layer used flags -> compact_layers remap
     // 0xFF-initialised: [S] first-insert time per key slot (INF = key absent)
     uint64_t o_tkey;

@@ -434,8 +434,7 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     uint32_t* tb = S + d.o_tb;
     uint32_t* within = S + d.o_within;
     uint32_t* etot = S + d.o_etot;
-    unsigned long long* bmask = (unsigned long long*)w64(S, d.o_bmask);
-    uint32_t* bcnt = S + d.o_bcnt;
+    unsigned long long* bpack = (unsigned long long*)w64(S, d.o_bmask);
     const bool stat = d.g_head != kNoGrp;
     const uint32_t* ghead = g.grp + (stat ? d.g_head : 0);
     const uint32_t* gnext = g.grp + (stat ? d.g_next : 0);
@@ -475,8 +474,12 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
         within[s] = w;
         if (tmin == t) {
             etot[s] = E;
-            atomicOr(&bmask[t >> 6], 1ull << (t & 63u));
-            if (E) atomicAdd(&bcnt[t >> 6], E);
+            // one atomic per leader: its edge code lands in 2 free bits (first-insert times are
+            // unique, so the add is an OR) and its edges in the block count
+            if (E) {
+                const uint64_t code = E < 3u ? E : 3u;
+                atomicAdd(&bpack[t >> 4], ((unsigned long long)E << 32) | (code << (2u * (t & 15u))));
+            }
         }
     }
 }
@@ -490,19 +493,31 @@ __global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
     uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
     const int tid = threadIdx.x;
-    uint32_t* bcnt = S + d.o_bcnt;
+    unsigned long long* bpack = (unsigned long long*)w64(S, d.o_bmask);
     const uint32_t nblk = (uint32_t)d.nblk;
-    uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < nblk; r0 += kLBig) {   // reversed index r -> block nblk-1-r
-        const uint32_t r = r0 + tid;
-        const uint32_t b = nblk - 1 - r;
-        const uint32_t v = r < nblk ? bcnt[b] : 0u;
+    // reversed block index r (block nblk-1-r) in rounds of 4 kLBig: thread t takes r = base + 4t .. 4t+3
+    // (adjacent threads, adjacent words: coalesced), one workgroup scan per round
+    uint32_t total = 0;
+    for (uint32_t base = 0; base < nblk; base += 4u * kLBig) {
+        const uint32_t r0 = base + 4u * (uint32_t)tid;
+        unsigned long long v[4];
+        uint32_t local = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = r0 + (uint32_t)k;
+            v[k] = r < nblk ? bpack[nblk - 1 - r] : 0ull;
+            local += (uint32_t)(v[k] >> 32);
+        }
         uint32_t tot;
-        const uint32_t ex = wg_exclusive_scan<kLBig>(v, part, tot);
-        if (r < nblk) bcnt[b] = carry + ex;
-        carry += tot;
+        uint32_t run = total + wg_exclusive_scan<kLBig>(local, part, tot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = r0 + (uint32_t)k;
+            if (r < nblk) bpack[nblk - 1 - r] = ((unsigned long long)run << 32) | (v[k] & 0xFFFFFFFFull);
+            run += (uint32_t)(v[k] >> 32);
+        }
+        total += tot;
     }
-    const uint32_t total = carry;
     const bool canonical = (g.flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > g.edge_budget;
     if (tid == 0) {
         cnt[3] = total;
@@ -514,7 +529,7 @@ __global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
     const uint32_t* tkey = S + d.o_tkey;
     const uint32_t* info = S + d.o_info;
     uint32_t* cpos = S + d.o_cpos;
-    carry = 0;
+    uint32_t carry = 0;
     for (uint64_t s0 = 0; s0 < d.S; s0 += kLBig) {
         const uint64_t s = s0 + tid;
         const uint32_t v = (s < d.S && tkey[s] != kInf) ? (uint32_t)__popc(info[s] & 3u) : 0u;
@@ -539,8 +554,7 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     const uint32_t* tb = S + d.o_tb;
     const uint32_t* within = S + d.o_within;
     const uint32_t* etot = S + d.o_etot;
-    const unsigned long long* bmask = (const unsigned long long*)w64(S, d.o_bmask);
-    const uint32_t* bcnt = S + d.o_bcnt;
+    const unsigned long long* bpack = (const unsigned long long*)w64(S, d.o_bmask);
     const uint32_t* cpos = S + d.o_cpos;
     uint32_t* order = S + d.o_order;
     uint32_t* hpos = S + d.o_hpos;
@@ -548,13 +562,20 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
         if (tkey[s] == kInf) continue;
         const uint32_t eb = info[s] & 3u;
         if (!eb) continue;
-        const uint32_t t = tb[s], blk = t >> 6, bit = t & 63u;
-        uint32_t hp = bcnt[blk] + within[s];
-        uint64_t m = bmask[blk] & ~((2ull << bit) - 1ull);   // leaders later in this block
+        const uint32_t t = tb[s], blk = t >> 4, bit = t & 15u;
+        const unsigned long long v = bpack[blk];
+        // edge codes of the leaders later in this block (2 bits per time): 1 and 2 are their edge
+        // counts; 3 (buckets of 3+ edges) is resolved from the leader's slot, found from its
+        // (i, j) = (t / |B.E|, t % |B.E|)
+        const uint64_t codes = (v & 0xFFFFFFFFull) >> (2u * bit + 2u);
+        const uint64_t esc = codes & (codes >> 1) & 0x5555555555555555ull;
+        uint32_t hp = (uint32_t)(v >> 32) + within[s] + (uint32_t)__popcll(codes & 0x5555555555555555ull) +
+                      2u * (uint32_t)__popcll(codes & 0xAAAAAAAAAAAAAAAAull) - 3u * (uint32_t)__popcll(esc);
+        uint64_t m = esc;
         while (m) {
-            const uint32_t b2 = (uint32_t)__ffsll((long long)m) - 1u;
+            const uint32_t b2 = ((uint32_t)__ffsll((long long)m) - 1u) / 2u + bit + 1u;
             m &= m - 1ull;
-            const uint32_t t2 = (blk << 6) | b2;
+            const uint32_t t2 = (blk << 4) | b2;
             const uint32_t i2 = t2 / nB, j2 = t2 - i2 * nB;
             const uint64_t ma = g.A.meta[aeo + i2], mb = g.B.meta[beo + j2];
             const uint64_t s2 = (uint64_t)(meta_layer(ma) * LB + meta_layer(mb)) * Bm +

@@ -235,7 +235,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
         return PVAC_ENOSYS;
     }
     d.LA = (uint32_t)LA; d.LB = (uint32_t)LB; d.nA = (uint32_t)nA; d.nB = (uint32_t)nB;
-    d.nblk = (d.n + 63) / 64;
+    d.nblk = (d.n + 15) / 16;
     const uint64_t keys = std::min(d.n, d.S);
     d.capE = 2 * keys;
     d.nbm = make_fastmod64(bucket_count_after_reserve(d.n));
@@ -252,7 +252,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.o_hhead = o; o += hcap;
     even();
     d.o_bmask = o; o += 2 * d.nblk;
-    d.o_bcnt = o; o += d.nblk + 1;
+    d.o_bcnt = o;
     d.o_used = o; o += d.Lc;
     d.zero_words = o - d.o_zero;
     d.o_tkey = o; o += d.S;
