@@ -220,3 +220,40 @@ def test_engine_chain_depth5_vs_oracle(oracle):
             _same(out[p], ref, view=False)
         cur = [Cipher(o.layers, o.meta, o.w_lo, o.w_hi) for o in out]
     assert cur[0].nE > 10000
+
+
+def _max_bucket_edges(oracle, x, y, B=337):
+    """Edges of the fullest libstdc++ bucket of ct_mul(x, y)'s keys (channels with products; random
+    weights make every such sum nonzero), and whether the pair takes the static-group path."""
+    G = 0x9E3779B97F4A7C15
+    LB = len(y.layers)
+    la, ia, ca = (x.meta & 0xFFFFFFFF).astype(np.int64), ((x.meta >> np.uint64(32)) & 0xFFFF).astype(np.int64), (x.meta >> np.uint64(48)).astype(np.int64)
+    lb, ib, cb = (y.meta & 0xFFFFFFFF).astype(np.int64), ((y.meta >> np.uint64(32)) & 0xFFFF).astype(np.int64), (y.meta >> np.uint64(48)).astype(np.int64)
+    lp = (la[:, None] * LB + lb[None, :]).ravel()
+    r = ((ia[:, None] + ib[None, :]) % B).ravel()
+    ch = (ca[:, None] ^ cb[None, :]).ravel()
+    keych = np.unique(lp * (2 * B) + r * 2 + ch)
+    keys, E = np.unique(keych // 2, return_counts=True)
+    n = x.nE * y.nE
+    nbk = oracle.bucket_count(n)
+    bk = np.array([(((int(k) // B) << 32 | (int(k) % B)) * G % 2**64) % nbk for k in keys], dtype=np.uint64)
+    _, inv = np.unique(bk, return_inverse=True)
+    per = np.bincount(inv, weights=E)
+    S = len(x.layers) * LB * B
+    return int(per.max()), nbk >= 2 * S
+
+
+def test_static_bucket_groups_and_escape_codes_vs_oracle(oracle):
+    """General-path ordering structures: static bucket groups (bucket count >= 2 S: saturated
+    4-layer ciphers x sparse 8-layer ciphers, whose colliding buckets hold 3+ edges, the escape code
+    of the 16-time leader blocks) next to dynamic bucket chains (sparse pairs) in one batch."""
+    rng = np.random.default_rng(9)
+    xs, ys = [], []
+    for k in range(6):
+        xs.append(_mk(rng, 4, 4 * 2 * 337, dup_ok=False)); ys.append(_mk(rng, 8, 16, dup_ok=False))
+        xs.append(_mk(rng, 4, 30, dup_ok=False)); ys.append(_mk(rng, 2, 40, dup_ok=False))
+    kinds = [_max_bucket_edges(oracle, x, y) for x, y in zip(xs, ys)]
+    assert any(st and mx >= 3 for mx, st in kinds), kinds   # static groups with escape codes
+    assert any(not st for _, st in kinds), kinds             # dynamic chains
+    plan = _check_vs_oracle(oracle, {"canon_tag": 11}, xs, ys, 15)
+    assert plan.n_large == len(xs)
