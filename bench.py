@@ -188,6 +188,10 @@ def main():
             if pm.get("pairs") == n and pm.get("epl") == args.epl:
                 result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
                 result["roofline"]["traffic_source"] = pm.get("source")
+                # the integer-ALU side of the same kernel (PMC): share of SIMD cycles issuing VALU
+                if pm.get("valu_busy_frac") is not None:
+                    result["roofline"]["valu_busy_frac"] = pm.get("valu_busy_frac")
+                    result["roofline"]["valu_insts_per_pair"] = pm.get("valu_insts_per_launch", 0) / n
         except Exception:
             pass
 

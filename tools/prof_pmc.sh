@@ -54,6 +54,7 @@ epl = int(args[args.index("--epl") + 1]) if "--epl" in args else 20
 if k and "hbm_bytes_per_launch" in k:
     json.dump({"pairs": pairs, "epl": epl, "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
                "hbm_read_bytes": k["hbm_read_bytes_corrected"], "hbm_write_bytes": k["hbm_write_bytes"],
+               "valu_busy_frac": k.get("valu_busy_frac"), "valu_insts_per_launch": k.get("SQ_INSTS_VALU"),
                "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) / WRITE_SIZE, "
                          "mean per dispatch; tools/prof_pmc.sh"}, open(sys.argv[2], "w"), indent=1)
 PY
