@@ -320,7 +320,25 @@ def extras(eng, args, with_cpu):
     res["ct_mul_with_sigma"] = sigma_bench(eng, args, with_cpu)
     res["cfg4_chain"] = chain_bench(eng, args)
     res["enc_value"] = enc_bench(eng, args, with_cpu)
+    res["ct_mul_host_roundtrip"] = _host_roundtrip()
     return res
+
+
+def _host_roundtrip(pairs=1 << 15):
+    """PCIe-inclusive rate through the C++ drop-in adapter (include/pvac_hip.hpp): host AoS
+    ciphers in and out (AoS -> SoA, H2D, plan + exec, D2H, SoA -> AoS), weights only. Never the
+    headline value; reported so the device-resident value can be read against it."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "test_adapter")
+    if not os.path.exists(exe):
+        return None
+    try:
+        outp = subprocess.run([exe, "--time", str(pairs)], capture_output=True, text=True, timeout=300)
+        r = json.loads([l for l in outp.stdout.splitlines() if l.startswith("{")][-1])
+        r["path"] = "pvac_hip::ct_mul_batch (host Cipher vectors), tests/cpp/test_adapter --time"
+        return r
+    except Exception as ex:
+        return {"error": repr(ex)}
 
 
 def sigma_bench(eng, args, with_cpu):

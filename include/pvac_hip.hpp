@@ -40,6 +40,7 @@
 #include <map>
 #include <memory>
 #include <stdexcept>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -119,6 +120,22 @@ struct batch {
     }
 };
 
+// Runs f(begin, end) over [0, n) on up to hardware_concurrency() threads (AoS <-> SoA conversion
+// of large batches; each cipher is independent).
+template <class F>
+void parallel_ranges(size_t n, F f) {
+    const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>(std::min<size_t>(hw, 32), n / 256 + 1);
+    if (nt <= 1) { f(size_t(0), n); return; }
+    std::vector<std::thread> th;
+    const size_t per = (n + nt - 1) / nt;
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t b = t * per, e = std::min(n, b + per);
+        if (b < e) th.emplace_back([=, &f]() { f(b, e); });
+    }
+    for (auto& x : th) x.join();
+}
+
 template <class CipherT>
 void to_host(const std::vector<const CipherT*>& cs, uint32_t sigma_words, bool with_sigma, batch& b) {
     const size_t n = cs.size();
@@ -132,23 +149,26 @@ void to_host(const std::vector<const CipherT*>& cs, uint32_t sigma_words, bool w
     b.layers.resize(lo);
     b.meta.resize(eo); b.w_lo.resize(eo); b.w_hi.resize(eo);
     if (with_sigma) b.sigma.assign(eo * sigma_words, 0);
-    size_t l = 0, e = 0;
-    for (const CipherT* c : cs) {
-        for (const auto& L : c->L) {
-            pvac_layer& y = b.layers[l++];
-            y.rule = (uint32_t)L.rule; y.pa = L.pa; y.pb = L.pb; y.pad = 0;
-            y.ztag = L.seed.ztag; y.nonce_lo = L.seed.nonce.lo; y.nonce_hi = L.seed.nonce.hi;
-        }
-        for (const auto& E : c->E) {
-            b.meta[e] = (uint64_t)E.layer_id | ((uint64_t)E.idx << 32) | ((uint64_t)E.ch << 48);
-            b.w_lo[e] = E.w.lo; b.w_hi[e] = E.w.hi;
-            if (with_sigma) {
-                const size_t k = std::min<size_t>(E.s.w.size(), sigma_words);
-                if (k) std::memcpy(&b.sigma[e * sigma_words], E.s.w.data(), k * 8);
+    parallel_ranges(n, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            const CipherT* c = cs[i];
+            size_t l = b.l_off[i], e = b.e_off[i];
+            for (const auto& L : c->L) {
+                pvac_layer& y = b.layers[l++];
+                y.rule = (uint32_t)L.rule; y.pa = L.pa; y.pb = L.pb; y.pad = 0;
+                y.ztag = L.seed.ztag; y.nonce_lo = L.seed.nonce.lo; y.nonce_hi = L.seed.nonce.hi;
             }
-            ++e;
+            for (const auto& E : c->E) {
+                b.meta[e] = (uint64_t)E.layer_id | ((uint64_t)E.idx << 32) | ((uint64_t)E.ch << 48);
+                b.w_lo[e] = E.w.lo; b.w_hi[e] = E.w.hi;
+                if (with_sigma) {
+                    const size_t k = std::min<size_t>(E.s.w.size(), sigma_words);
+                    if (k) std::memcpy(&b.sigma[e * sigma_words], E.s.w.data(), k * 8);
+                }
+                ++e;
+            }
         }
-    }
+    });
 }
 
 inline void upload(batch& b, hipStream_t s, bool with_sigma) {
@@ -189,7 +209,8 @@ std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t e
     }
     hip_ok(hipStreamSynchronize(s), "sync");
     std::vector<CipherT> out(n);
-    for (size_t i = 0; i < n; ++i) {
+    parallel_ranges(n, [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; ++i) {
         CipherT& C = out[i];
         C.L.resize(c.l_cnt[i]);
         for (size_t l = 0; l < c.l_cnt[i]; ++l) {
@@ -207,11 +228,15 @@ std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t e
             E.idx = (uint16_t)(c.meta[e] >> 32);
             E.ch = (uint8_t)(c.meta[e] >> 48);
             E.w.lo = c.w_lo[e]; E.w.hi = c.w_hi[e];
-            E.s.nbits = m_bits;
-            if (with_sigma) E.s.w.assign(&c.sigma[e * c.sigma_words], &c.sigma[e * c.sigma_words] + c.sigma_words);
-            else E.s.w.assign(c.sigma_words, 0);
+            // weights-only results (an engine extension: the reference always draws sigma) keep an
+            // empty BitVec instead of a zeroed m_bits one (1 KiB per edge); save_cts zero-pads it
+            if (with_sigma) {
+                E.s.nbits = m_bits;
+                E.s.w.assign(&c.sigma[e * c.sigma_words], &c.sigma[e * c.sigma_words] + c.sigma_words);
+            }
         }
     }
+    });
     return out;
 }
 

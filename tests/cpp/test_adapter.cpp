@@ -4,7 +4,9 @@
 // the unmodified reference (tests/golden/ref, tests/golden/bounty). Runs on the GPU box:
 //   test_adapter <golden_dir> <canon_tag> <H_digest_hex>
 // Exit 0 = every check passed; failures abort with a message (like the reference's must()).
+//   test_adapter --time <pairs>   end-to-end (host ciphers in and out) ct_mul rate, JSON
 #include <array>
+#include <chrono>
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
@@ -197,7 +199,55 @@ struct replay_pad {
     uint64_t operator()() { return k < s.size() ? s[k++] : (++k, 0ull); }
 };
 
+// --time <pairs>: end-to-end rate of the by-value batched ct_mul (weights only) on host ciphers
+// shaped like enc_value output (2 BASE layers x 20 distinct (idx, ch) edges): AoS -> SoA, H2D,
+// plan + exec, D2H, SoA -> AoS all inside the timed region. Prints one JSON line.
+static int time_host_roundtrip(size_t n) {
+    uint64_t st = 0x5EED0006;
+    auto rnd = [&]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto fresh = [&]() {
+        Cipher c;
+        c.L.resize(2);
+        for (auto& l : c.L) { l.rule = mirror::RRule::BASE; l.seed.ztag = rnd(); l.seed.nonce = {rnd(), rnd()}; l.pa = l.pb = 0; }
+        for (uint32_t la = 0; la < 2; ++la) {
+            std::vector<uint32_t> used;
+            while (used.size() < 20) {
+                const uint32_t k = (uint32_t)(rnd() % (2 * 337));
+                bool dup = false;
+                for (uint32_t u : used) dup |= u == k;
+                if (dup) continue;
+                used.push_back(k);
+                mirror::Edge e{};
+                e.layer_id = la; e.idx = (uint16_t)(k >> 1); e.ch = (uint8_t)(k & 1);
+                e.w = mirror::Fp{rnd(), rnd() & 0x7FFFFFFFFFFFFFFFull};
+                c.E.push_back(e);
+            }
+        }
+        return c;
+    };
+    std::vector<Cipher> A(n), B(n);
+    for (size_t i = 0; i < n; ++i) { A[i] = fresh(); B[i] = fresh(); }
+    mirror::PubKey pk;
+    pk.canon_tag = 0x5EED0006;
+    auto src = [&]() { return rnd(); };
+    (void)pvac_hip::ct_mul_batch(pk, A, B, false, src);   // warm-up (allocations, code objects)
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto C = pvac_hip::ct_mul_batch(pk, A, B, false, src);
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    size_t edges = 0;
+    for (const auto& c : C) edges += c.E.size();
+    std::printf("{\"pairs\": %zu, \"seconds\": %.6f, \"ct_mul_per_s\": %.1f, \"output_edges\": %zu}\n", n, sec,
+                n / sec, edges);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 3 && std::string(argv[1]) == "--time") return time_host_roundtrip(std::strtoull(argv[2], nullptr, 10));
     if (argc < 5) {
         std::fprintf(stderr, "usage: %s <golden_dir> <canon_tag> <H_digest_hex> <v0,v1,...>\n", argv[0]);
         return 2;
