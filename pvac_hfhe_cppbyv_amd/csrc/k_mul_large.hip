@@ -190,7 +190,8 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
             const uint32_t e = dids[k];
             const uint64_t m = D.meta[deo + e];
             const uint32_t sl = meta_idx(m) * 2 + meta_ch(m);
-            if (atomicCAS(&di[sl], kInf, e) != kInf) {
+            // di holds the dense side's share of the first-insert time t = i |B.E| + j
+            if (atomicCAS(&di[sl], kInf, denseA ? e * nB : e) != kInf) {
                 *dup = 1;
             } else {   // canonical operands: the lazy product below needs a, b < 2^127
                 const fp w = fp_canon(D.w_lo[deo + e], D.w_hi[deo + e]);
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                     const fp w = fp_canon(Sp.w_lo[seo + e], Sp.w_hi[seo + e]);
                     swv[k] = make_ulonglong2(w.lo, w.hi);
                     sinf[k] = meta_idx(m) | (meta_ch(m) << 16);
-                    sidv[k] = e;
+                    sidv[k] = denseA ? e : e * nB;   // the sparse side's share of t
                 }
                 __syncthreads();
 #pragma unroll
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                                 fp_mul_fold1(fp{dv.x, dv.y}, fp{sw.x, sw.y}, x0, x1);
                                 if (c == sch) acc_add(P[u], x0, x1);
                                 else acc_add(M[u], x0, x1);
-                                const uint32_t t = denseA ? e * nB + se : se * nB + e;
+                                const uint32_t t = e + se;
                                 tmin[u] = t < tmin[u] ? t : tmin[u];
                             }
                         }
