@@ -52,10 +52,23 @@ __device__ __forceinline__ void derive(const prf_consts& k, uint64_t ztag, uint6
     for (int i = 0; i < 8; ++i) key[i] = bswap32d(s.h[i]);   // digest bytes -> little-endian key words
 }
 
+// T0 only, replicated kTCopies times in a bank-per-lane layout: entry x of copy c is LDS word
+// x * kTCopies + c, and lane l reads copy l % kTCopies, so the 64 lanes of a lookup hit at most two
+// words per bank (one per lane half) instead of colliding at random; T1..T3 are byte rotations.
+constexpr uint32_t kTCopies = 32;
+
+__device__ __forceinline__ uint32_t tlook(const uint32_t* T, uint32_t x) {
+    return T[(x * kTCopies) | (threadIdx.x & (kTCopies - 1))];
+}
+
 __device__ __forceinline__ void ctr_block(uint64_t ctr, const uint32_t* T, const uint32_t* rk, uint64_t& lo,
                                           uint64_t& hi) {
     uint32_t w0 = (uint32_t)ctr, w1 = (uint32_t)(ctr >> 32), w2 = 0, w3 = 0;
-    aes256_encrypt(w0, w1, w2, w3, [&](int t, uint32_t x) { return T[t * 256 + x]; },
+    aes256_encrypt(w0, w1, w2, w3,
+                   [&](int t, uint32_t x) {
+                       const uint32_t v = tlook(T, x);
+                       return t == 0 ? v : __builtin_amdgcn_alignbit(v, v, 32 - 8 * t);   // rotl(v, 8t)
+                   },
                    [&](int i) { return rk[i]; });
     lo = ((uint64_t)w1 << 32) | w0;
     hi = ((uint64_t)w3 << 32) | w2;
@@ -63,7 +76,7 @@ __device__ __forceinline__ void ctr_block(uint64_t ctr, const uint32_t* T, const
 
 __device__ void expand_key(const uint32_t key[8], uint32_t* rk, const uint32_t* T) {
     uint32_t r[60];
-    aes256_expand(key, r, [&](uint32_t x) { return (T[x] >> 8) & 0xFFu; });
+    aes256_expand(key, r, [&](uint32_t x) { return (tlook(T, x) >> 8) & 0xFFu; });
     for (int i = threadIdx.x & 63; i < 60; i += 64) rk[i] = r[i];
 }
 
@@ -73,11 +86,11 @@ __device__ __forceinline__ uint64_t wave_xor_u64(uint64_t x) {
     return x;
 }
 
-__global__ __launch_bounds__(kPB) void k_prf_core(prf_consts k, const prf_request* req, uint64_t n, uint64_t* out) {
-    __shared__ uint32_t T[4 * 256];
+__global__ __launch_bounds__(kPB, 4) void k_prf_core(prf_consts k, const prf_request* req, uint64_t n, uint64_t* out) {
+    __shared__ uint32_t T[256 * kTCopies];
     __shared__ uint64_t S[64];
     __shared__ uint32_t RK[kPB / 64][2][60];
-    for (int i = threadIdx.x; i < 4 * 256; i += kPB) T[i] = c_aes.T[i >> 8][i & 255];
+    for (int i = threadIdx.x; i < 256 * (int)kTCopies; i += kPB) T[i] = c_aes.T[0][i / kTCopies];
     for (int i = threadIdx.x; i < 64; i += kPB) S[i] = i < (int)k.s_words ? k.s_bits[i] : 0ull;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
