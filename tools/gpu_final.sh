@@ -1,0 +1,14 @@
+#!/bin/bash
+# round-end rehearsal on the GPU box: gpu tests, smoke(), default bench, rocprof kernel stats
+set -o pipefail
+mkdir -p gpurun_out/final
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/final/pytest.log 2>&1 || { tail -20 gpurun_out/final/pytest.log; exit 1; }
+tail -1 gpurun_out/final/pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1 || { tail -20 gpurun_out/final/smoke.log; exit 1; }
+tail -1 gpurun_out/final/smoke.log
+timeout -k 10 600 python bench.py > gpurun_out/final/bench.log 2>&1 || { tail -20 gpurun_out/final/bench.log; exit 1; }
+tail -1 gpurun_out/final/bench.log | cut -c1-600
+(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/final/prof" -o run --output-format csv \
+    -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/final/prof.log" 2>&1) || exit $?
+echo prof ok
