@@ -247,20 +247,31 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
           // block-0 midstates of the wave's next kMidBatch edges: lane j computes edge j's X-stream
           // midstate, lane 32 + j its noise-stream midstate (block 0 holds the label, the first six
           // words and the salt's low byte(s); it does not depend on the counter)
+          // The same lane then draws counter 32 of its edge and stream (the first block of pass 1):
+          // pass 0's 128 draws hold K = 128 distinct values only when there is no repeat, so most
+          // edges need a few more draws, and these four (kept in registers, read by the edge's
+          // turn with readlane) usually suffice instead of a whole second pass.
+          uint32_t pre[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
           {
             const uint64_t kk = kb + (uint64_t)(lane & 31) * nsub;
             if (kk < ne) {
                 uint64_t words[7];
                 edge_words(eo, lo, nl, eo + kk, words);
-                uint32_t b0[16];
-                if (isX) build_block<15, 7>(b0, 0, kLabX, words, 0);
-                else build_block<14, 7>(b0, 0, kLabN, words, 0);
+                uint32_t b0[16], b1[16];
+                if (isX) { build_block<15, 7>(b0, 0, kLabX, words, 0); build_block<15, 7>(b1, 1, kLabX, words, 32); }
+                else { build_block<14, 7>(b0, 0, kLabN, words, 0); build_block<14, 7>(b1, 1, kLabN, words, 32); }
                 sha_state ms;
                 sha_init(ms);
                 sha_compress(ms, b0);
                 uint32_t* dst = mids + ((lane & 31) * 2 + (isX ? 0 : 1)) * 8;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) dst[i] = ms.h[i];
+                sha_compress(ms, b1);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t x = (uint64_t)bswap32(ms.h[2 * q]) | ((uint64_t)bswap32(ms.h[2 * q + 1]) << 32);
+                    pre[q] = x <= lim ? (uint32_t)(POW2 ? (x & (uint64_t)(Nmod - 1u)) : x % Nmod) : 0xFFFFFFFFu;
+                }
             }
             __builtin_amdgcn_wave_barrier();
           }
@@ -287,7 +298,20 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // as a big-endian 96-bit window over words 1..3 that is bswap64(ctr) << 8 or << 16
             const uint32_t csh = isX ? 8u : 16u;
             uint32_t have = 0;
-            for (uint32_t pass = 0; pass < kMaxPasses; ++pass) {   // bounded: never hang the GPU
+            // step 0: pass 0; step 1: counter 32 alone (precomputed above, lanes 0 and 32); step
+            // s >= 2: pass s - 1, whose counter-32 block was consumed by step 1 (draw order kept)
+            const uint32_t jl = (uint32_t)jb;
+            for (uint32_t step = 0; step < kMaxPasses; ++step) {   // bounded: never hang the GPU
+                uint32_t val[4];
+                if (step == 1) {   // wave-uniform
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t vx = __builtin_amdgcn_readlane(pre[q], jl);
+                        const uint32_t vn = __builtin_amdgcn_readlane(pre[q], 32 + jl);
+                        val[q] = (have < K && (lane & 31) == 0) ? (isX ? vx : vn) : 0xFFFFFFFFu;
+                    }
+                } else {
+                const uint32_t pass = step == 0 ? 0u : step - 1u;
                 const uint64_t ctr = (uint64_t)pass * 32 + (lane & 31);
                 const uint64_t bs = ((uint64_t)bswap32((uint32_t)ctr) << 32) | bswap32((uint32_t)(ctr >> 32));
                 uint32_t blk[16];
@@ -298,12 +322,13 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                 blk[3] |= (uint32_t)(bs << csh);
                 sha_state s = mid;
                 sha_compress(s, blk);
-                uint32_t val[4];
+                const bool used = pass == 1 && (lane & 31) == 0;   // counter 32: taken in step 1
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint64_t x = (uint64_t)bswap32(s.h[2 * q]) | ((uint64_t)bswap32(s.h[2 * q + 1]) << 32);
-                    val[q] = (have < K && x <= lim) ? (uint32_t)(POW2 ? (x & (uint64_t)(Nmod - 1u)) : x % Nmod)
-                                                    : 0xFFFFFFFFu;
+                    val[q] = (have < K && x <= lim && !used) ? (uint32_t)(POW2 ? (x & (uint64_t)(Nmod - 1u)) : x % Nmod)
+                                                             : 0xFFFFFFFFu;
+                }
                 }
                 int rank[4];
                 select_pass2x32(val, bm, K, have, rank);
