@@ -257,3 +257,21 @@ def test_static_bucket_groups_and_escape_codes_vs_oracle(oracle):
     assert any(not st for _, st in kinds), kinds             # dynamic chains
     plan = _check_vs_oracle(oracle, {"canon_tag": 11}, xs, ys, 15)
     assert plan.n_large == len(xs)
+
+
+def test_engine_chain_depth8_vs_oracle(oracle):
+    """BASELINE cfg 4 at its full depth: c_k = c_{k-1} * x for two fresh inputs to depth 8
+    (345,088 edges, 6.8 M products per pair at step 8, static bucket groups and 16-time leader
+    blocks in use), every step bit-exact vs the oracle on the engine's previous output."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0xC8)
+    n = 2
+    X = [Cipher(c.layers, c.meta, c.w_lo, c.w_hi) for c in eng.gen_fresh(n, 0x8000, 20).to_host()]
+    cur = X
+    for k in range(1, 9):
+        out, plan, per = _run_mul(eng, cur, X, seed=200 + k)
+        for p in range(n):
+            ref = oracle.ct_mul(cur[p], X[p], per[p], canon_tag=0xC8)
+            _same(out[p], ref, view=False)
+        cur = [Cipher(o.layers, o.meta, o.w_lo, o.w_hi) for o in out]
+    assert min(c.nE for c in cur) == 345088

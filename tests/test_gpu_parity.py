@@ -297,3 +297,47 @@ def test_sigma_batch_matches_oracle(engine, oracle):
                                (int(c.meta[e]) >> 32) & 0xFFFF, (int(c.meta[e]) >> 48) & 0xFF, int(sl[k]))
             assert np.array_equal(c.sigma[e], ref), (k,)
             k += 1
+
+
+def _pair_host(X, p):
+    """Cipher p of a device batch, copied alone (no full-batch transfer)."""
+    from helpers import LAYER_DT
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    lo, lc = int(X.l_off[p].item()), int(X.l_cnt[p].item())
+    eo, ec = int(X.e_off[p].item()), int(X.e_cnt[p].item())
+    layers = X.layers[lo:lo + lc].cpu().numpy().reshape(-1).view(LAYER_DT).copy()
+    return Cipher(layers, u(X.meta[eo:eo + ec]).copy(), u(X.w_lo[eo:eo + ec]).copy(), u(X.w_hi[eo:eo + ec]).copy())
+
+
+def test_cfg3_full_batch_sampled_vs_oracle(oracle):
+    """BASELINE cfg 3 at its full size (2^20 fresh-shaped pairs, the bench's batch and generator):
+    512 pairs spread over the whole batch bit-exact vs the oracle (weights, emit order, layers incl.
+    ztags), every pair within its planned capacity with status 0, and a second run of the same
+    batch identical (per-pair device digests)."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0x5EED0003)
+    n = 1 << 20
+    A = eng.gen_fresh(n, 0x5EED0003, 20)
+    B = eng.gen_fresh(n, 0x5EED0004, 20)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    nonces = eng.fill_nonces(A, B, Cb, plan, 0x5EED0005)
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    ecnt, eoff = u(out.e_cnt[:n]), u(out.e_off[:n])
+    cap = np.diff(np.append(eoff, np.uint64(plan.total_edge_slots)))
+    assert (ecnt <= cap).all() and ecnt.min() > 0
+    dig1 = u(eng.digest(out)[:n]).copy()
+    rng = np.random.default_rng(3)
+    picks = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 510)]))
+    nz = nonces.cpu().numpy().view(np.uint64)
+    loff = u(Cb.l_off[:n])
+    for p in picks:
+        x, y = _pair_host(A, int(p)), _pair_host(B, int(p))
+        base = int(loff[p]) + x.nL + y.nL
+        ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0x5EED0003)
+        _assert_same(_pair_host(out, int(p)), ref, layers_view=False)
+    del out, Cb   # two 2^20-pair outputs together are ~140 GB
+    eng.torch.cuda.empty_cache()
+    Cb2, plan2 = eng.ct_mul_plan(A, B)
+    out2 = eng.ct_mul(A, B, nonces=nonces, C_=Cb2, plan=plan2)
+    assert np.array_equal(u(eng.digest(out2)[:n]), dig1)
