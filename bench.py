@@ -57,12 +57,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL; PVAC_BENCH_BACKEND=gloo rehearses the multi-rank flow with
+    # ranks sharing the visible GPUs (local rank modulo the device count)
+    backend = os.environ.get("PVAC_BENCH_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
     from pvac_hfhe_cppbyv_amd import Engine
 
-    eng = Engine(device=local, canon_tag=0x5EED0003)
+    eng = Engine(device=gpu, canon_tag=0x5EED0003)
     dev = eng.device
     if args.only == "chain":
         print(json.dumps(chain_bench(eng, args)), flush=True)

@@ -36,6 +36,8 @@ def global_edge_offsets(local_total: int, device=None):
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return 0, int(local_total), [int(local_total)]
     world, rank = dist.get_world_size(), dist.get_rank()
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     mine = torch.tensor([int(local_total)], dtype=torch.int64, device=device)
     allt = torch.zeros(world, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(allt, mine)
@@ -50,6 +52,8 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
