@@ -148,7 +148,6 @@ struct mul_fresh_args {
     const uint32_t* nb_table;    // libstdc++ bucket count after reserve(n), n <= kFreshProdMax
     const uint64_t* nb_magic;    // fastmod64 multipliers for nb_table
     uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
-    const uint32_t* grp;         // static bucket-group tables (large_desc::g_head / g_next)
     uint64_t canon_tag;
     uint64_t edge_budget;
     uint32_t Bm;
