@@ -16,6 +16,7 @@
 // ranks come from a 32-lane prefix count. Selected columns are expanded through the sparse
 // H rows with LDS atomic XOR into a 1 KiB sigma image, written out as one 16-byte store per
 // lane.
+#include <algorithm>
 #include <vector>
 #include <cstring>
 
@@ -193,6 +194,7 @@ struct sig_args {
     const uint16_t* rows;
     const uint32_t* counts;
     uint32_t width;
+    uint32_t full;   // every column has exactly width rows
     uint64_t canon;
     uint32_t n_bits, m_bits, x_col_wt, err_wt;
     uint32_t sub_blocks;
@@ -351,6 +353,53 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // different groups never contend for a word. Copy 0 already holds the noise bits.
             const uint32_t W = a.width;
             const bool split = sw32 == 256u && bx32 + bn32 >= 768u;   // default Params: 4 copies fit
+            // Full row lists (every column exactly W rows, as gen_H makes them): no per-row guard,
+            // the copies sit 272 words apart (bank offset 16 g without a modular wrap), and a flip
+            // is one bit-field extract, one address add and one shift from the packed row pair.
+            // Copy 3 reaches into the column list, so both column ids are read first.
+            const bool fast = split && a.full && a.x_col_wt <= 128u && per_wave >= 1072u;
+            if (fast) {
+                const uint32_t c0 = (uint32_t)lane < a.x_col_wt ? cols[lane] : 0u;
+                const uint32_t c1 = (uint32_t)lane + 64u < a.x_col_wt ? cols[lane + 64] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t w4 = lane; w4 < (1072u - 256u) / 4u; w4 += 64) ((uint4*)(sig + 256))[w4] = make_uint4(0, 0, 0, 0);
+                __builtin_amdgcn_wave_barrier();
+                uint32_t* img = sig + 272u * ((uint32_t)lane >> 4);
+                auto flip2 = [&](uint32_t x) {   // rows x & 0xFFFF and x >> 16
+                    atomicXor(&img[__builtin_amdgcn_ubfe(x, 5, 11)], 1u << (x & 31u));
+                    atomicXor(&img[__builtin_amdgcn_ubfe(x, 21, 11)], 1u << __builtin_amdgcn_ubfe(x, 16, 5));
+                };
+#pragma unroll 1
+                for (uint32_t cc = 0; cc < 2; ++cc) {
+                    if ((uint32_t)lane + 64u * cc >= a.x_col_wt) break;
+                    const uint4* rp = (const uint4*)(a.rows + (size_t)(cc ? c1 : c0) * W);
+                    constexpr uint32_t kB = 8;
+                    for (uint32_t q8 = 0; q8 < W / 8u; q8 += kB) {
+                        uint4 v[kB];
+#pragma unroll
+                        for (uint32_t b = 0; b < kB; ++b) v[b] = q8 + b < W / 8u ? rp[q8 + b] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                        for (uint32_t b = 0; b < kB; ++b) {
+                            if (q8 + b >= W / 8u) break;
+                            flip2(v[b].x); flip2(v[b].y); flip2(v[b].z); flip2(v[b].w);
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t* out = a.X.sigma + e * words_per_sigma;
+                for (uint32_t w4 = lane; w4 < 64u; w4 += 64) {
+                    uint4 v = *(const uint4*)(sig + w4 * 4);
+#pragma unroll
+                    for (uint32_t g = 1; g < 4; ++g) {
+                        const uint4 u = *(const uint4*)(sig + 272u * g + w4 * 4);
+                        v.x ^= u.x; v.y ^= u.y; v.z ^= u.z; v.w ^= u.w;
+                    }
+                    ((ulonglong2*)out)[w4] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
+                                                             (uint64_t)v.z | ((uint64_t)v.w << 32));
+                }
+                for (uint32_t w = lane; w < 1072u; w += 64) sig[w] = 0;
+                continue;
+            }
             if (split) {
                 for (uint32_t w4 = lane; w4 < 192u; w4 += 64) ((uint4*)(sig + 256))[w4] = make_uint4(0, 0, 0, 0);
                 __builtin_amdgcn_wave_barrier();
@@ -518,6 +567,7 @@ hipError_t sigma_tables_from_dense(sigma_tables& T, const pvac_hip_params& prm, 
         }
     }
     hipError_t e = alloc_tables(T, prm.n_bits, width);
+    T.full = std::all_of(cnt.begin(), cnt.end(), [&](uint32_t k) { return k == width; });
     if (e == hipSuccess) e = hipMemcpyAsync(T.rows, rows.data(), rows.size() * 2, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(T.counts, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -531,6 +581,7 @@ hipError_t sigma_tables_generate(sigma_tables& T, const pvac_hip_params& prm, ui
     // row lists padded to 16-byte multiples (k_sigma reads uint4); counts bound every reader
     hipError_t e = alloc_tables(T, prm.n_bits, (prm.h_col_wt + 7) & ~7u);
     if (e != hipSuccess) return e;
+    T.full = T.width == prm.h_col_wt;   // gen_H draws exactly h_col_wt distinct rows per column
     const size_t lds = (size_t)4 * (prm.m_bits / 32) * 4;
     hipLaunchKernelGGL(k_gen_H, dim3(2048), dim3(256), lds, st, T.rows, T.counts, T.width, prm.m_bits, prm.n_bits,
                        prm.h_col_wt, prm.canon_tag);
@@ -575,6 +626,7 @@ hipError_t launch_sigma(const sigma_tables& T, const pvac_hip_params& prm, const
     a.rows = T.rows;
     a.counts = T.counts;
     a.width = T.width;
+    a.full = T.full ? 1u : 0u;
     a.canon = prm.canon_tag;
     a.n_bits = prm.n_bits;
     a.m_bits = prm.m_bits;

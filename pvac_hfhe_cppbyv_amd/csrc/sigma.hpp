@@ -13,6 +13,7 @@ struct sigma_tables {
     uint32_t* counts = nullptr;
     uint32_t width = 0;
     uint32_t n_cols = 0;
+    bool full = false;   // every column has exactly `width` rows (no padding: k_sigma drops its guards)
     bool ready = false;
 };
 
