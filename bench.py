@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--chain-chunk", type=int, default=1 << 10)
     ap.add_argument("--chain-depth", type=int, default=8)
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
-    ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc"], default=None,
+    ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc", "add"], default=None,
                     help="run one side measurement alone (profiling) and print its JSON")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
@@ -79,6 +79,9 @@ def main():
         return
     if args.only == "enc":
         print(json.dumps(enc_bench(eng, args, False)), flush=True)
+        return
+    if args.only == "add":
+        print(json.dumps(add_bench(eng, args)), flush=True)
         return
     from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks
     n = args.pairs if args.pairs else (1 << 20 if world == 1 else 1 << 21)
@@ -324,6 +327,7 @@ def extras(eng, args, with_cpu):
             fp[name]["gpu_output_matches"] = bool(np.array_equal(glo, olo))
     res["fp127_cfg2"] = fp
     del bufs
+    res["ct_add_sub_cfg3"] = add_bench(eng, args)
     res["ct_mul_with_sigma"] = sigma_bench(eng, args, with_cpu)
     res["cfg4_chain"] = chain_bench(eng, args)
     res["enc_value"] = enc_bench(eng, args, with_cpu)
@@ -346,6 +350,46 @@ def _host_roundtrip(pairs=1 << 15):
         return r
     except Exception as ex:
         return {"error": repr(ex)}
+
+
+def add_bench(eng, args):
+    """Batched ct_add / ct_sub (A13 / A6) on the cfg-3 batch shape (2^20 fresh-shaped pairs,
+    weights only): the k_ct_add stream kernel against the HBM roofline. Algorithmic bytes per
+    pair: every input edge read and written once (2 x 24 B x (|A.E| + |B.E|)), every layer record
+    read and written (2 x 40 B x (|A.L| + |B.L|)), plus 5 x 8 B of counts / offsets per cipher."""
+    import torch
+    dev = eng.device
+    n = args.pairs if args.pairs else 1 << 20
+    A = eng.gen_fresh(n, 0x5EED0A01, args.epl)
+    B = eng.gen_fresh(n, 0x5EED0A02, args.epl)
+    res = {"pairs": n}
+    for name, neg in (("add", False), ("sub", True)):
+        C_ = eng.ct_add(A, B, negate=neg)   # warm-up
+        del C_
+        torch.cuda.synchronize(dev)
+        eng.timing_reset()
+        eng.timing(True)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            C_ = None
+            C_ = eng.ct_add(A, B, negate=neg)
+        torch.cuda.synchronize(dev)
+        el = (time.perf_counter() - t0) / reps
+        eng.timing(False)
+        ms, cnt = eng.timing_get("ct_add")
+        avg = ms / max(cnt, 1)
+        ne = float((A.e_cnt[:n] + B.e_cnt[:n]).sum().item())
+        nl = float((A.l_cnt[:n] + B.l_cnt[:n]).sum().item())
+        alg = 48.0 * ne + 80.0 * nl + 5 * 8.0 * 3 * n
+        res[name] = {"ops_per_s": n / el, "ms_per_batch": el * 1000, "avg_kernel_ms": avg,
+                     "achieved_GBs": alg / (avg / 1000.0) / 1e9 if avg > 0 else None,
+                     "frac_of_hbm_peak": alg / (avg / 1000.0) / 1e9 / HBM_PEAK_GBS if avg > 0 else None,
+                     "output_edges": int(C_.e_cnt[:n].sum().item())}
+        del C_
+    del A, B
+    torch.cuda.empty_cache()
+    return res
 
 
 def sigma_bench(eng, args, with_cpu):
