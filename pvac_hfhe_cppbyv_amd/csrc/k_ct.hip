@@ -333,54 +333,68 @@ __global__ __launch_bounds__(kAddBlock) void k_ct_add(pvac_ct_batch A, pvac_ct_b
 }
 
 
-// Pairs of at most 64 layers (every fresh and most chain ciphers): one WAVE per pair, four per
-// workgroup, no barriers. compact_layers is a 64-bit mask closure (lane l holds layer l's PROD
-// parents, as in k_ct_mul_fresh), the remap a popcount below each kept layer, kept in a per-wave
-// LDS table for the edges' lookups. k_ct_add's one workgroup per pair spent six barriers on
-// ~80 edges and ran at 14% of the HBM roofline.
+// Pairs of at most 64 layers (every fresh and most chain ciphers): a group of G lanes per pair,
+// G = 64 (one wave) or 32 (two pairs per wave, for pairs of at most 32 layers: twice the pairs in
+// flight per wave; the kernel is bound by each pair's chain of dependent memory round trips).
+// No barriers: compact_layers is a 64-bit mask closure (lane l of the group holds layer l's PROD
+// parents, as in k_ct_mul_fresh), the remap a popcount below each kept layer, kept in a per-group
+// LDS table for the edges' lookups. k_ct_add's one workgroup per pair spent six barriers on ~80
+// edges and ran at 14% of the HBM roofline.
 constexpr int kAddWaves = 4;
+
+template <int G>
+__device__ __forceinline__ uint64_t group_or_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) v |= (uint64_t)__shfl_xor((long long)v, d, 64);
+    return v;
+}
+
+template <int G>
 __global__ __launch_bounds__(64 * kAddWaves) void k_ct_add_wave(pvac_ct_batch A, pvac_ct_batch B, pvac_ct_batch C,
                                                                int negate_b, const uint8_t* pair_class) {
+    static_assert(G == 32 || G == 64, "lane groups of 32 or 64 (16 measured no faster than 32)");
     __shared__ uint32_t remap_s[kAddWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t pr = (uint64_t)blockIdx.x * kAddWaves + wave;
-    if (pr >= A.n) return;   // wave-uniform; no block barrier below
-    if (pair_class && pair_class[pr] == PAIR_LARGE) return;   // over edge_budget: k_add_merge.hip
-    const uint32_t LA = (uint32_t)A.l_cnt[pr], LB = (uint32_t)B.l_cnt[pr];
-    const uint32_t L = LA + LB;   // <= 64 (host-checked)
-    const uint64_t nA = A.e_cnt[pr], nB = B.e_cnt[pr];
-    const uint64_t alo = A.l_off[pr], blo = B.l_off[pr], aeo = A.e_off[pr], beo = B.e_off[pr];
-    const uint64_t clo = C.l_off[pr], ceo = C.e_off[pr];
+    const uint32_t gl = (uint32_t)lane & (G - 1);   // lane within the pair's group
+    const uint64_t pr = ((uint64_t)blockIdx.x * kAddWaves + wave) * (64 / G) + (uint32_t)lane / G;
+    // a group without a pair (batch tail, over-budget pair: k_add_merge.hip) runs with zero counts
+    // and stores nothing, so every group reaches the same shuffles
+    const bool live = pr < A.n && !(pair_class && pair_class[pr] == PAIR_LARGE);
+    const uint32_t LA = live ? (uint32_t)A.l_cnt[pr] : 0u, LB = live ? (uint32_t)B.l_cnt[pr] : 0u;
+    const uint32_t L = LA + LB;   // <= G (host-checked)
+    const uint64_t nA = live ? A.e_cnt[pr] : 0ull, nB = live ? B.e_cnt[pr] : 0ull;
+    const uint64_t alo = live ? A.l_off[pr] : 0ull, blo = live ? B.l_off[pr] : 0ull;
+    const uint64_t aeo = live ? A.e_off[pr] : 0ull, beo = live ? B.e_off[pr] : 0ull;
+    const uint64_t clo = live ? C.l_off[pr] : 0ull, ceo = live ? C.e_off[pr] : 0ull;
     // layers used by edges (encrypt.hpp:78)
     uint64_t used = 0;
-    for (uint64_t e = lane; e < nA; e += 64) {
+    for (uint64_t e = gl; e < nA; e += G) {
         const uint32_t lid = meta_layer(A.meta[aeo + e]);
         used |= lid < L ? 1ull << lid : 0ull;
     }
-    for (uint64_t e = lane; e < nB; e += 64) {
+    for (uint64_t e = gl; e < nB; e += G) {
         const uint32_t lid = meta_layer(B.meta[beo + e]) + LA;
         used |= lid < L ? 1ull << lid : 0ull;
     }
-    used = wave_or_u64(used);
+    used = group_or_u64<G>(used);
     // transitive PROD parents (encrypt.hpp:80-93)
-    const uint32_t l = (uint32_t)lane;
+    const uint32_t l = gl;
     pvac_layer x{};
     if (l < L) x = l < LA ? A.layers[alo + l] : B.layers[blo + (l - LA)];
     const uint32_t off = l < LA ? 0u : LA;
     const uint32_t pa = x.pa + off, pb = x.pb + off;
     const uint64_t mypm = (l < L && x.rule == 1) ? ((pa < L ? 1ull << pa : 0ull) | (pb < L ? 1ull << pb : 0ull)) : 0ull;
     uint64_t keep = used;
-    for (;;) {   // depth-bounded by L
-        const uint64_t nk = keep | wave_or_u64(((keep >> l) & 1ull) ? mypm : 0ull);
-        if (nk == keep) break;
+    for (;;) {   // depth-bounded by L; the wave stops when every group has reached its fixpoint
+        const uint64_t nk = keep | group_or_u64<G>(((keep >> l) & 1ull) ? mypm : 0ull);
+        const bool moved = nk != keep;
         keep = nk;
+        if (!__any(moved)) break;
     }
     const uint32_t kept = (uint32_t)__popcll(keep);
     const bool identity = kept == L;
-    const uint32_t to = ((keep >> l) & 1ull)
-                            ? __builtin_amdgcn_mbcnt_hi((uint32_t)(keep >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u))
-                            : 0xFFFFFFFFu;
-    uint32_t* remap = remap_s[wave];
+    const uint32_t to = ((keep >> l) & 1ull) ? (uint32_t)__popcll(keep & ((1ull << l) - 1ull)) : 0xFFFFFFFFu;
+    uint32_t* remap = remap_s[wave] + ((uint32_t)lane & ~(uint32_t)(G - 1));
     remap[l] = to;
     __builtin_amdgcn_wave_barrier();
     if (l < L && to != 0xFFFFFFFFu) {
@@ -392,13 +406,13 @@ __global__ __launch_bounds__(64 * kAddWaves) void k_ct_add_wave(pvac_ct_batch A,
         }
         C.layers[clo + to] = y;
     }
-    if (lane == 0) {
+    if (live && gl == 0) {
         C.l_cnt[pr] = kept;
         C.e_cnt[pr] = nA + nB;
     }
     // edges (concat; B shifted and optionally scaled by p-1)
     const fp pm1{kAll - 1, kM63};
-    for (uint64_t e = lane; e < nA + nB; e += 64) {
+    for (uint64_t e = gl; e < nA + nB; e += G) {
         const bool fromB = e >= nA;
         const uint64_t src = fromB ? beo + (e - nA) : aeo + e;
         uint64_t m = fromB ? B.meta[src] : A.meta[src];
@@ -419,7 +433,7 @@ __global__ __launch_bounds__(64 * kAddWaves) void k_ct_add_wave(pvac_ct_batch A,
         const uint32_t sw = C.sigma_words;
         const uint64_t chunks_per_edge = sw / 2;
         const uint64_t total = (nA + nB) * chunks_per_edge;
-        for (uint64_t c = lane; c < total; c += 64) {
+        for (uint64_t c = gl; c < total; c += G) {
             const uint64_t e = c / chunks_per_edge, k = c - e * chunks_per_edge;
             const bool fromB = e >= nA;
             const ulonglong2* srcp = fromB ? (const ulonglong2*)(B.sigma + (beo + (e - nA)) * B.sigma_words)
@@ -480,9 +494,14 @@ hipError_t launch_exclusive_scan_u64(uint64_t* data, size_t n, uint64_t* scratch
 hipError_t launch_ct_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, int negate_b,
                          uint32_t max_layers, const uint8_t* pair_class, hipStream_t st) {
     if (!A.n) return hipSuccess;
+    if (max_layers <= 32) {
+        hipLaunchKernelGGL(k_ct_add_wave<32>, dim3((unsigned)((A.n + 2 * kAddWaves - 1) / (2 * kAddWaves))),
+                           dim3(64 * kAddWaves), 0, st, A, B, C, negate_b, pair_class);
+        return hipGetLastError();
+    }
     if (max_layers <= 64) {
-        hipLaunchKernelGGL(k_ct_add_wave, dim3((unsigned)((A.n + kAddWaves - 1) / kAddWaves)), dim3(64 * kAddWaves), 0,
-                           st, A, B, C, negate_b, pair_class);
+        hipLaunchKernelGGL(k_ct_add_wave<64>, dim3((unsigned)((A.n + kAddWaves - 1) / kAddWaves)), dim3(64 * kAddWaves),
+                           0, st, A, B, C, negate_b, pair_class);
         return hipGetLastError();
     }
     const size_t lds = ((size_t)max_layers * 4 + 15) & ~(size_t)15;
