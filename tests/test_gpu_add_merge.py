@@ -156,3 +156,35 @@ def test_codec_interop_gpu():
     s = eng.ct_add(a, b, sigma=True)
     with open(os.path.join(GOLD, "bounty", "sum.ct"), "rb") as f:
         assert codec.write_ct(s.to_host()) == f.read()
+
+
+@pytest.mark.parametrize("nl_total", [6, 30, 40, 62, 90])
+@pytest.mark.parametrize("negate", [False, True])
+def test_add_layer_widths_vs_oracle(oracle, nl_total, negate):
+    """ct_add / ct_sub below edge_budget for every kernel width: 32-lane groups (<= 32 layers),
+    64-lane groups (<= 64) and the workgroup kernel (> 64). PROD layers with parents, layers no edge
+    references (compact_layers drops them unless a kept PROD layer needs them), batch tails that
+    leave half-empty lane groups, sigma carried."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    rng = np.random.default_rng(nl_total * 7 + negate)
+    xs, ys = [], []
+    for k in range(13):   # odd count: the last 32-lane group of the last wave has no pair
+        la = max(1, nl_total // 2 - k % 3)
+        lb = max(1, nl_total - la)
+        x, y = _mk(rng, la, 30 + k, sigma=True), _mk(rng, lb, 25, sigma=True)
+        for c in (x, y):
+            n = len(c.layers)
+            # edges only on even layers; odd layers >= 2 are PROD of two earlier layers
+            c.meta = (c.meta & ~np.uint64(0xFFFFFFFF)) | ((c.meta & np.uint64(0xFFFFFFFF)) & ~np.uint64(1))
+            for l in range(3, n, 4):
+                c.layers["rule"][l] = 1
+                c.layers["pa"][l] = l - 1
+                c.layers["pb"][l] = l - 3
+        xs.append(x)
+        ys.append(y)
+    eng = Engine(device=0)
+    A, B = _dev_batch(eng, xs, True), _dev_batch(eng, ys, True)
+    out = eng.ct_add(A, B, negate=negate, sigma=True).to_host()
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        ref = oracle.ct_add(x, y, negate=negate)
+        _same(out[p], ref, sigma=True)
