@@ -353,7 +353,7 @@ def _host_roundtrip(pairs=1 << 15):
 
 
 def add_bench(eng, args):
-    """Batched ct_add / ct_sub (A13 / A6) on the cfg-3 batch shape (2^20 fresh-shaped pairs,
+    """Batched ct_add / ct_sub / ct_scale (A13 / A6) on the cfg-3 batch shape (2^20 fresh-shaped pairs,
     weights only): the k_ct_add stream kernel against the HBM roofline. Algorithmic bytes per
     pair: every input edge read and written once (2 x 24 B x (|A.E| + |B.E|)), every layer record
     read and written (2 x 40 B x (|A.L| + |B.L|)), plus 5 x 8 B of counts / offsets per cipher."""
@@ -387,6 +387,24 @@ def add_bench(eng, args):
                      "frac_of_hbm_peak": alg / (avg / 1000.0) / 1e9 / HBM_PEAK_GBS if avg > 0 else None,
                      "output_edges": int(C_.e_cnt[:n].sum().item())}
         del C_
+    # ct_scale (A6), in place on A: each edge's weight read and written (2 x 16 B) plus its count/offset
+    s = (1 << 100) + 12345
+    for _ in range(2):
+        eng.ct_scale(A, s)
+    torch.cuda.synchronize(dev)
+    eng.timing_reset()
+    eng.timing(True)
+    for _ in range(5):
+        eng.ct_scale(A, s)
+    torch.cuda.synchronize(dev)
+    eng.timing(False)
+    ms, cnt = eng.timing_get("ct_scale")
+    avg = ms / max(cnt, 1)
+    ne_a = float(A.e_cnt[:n].sum().item())
+    alg = 32.0 * ne_a + 16.0 * n
+    res["scale"] = {"avg_kernel_ms": avg, "ops_per_s": n / (avg / 1000.0) if avg > 0 else None,
+                    "achieved_GBs": alg / (avg / 1000.0) / 1e9 if avg > 0 else None,
+                    "frac_of_hbm_peak": alg / (avg / 1000.0) / 1e9 / HBM_PEAK_GBS if avg > 0 else None}
     del A, B
     torch.cuda.empty_cache()
     return res

@@ -197,12 +197,14 @@ __global__ void k_batch_digest(pvac_ct_batch X, uint64_t* out) {
     out[i] = h;
 }
 
+// ct_scale (arithmetic.hpp:33-37), in place: 32 lanes per cipher, eight ciphers per workgroup
+// (fresh ciphers have ~40 edges; a workgroup per cipher left most lanes idle)
 __global__ __launch_bounds__(256) void k_ct_scale(pvac_ct_batch X, uint64_t slo, uint64_t shi) {
-    const uint64_t c = blockIdx.x;
+    const uint64_t c = (uint64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
     if (c >= X.n) return;
     const uint64_t o = X.e_off[c], n = X.e_cnt[c];
     const fp s{slo, shi};
-    for (uint64_t e = threadIdx.x; e < n; e += 256) {
+    for (uint64_t e = threadIdx.x & 31u; e < n; e += 32) {
         const fp r = fp_mul(fp{X.w_lo[o + e], X.w_hi[o + e]}, s);
         X.w_lo[o + e] = r.lo;
         X.w_hi[o + e] = r.hi;
@@ -260,7 +262,7 @@ hipError_t launch_batch_digest(const pvac_ct_batch& X, uint64_t* out, hipStream_
 
 hipError_t launch_ct_scale(const pvac_ct_batch& X, uint64_t slo, uint64_t shi, hipStream_t st) {
     if (!X.n) return hipSuccess;
-    hipLaunchKernelGGL(k_ct_scale, dim3((unsigned)X.n), dim3(256), 0, st, X, slo, shi);
+    hipLaunchKernelGGL(k_ct_scale, dim3((unsigned)((X.n + 7) / 8)), dim3(256), 0, st, X, slo, shi);
     return hipGetLastError();
 }
 
