@@ -650,6 +650,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         for (int k = 0; k < KI; ++k)
             if (kt[k] != kTInf && tb[k] == kt[k]) *G_at(tb[k]) = (uint16_t)cE[k];
         if (wave == 0) {
+            __builtin_amdgcn_s_setprio(3);   // the closure holds up the barrier below
             const uint64_t all = Lc >= 64 ? ~0ull : ((1ull << Lc) - 1ull);
             uint64_t used_lp = 0;
 #pragma unroll
@@ -671,6 +672,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 *(uint64_t*)(misc + MF_KEEP) = keep;
                 misc[MF_IDENT] = keep == all;
             }
+            __builtin_amdgcn_s_setprio(0);
         }
         __syncthreads();
         gq = launder(gq);
@@ -684,6 +686,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         //      other waves stage the next pair: a_w/a_inf/b_w/b_inf were last read in S1 and pm in
         //      the S2c closure, and the prefetched loads have had S2a and S2c to land.
         if (wave == NW - 1) {
+            __builtin_amdgcn_s_setprio(3);   // the scan is the phase's critical path
             const uint32_t c8 = (n + 511u) / 512u;   // b128 chunks (8 times) per lane
             uint4* gv = (uint4*)X4;
             const uint32_t q0 = (63u - (uint32_t)lane) * c8;
@@ -713,6 +716,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 gv[q0 + q] = make_uint4(w[0], w[1], w[2], w[3]);
             }
             if (lane == 63) misc[MF_TOTAL] = run;   // lane 63 owns t = 0: its running sum is the total
+            __builtin_amdgcn_s_setprio(0);
         }
         stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
         __syncthreads();
