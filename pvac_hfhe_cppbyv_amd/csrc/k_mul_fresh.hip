@@ -534,6 +534,9 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(1);
+        // S2a..S4 are chains of short dependent steps; S1 (products) and S5 (stores) are bulk work:
+        // the workgroup in its ordering phases is served first by the arbiter of a shared SIMD
+        __builtin_amdgcn_s_setprio(1);
         // next pair's header (from the control wave) and raw inputs: the data loads stay in
         // flight until stage_pair in S3
         const fresh_hdr nxt = hdr_next(gq, misc[MF_HDR + (lane & 15)], qn, n_pairs);
@@ -672,7 +675,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 *(uint64_t*)(misc + MF_KEEP) = keep;
                 misc[MF_IDENT] = keep == all;
             }
-            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(1);
         }
         __syncthreads();
         gq = launder(gq);
@@ -716,7 +719,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
                 gv[q0 + q] = make_uint4(w[0], w[1], w[2], w[3]);
             }
             if (lane == 63) misc[MF_TOTAL] = run;   // lane 63 owns t = 0: its running sum is the total
-            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(1);
         }
         stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
         __syncthreads();
@@ -815,6 +818,7 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
         __syncthreads();
         gq = launder(gq);
         PHASE_STAMP(6);
+        __builtin_amdgcn_s_setprio(0);
 
         // ---- S5 (reference order): coalesced writer over emit positions; clears what it read
         if (gather) {
