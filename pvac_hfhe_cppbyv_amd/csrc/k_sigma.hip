@@ -359,6 +359,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // Copy 3 reaches into the column list, so both column ids are read first.
             const bool fast = split && a.full && a.x_col_wt <= 128u && per_wave >= 1072u;
             if (fast) {
+                __builtin_amdgcn_s_setprio(1);   // LDS-atomic phase ahead of other waves' SHA-256
                 const uint32_t c0 = (uint32_t)lane < a.x_col_wt ? cols[lane] : 0u;
                 const uint32_t c1 = (uint32_t)lane + 64u < a.x_col_wt ? cols[lane + 64] : 0u;
                 __builtin_amdgcn_wave_barrier();
@@ -398,6 +399,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                                                              (uint64_t)v.z | ((uint64_t)v.w << 32));
                 }
                 for (uint32_t w = lane; w < 1072u; w += 64) sig[w] = 0;
+                __builtin_amdgcn_s_setprio(0);
                 continue;
             }
             if (split) {
