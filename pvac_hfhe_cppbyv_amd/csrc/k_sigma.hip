@@ -303,6 +303,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // step 0: pass 0; step 1: counter 32 alone (precomputed above, lanes 0 and 32); step
             // s >= 2: pass s - 1, whose counter-32 block was consumed by step 1 (draw order kept)
             const uint32_t jl = (uint32_t)jb;
+            __builtin_amdgcn_s_setprio(1);   // selection (SHA-256 + bitmap) above the next edge's midstates
             for (uint32_t step = 0; step < kMaxPasses; ++step) {   // bounded: never hang the GPU
                 uint32_t val[4];
                 if (step == 1) {   // wave-uniform
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // Copy 3 reaches into the column list, so both column ids are read first.
             const bool fast = split && a.full && a.x_col_wt <= 128u && per_wave >= 1072u;
             if (fast) {
-                __builtin_amdgcn_s_setprio(1);   // LDS-atomic phase ahead of other waves' SHA-256
+                __builtin_amdgcn_s_setprio(2);   // LDS-atomic phase ahead of other waves' SHA-256
                 const uint32_t c0 = (uint32_t)lane < a.x_col_wt ? cols[lane] : 0u;
                 const uint32_t c1 = (uint32_t)lane + 64u < a.x_col_wt ? cols[lane + 64] : 0u;
                 __builtin_amdgcn_wave_barrier();
