@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--chain-inputs", type=int, default=1 << 16, help="cfg 4 chain inputs (enc_value outputs)")
     ap.add_argument("--chain-chunk", type=int, default=1 << 10)
     ap.add_argument("--chain-depth", type=int, default=8)
+    ap.add_argument("--chain-streams", type=int, default=1,
+                    help="host threads / HIP streams running chunks (2 measured no faster: the products kernel is VALU-bound)")
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
     ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc", "add"], default=None,
                     help="run one side measurement alone (profiling) and print its JSON")
@@ -519,60 +521,94 @@ def _ref_enc_baseline():
 
 
 def chain_bench(eng, args):
-    """cfg 4 (SURVEY 8(d) restatement of test_depth): x_i = enc_value(v_i) on the GPU, c_0 = x_i,
-    c_k = ct_mul(c_{k-1}, x_i) to depth 8, over 2^16 inputs in chunks; every ct_mul step is
-    plan + exec on the general path. Reports the chain alone and enc_value + chain."""
+    """cfg 4 (SURVEY 8(d) restatement of test_depth): x_i = enc_value(v_i) on the GPU for all 2^16
+    inputs (timed on its own), then c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) to depth 8 in chunks.
+    Every ct_mul step is plan + exec on the general path. Chunks are dealt to `--chain-streams`
+    host threads, each with its own engine context on its own HIP stream, so one chunk's
+    VALU-bound products overlap another chunk's atomic / memory-bound ordering kernels."""
+    import threading
     import torch
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine
     dev = eng.device
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
+    S = max(1, args.chain_streams)
     _enc_keys(eng)
-    step_ms = [0.0] * depth
-    step_edges = [0.0] * depth
-    last_ms = []   # deepest step per chunk
-    products = 0.0
-    enc_s = 0.0
-    in_edges = 0.0
-    bad = 0
-    vals = torch.empty(chunk, dtype=torch.int64, device=dev)
-    rnd = torch.empty(chunk * ENC_STRIDE, dtype=torch.int64, device=dev)
+    vals = torch.empty(n, dtype=torch.int64, device=dev)
+    rnd = torch.empty(n * ENC_STRIDE, dtype=torch.int64, device=dev)
+    eng.fill_random(vals, 0x5EED0004)
+    eng.fill_random(rnd, 0x5EED1004)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for c0 in range(0, n, chunk):
-        k = min(chunk, n - c0)
-        ts = time.perf_counter()
-        eng.fill_random(vals[:k], 0x5EED0004 + c0)
-        eng.fill_random(rnd[:k * ENC_STRIDE], 0x5EED1004 + c0)
-        X, st = eng.enc_value(vals[:k], rnd[:k * ENC_STRIDE])   # status read back = synchronised
-        enc_s += time.perf_counter() - ts
-        bad += int((st != 0).sum())
-        in_edges += float(X.e_cnt[:k].sum().item())
-        cur = X
-        for d in range(depth):
-            ts = time.perf_counter()
-            Cb, plan = eng.ct_mul_plan(cur, X)
-            nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=dev)
-            eng.fill_random(nonces, 0x5EED0040 + 97 * c0 + d)
-            out = eng.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
-            torch.cuda.synchronize(dev)
-            step_ms[d] += 1000.0 * (time.perf_counter() - ts)
-            if d == depth - 1:
-                last_ms.append(round(1000.0 * (time.perf_counter() - ts), 1))
-            products += float((cur.e_cnt[:k].to(torch.float64) * X.e_cnt[:k].to(torch.float64)).sum().item())
-            step_edges[d] += float(out.e_cnt[:k].sum().item())
-            del Cb, nonces, plan
-            cur = out
-        # no empty_cache() here: chunks reuse torch's cached blocks (the driver clears freshly
-        # mapped VRAM, so re-allocating ~10 GB per chunk stalled single steps for seconds)
-        del cur, X, out
-    el = time.perf_counter() - t0
-    chain_s = sum(step_ms) / 1000.0
-    return {"inputs": n, "depth": depth, "chunk": chunk, "producer": "GPU enc_value (weights-only)",
-            "seconds": el, "enc_seconds": enc_s, "chain_seconds": chain_s,
-            "chains_per_s": n / el, "ct_mul_per_s": n * depth / chain_s, "ct_mul_per_s_incl_enc": n * depth / el,
-            "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
-            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
-            "edges_per_input_by_step": [e / n for e in step_edges], "ms_by_step": step_ms,
-            "last_step_ms_by_chunk": last_ms}
+    X_all, st = eng.enc_value(vals, rnd)   # status read back = synchronised
+    enc_s = time.perf_counter() - t0
+    del rnd
+    bad = int((st != 0).sum())
+    in_edges = float(X_all.e_cnt[:n].sum().item())
+
+    def view(c0, k):   # chunk of the producer's batch (offsets are absolute: no copy)
+        return DeviceBatch(k, X_all.l_off[c0:c0 + k], X_all.l_cnt[c0:c0 + k], X_all.layers, X_all.e_off[c0:c0 + k],
+                           X_all.e_cnt[c0:c0 + k], X_all.meta, X_all.w_lo, X_all.w_hi)
+
+    results = [dict(step_ms=[0.0] * depth, step_edges=[0.0] * depth, products=0.0, last_ms=[]) for _ in range(S)]
+
+    def worker(w):
+        r = results[w]
+        try:
+            stream = torch.cuda.Stream(dev)
+            with torch.cuda.device(dev), torch.cuda.stream(stream):
+                e2 = Engine(device=dev.index, canon_tag=eng.params.canon_tag)   # binds to `stream`
+                for c0 in range(w * chunk, n, S * chunk):
+                    k = min(chunk, n - c0)
+                    X = view(c0, k)
+                    cur = X
+                    for d in range(depth):
+                        ts = time.perf_counter()
+                        Cb, plan = e2.ct_mul_plan(cur, X)
+                        nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=dev)
+                        e2.fill_random(nonces, 0x5EED0040 + 97 * c0 + d)
+                        out = e2.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
+                        stream.synchronize()
+                        r["step_ms"][d] += 1000.0 * (time.perf_counter() - ts)
+                        if d == depth - 1:
+                            r["last_ms"].append(round(1000.0 * (time.perf_counter() - ts), 1))
+                        r["products"] += float((cur.e_cnt[:k].to(torch.float64) *
+                                                X.e_cnt[:k].to(torch.float64)).sum().item())
+                        r["step_edges"][d] += float(out.e_cnt[:k].sum().item())
+                        del Cb, nonces, plan
+                        cur = out
+                    # chunks reuse this stream's cached blocks (re-allocating ~10 GB per chunk made
+                    # the driver clear fresh VRAM and stalled single steps for seconds)
+                    del cur, X, out
+                stream.synchronize()
+                del e2
+        except Exception as ex:   # reported, never hidden
+            r["error"] = repr(ex)
+
+    threads = [threading.Thread(target=worker, args=(w,)) for w in range(S)]
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize(dev)
+    chain_s = time.perf_counter() - t1
+    del X_all, vals
+    errors = [r["error"] for r in results if "error" in r]
+    step_ms = [sum(r["step_ms"][d] for r in results) for d in range(depth)]
+    step_edges = [sum(r["step_edges"][d] for r in results) for d in range(depth)]
+    products = sum(r["products"] for r in results)
+    out = {"inputs": n, "depth": depth, "chunk": chunk, "streams": S, "producer": "GPU enc_value (weights-only)",
+           "seconds": enc_s + chain_s, "enc_seconds": enc_s, "chain_seconds": chain_s,
+           "chains_per_s": n / (enc_s + chain_s), "ct_mul_per_s": n * depth / chain_s,
+           "ct_mul_per_s_incl_enc": n * depth / (enc_s + chain_s),
+           "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
+           "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
+           "edges_per_input_by_step": [e / n for e in step_edges],
+           "stream_ms_by_step": step_ms, "last_step_ms_by_chunk": [r["last_ms"] for r in results]}
+    if errors:
+        out["errors"] = errors
+    return out
 
 
 def _ref_full_baseline():
