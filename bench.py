@@ -550,13 +550,32 @@ def chain_bench(eng, args):
                            X_all.e_cnt[c0:c0 + k], X_all.meta, X_all.w_lo, X_all.w_hi)
 
     results = [dict(step_ms=[0.0] * depth, step_edges=[0.0] * depth, products=0.0, last_ms=[]) for _ in range(S)]
+    ready = threading.Barrier(S + 1)
+
+    def warm(e2, stream):
+        # one untimed chunk through every depth: sizes the context's scratch arena and this
+        # stream's cached blocks (a first allocation of tens of GB waits for the driver to clear
+        # the VRAM, ~1.5 s, once)
+        k = min(chunk, n)
+        X = view(0, k)
+        cur = X
+        for d in range(depth):
+            Cb, plan = e2.ct_mul_plan(cur, X)
+            nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=dev)
+            e2.fill_random(nonces, 0x5EED0F40 + d)
+            cur = e2.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
+        stream.synchronize()
 
     def worker(w):
         r = results[w]
+        released = False
         try:
             stream = torch.cuda.Stream(dev)
             with torch.cuda.device(dev), torch.cuda.stream(stream):
                 e2 = Engine(device=dev.index, canon_tag=eng.params.canon_tag)   # binds to `stream`
+                warm(e2, stream)
+                ready.wait()
+                released = True
                 for c0 in range(w * chunk, n, S * chunk):
                     k = min(chunk, n - c0)
                     X = view(c0, k)
@@ -583,12 +602,17 @@ def chain_bench(eng, args):
                 del e2
         except Exception as ex:   # reported, never hidden
             r["error"] = repr(ex)
+            if not released:
+                ready.abort()
 
     threads = [threading.Thread(target=worker, args=(w,)) for w in range(S)]
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
     for t in threads:
         t.start()
+    try:
+        ready.wait()   # every worker warmed up
+    except threading.BrokenBarrierError:
+        pass
+    t1 = time.perf_counter()
     for t in threads:
         t.join()
     torch.cuda.synchronize(dev)
