@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--epl", type=int, default=20, help="edges per BASE layer")
     ap.add_argument("--cpu-pairs", type=int, default=1 << 17)
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--cpu-share-threads", type=int, default=16, help="second CPU baseline: the box's CPU share")
     ap.add_argument("--sigma-pairs", type=int, default=1 << 12)
     ap.add_argument("--chain-inputs", type=int, default=1 << 16, help="cfg 4 chain inputs (enc_value outputs)")
     ap.add_argument("--chain-chunk", type=int, default=1 << 10)
@@ -262,7 +263,12 @@ def cpu_baseline(eng, A, B, out, n, args):
                                           P(counts), P(digests))
     gpu_dig = u(eng.digest(out)[:k])
     gpu_cnt = u(out.e_cnt[:k])
+    # the same port on the GPU box's CPU share (16 threads, independent pairs), for scale
+    mt = max(1, args.cpu_share_threads)
+    secs_mt = orc.lib.orc_ct_mul_batch_timed(C.byref(prm), k, P(al), P(a_lay), P(ae), P(am), P(awl), P(awh),
+                                             P(bl), P(b_lay), P(be), P(bm), P(bwl), P(bwh), mt, P(counts), P(digests))
     return {
+        "multi_thread": {"value": k / secs_mt, "cores": mt, "seconds": secs_mt},
         "value": k / secs,
         "unit": "ct_mul/s",
         "cores": args.cpu_threads,
