@@ -341,6 +341,7 @@ __global__ __launch_bounds__(kAddBlock) void k_ct_add(pvac_ct_batch A, pvac_ct_b
 // LDS table for the edges' lookups. k_ct_add's one workgroup per pair spent six barriers on ~80
 // edges and ran at 14% of the HBM roofline.
 constexpr int kAddWaves = 4;
+constexpr int kPre = 3;   // edges per lane held in registers by k_ct_add_wave (fresh pairs: all)
 
 template <int G>
 __device__ __forceinline__ uint64_t group_or_u64(uint64_t v) {
@@ -366,21 +367,40 @@ __global__ __launch_bounds__(64 * kAddWaves) void k_ct_add_wave(pvac_ct_batch A,
     const uint64_t alo = live ? A.l_off[pr] : 0ull, blo = live ? B.l_off[pr] : 0ull;
     const uint64_t aeo = live ? A.e_off[pr] : 0ull, beo = live ? B.e_off[pr] : 0ull;
     const uint64_t clo = live ? C.l_off[pr] : 0ull, ceo = live ? C.e_off[pr] : 0ull;
+    // The group's first kPre*G edges (every fresh pair: 80 edges) are loaded once, up front, with
+    // the layer record below in flight beside them: they feed both the used-layer mask and the
+    // output, so the pair pays one dependent memory round trip for its edges instead of two.
+    const uint64_t nE = nA + nB;
+    uint64_t pm[kPre], pwl[kPre], pwh[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const uint64_t e = gl + (uint64_t)u * G;
+        const bool fromB = e >= nA;
+        const uint64_t src = fromB ? beo + (e - nA) : aeo + e;
+        const uint64_t* mp = fromB ? B.meta : A.meta;
+        const uint64_t* lp = fromB ? B.w_lo : A.w_lo;
+        const uint64_t* hp = fromB ? B.w_hi : A.w_hi;
+        pm[u] = 0; pwl[u] = 0; pwh[u] = 0;
+        if (e < nE) { pm[u] = mp[src]; pwl[u] = lp[src]; pwh[u] = hp[src]; }
+    }
+    const uint32_t l = gl;
+    pvac_layer x{};
+    if (l < L) x = l < LA ? A.layers[alo + l] : B.layers[blo + (l - LA)];
     // layers used by edges (encrypt.hpp:78)
     uint64_t used = 0;
-    for (uint64_t e = gl; e < nA; e += G) {
-        const uint32_t lid = meta_layer(A.meta[aeo + e]);
-        used |= lid < L ? 1ull << lid : 0ull;
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const uint64_t e = gl + (uint64_t)u * G;
+        const uint32_t lid = meta_layer(pm[u]) + (e >= nA ? LA : 0u);
+        used |= (e < nE && lid < L) ? 1ull << lid : 0ull;
     }
-    for (uint64_t e = gl; e < nB; e += G) {
-        const uint32_t lid = meta_layer(B.meta[beo + e]) + LA;
+    for (uint64_t e = gl + (uint64_t)kPre * G; e < nE; e += G) {
+        const bool fromB = e >= nA;
+        const uint32_t lid = fromB ? meta_layer(B.meta[beo + (e - nA)]) + LA : meta_layer(A.meta[aeo + e]);
         used |= lid < L ? 1ull << lid : 0ull;
     }
     used = group_or_u64<G>(used);
     // transitive PROD parents (encrypt.hpp:80-93)
-    const uint32_t l = gl;
-    pvac_layer x{};
-    if (l < L) x = l < LA ? A.layers[alo + l] : B.layers[blo + (l - LA)];
     const uint32_t off = l < LA ? 0u : LA;
     const uint32_t pa = x.pa + off, pb = x.pb + off;
     const uint64_t mypm = (l < L && x.rule == 1) ? ((pa < L ? 1ull << pa : 0ull) | (pb < L ? 1ull << pb : 0ull)) : 0ull;
@@ -412,12 +432,8 @@ __global__ __launch_bounds__(64 * kAddWaves) void k_ct_add_wave(pvac_ct_batch A,
     }
     // edges (concat; B shifted and optionally scaled by p-1)
     const fp pm1{kAll - 1, kM63};
-    for (uint64_t e = gl; e < nA + nB; e += G) {
+    auto emit = [&](uint64_t e, uint64_t m, uint64_t wl, uint64_t wh) {
         const bool fromB = e >= nA;
-        const uint64_t src = fromB ? beo + (e - nA) : aeo + e;
-        uint64_t m = fromB ? B.meta[src] : A.meta[src];
-        uint64_t wl = fromB ? B.w_lo[src] : A.w_lo[src];
-        uint64_t wh = fromB ? B.w_hi[src] : A.w_hi[src];
         uint32_t lid = meta_layer(m) + (fromB ? LA : 0u);
         if (!identity) lid = lid < L ? remap[lid] : 0xFFFFFFFFu;
         m = (m & ~0xFFFFFFFFull) | lid;
@@ -428,6 +444,17 @@ __global__ __launch_bounds__(64 * kAddWaves) void k_ct_add_wave(pvac_ct_batch A,
         C.meta[ceo + e] = m;
         C.w_lo[ceo + e] = wl;
         C.w_hi[ceo + e] = wh;
+    };
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const uint64_t e = gl + (uint64_t)u * G;
+        if (e < nE) emit(e, pm[u], pwl[u], pwh[u]);
+    }
+    for (uint64_t e = gl + (uint64_t)kPre * G; e < nE; e += G) {
+        const bool fromB = e >= nA;
+        const uint64_t src = fromB ? beo + (e - nA) : aeo + e;
+        emit(e, fromB ? B.meta[src] : A.meta[src], fromB ? B.w_lo[src] : A.w_lo[src],
+             fromB ? B.w_hi[src] : A.w_hi[src]);
     }
     if (C.sigma && A.sigma && B.sigma) {   // sigma carry: 16 bytes per lane
         const uint32_t sw = C.sigma_words;
