@@ -204,7 +204,27 @@ __global__ __launch_bounds__(256) void k_ct_scale(pvac_ct_batch X, uint64_t slo,
     if (c >= X.n) return;
     const uint64_t o = X.e_off[c], n = X.e_cnt[c];
     const fp s{slo, shi};
-    for (uint64_t e = threadIdx.x & 31u; e < n; e += 32) {
+    // the first 64 weights (every fresh cipher: 40) are all loaded before the first store: the
+    // update is in place, so loads issued after a store could not be hoisted above it
+    constexpr int kPre = 2;
+    const uint64_t e0 = threadIdx.x & 31u;
+    fp w[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const uint64_t e = e0 + 32u * u;
+        w[u] = fp{0, 0};
+        if (e < n) w[u] = fp{X.w_lo[o + e], X.w_hi[o + e]};
+    }
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const uint64_t e = e0 + 32u * u;
+        if (e < n) {
+            const fp r = fp_mul(w[u], s);
+            X.w_lo[o + e] = r.lo;
+            X.w_hi[o + e] = r.hi;
+        }
+    }
+    for (uint64_t e = e0 + 32u * kPre; e < n; e += 32) {
         const fp r = fp_mul(fp{X.w_lo[o + e], X.w_hi[o + e]}, s);
         X.w_lo[o + e] = r.lo;
         X.w_hi[o + e] = r.hi;

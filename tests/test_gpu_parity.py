@@ -341,3 +341,23 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     Cb2, plan2 = eng.ct_mul_plan(A, B)
     out2 = eng.ct_mul(A, B, nonces=nonces, C_=Cb2, plan=plan2)
     assert np.array_equal(u(eng.digest(out2)[:n]), dig1)
+
+
+@pytest.mark.parametrize("s", [2, P - 1, (0x0123456789ABCDEF << 64) | 0xFEDCBA9876543210])
+def test_ct_scale_ragged(engine, oracle, s):
+    """ct_scale (ops/arithmetic.hpp:33-37) in place, per-edge fp_mul by s, on ciphers whose edge
+    counts straddle k_ct_scale's register-held first 64 weights (0, 1, 31..33, 63..65, 97, a
+    fresh cipher and the full chain-step-3 cipher); layers and edge metadata pass through."""
+    chain = read_ct(os.path.join(REF, "chain3.ct"))[0]
+    fresh = read_ct(os.path.join(REF, "pair0_x.ct"))[0]
+    cs = [Cipher(chain.layers, chain.meta[:k], chain.w_lo[:k], chain.w_hi[:k]) for k in (0, 1, 31, 32, 33, 63, 64, 65, 97)]
+    cs += [fresh, chain]
+    X = _dev_batch(engine, cs)
+    engine.ct_scale(X, s)
+    out = X.to_host()
+    s_lo, s_hi = np.uint64(s & ((1 << 64) - 1)), np.uint64(s >> 64)
+    for c, o in zip(cs, out):
+        n = len(c.w_lo)
+        want_lo, want_hi = oracle.fp("mul", c.w_lo, c.w_hi, np.full(n, s_lo, np.uint64), np.full(n, s_hi, np.uint64))
+        assert np.array_equal(o.w_lo, want_lo) and np.array_equal(o.w_hi, want_hi)
+        assert np.array_equal(o.meta, c.meta) and o.layers.tobytes() == c.layers.tobytes()
