@@ -46,6 +46,13 @@ __device__ __forceinline__ void block_reduce_stats(uint32_t (&v)[N], const bool 
             }
 }
 
+// atomicMax only when the block's value beats what is already there: the maxima of a uniform
+// batch are reached by the first blocks, so the rest issue no atomic (thousands of same-address
+// atomics serialise at one L2 channel). Skipping is exact: the stored maximum never decreases.
+__device__ __forceinline__ void max_if_greater(unsigned int* p, uint32_t v) {
+    if (v > __atomic_load_n(p, __ATOMIC_RELAXED)) atomicMax(p, v);
+}
+
 inline unsigned plan_grid(uint64_t n) {
     const uint64_t b = (n + kPlanBlock - 1) / kPlanBlock;
     return (unsigned)(b < 2048 ? b : 2048);
@@ -84,13 +91,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
     const bool is_sum[7] = {true, false, false, false, false, false, false};
     block_reduce_stats<7>(v, is_sum, red);
     if (threadIdx.x == 0) {
-        if (v[0]) atomicAdd(&stats->n_small, (unsigned long long)v[0]);
-        if (v[1]) atomicMax(&stats->max_keys, v[1]);
-        if (v[2]) atomicMax(&stats->max_prod, v[2]);
-        if (v[3]) atomicMax(&stats->max_na, v[3]);
-        if (v[4]) atomicMax(&stats->max_nb, v[4]);
-        if (v[5]) atomicMax(&stats->max_buckets, v[5]);
-        if (v[6]) atomicMax(&stats->max_layers, v[6]);
+        // n_small = n - n_large on the host: no per-block count
+        max_if_greater(&stats->max_keys, v[1]);
+        max_if_greater(&stats->max_prod, v[2]);
+        max_if_greater(&stats->max_na, v[3]);
+        max_if_greater(&stats->max_nb, v[4]);
+        max_if_greater(&stats->max_buckets, v[5]);
+        max_if_greater(&stats->max_layers, v[6]);
     }
 }
 
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_add(pvac_ct_batch A, pvac_c
     uint32_t v[1] = {ml};
     const bool is_sum[1] = {false};
     block_reduce_stats<1>(v, is_sum, red);
-    if (threadIdx.x == 0 && v[0]) atomicMax(&stats->max_layers, v[0]);
+    if (threadIdx.x == 0) max_if_greater(&stats->max_layers, v[0]);
 }
 
 // shapes and offsets of the over-budget ct_add pairs: {pair, LA, LB, nA, nB, aeo, beo, ceo}

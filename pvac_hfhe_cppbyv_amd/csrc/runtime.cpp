@@ -502,7 +502,7 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_plan");
     plan->total_layer_slots = tot[0];
     plan->total_edge_slots = tot[1];
-    plan->n_small = st.n_small;
+    plan->n_small = A->n - st.n_large;   // k_plan_mul classifies every pair as small or large
     plan->n_large = st.n_large;
     plan->max_keys = st.max_keys;
     plan->max_prod = st.max_prod;
