@@ -150,11 +150,15 @@ int pvac_hip_fp_binop(pvac_hip_ctx* ctx, int op, const uint64_t* a_lo, const uin
  *   salts : 1 word per OUTPUT edge slot (device, parallel to C->meta), in emit order; used only
  *           with PVAC_MUL_WITH_SIGMA (nullable otherwise).
  * Output edge order is the reference's std::unordered_map iteration order (bit-exact), unless
- * PVAC_MUL_ORDER_CANONICAL. guard_budget/compact_layers semantics are applied per pair. */
+ * PVAC_MUL_ORDER_CANONICAL. guard_budget/compact_layers semantics are applied per pair.
+ * exec synchronises the stream once at its end: a fresh-shape pair with a key sum of 0 mod p
+ * (cancelling products, zero weights) is re-run on the general path before it returns. */
 int pvac_hip_ct_mul_plan(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
                          pvac_hip_plan* plan);
 int pvac_hip_ct_mul_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pvac_ct_batch* A, const pvac_ct_batch* B,
                          const uint64_t* nonces, const uint64_t* salts, pvac_ct_batch* C, uint32_t flags);
+/* Pairs that ct_mul_exec re-ran on the general path (see above) since the context was created. */
+int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* ctx, uint64_t* out);
 
 /* ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45; combine_ciphers ops/encrypt.hpp:260-279).
  * negate_b != 0 gives ct_sub (B's weights scaled by p-1). Dense CSR output: the plan writes

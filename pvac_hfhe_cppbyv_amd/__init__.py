@@ -78,6 +78,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
                                   C.POINTER(Plan)], i32),
         "pvac_hip_ct_mul_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
                                   C.POINTER(CtBatch), u32], i32),
+        "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ct_add_plan": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch),
                                   C.POINTER(Plan)], i32),
         "pvac_hip_ct_add_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), i32,
@@ -359,6 +360,12 @@ class Engine:
         self._check(self.lib.pvac_hip_ct_mul_exec(self.ctx, C.byref(plan), C.byref(sa), C.byref(sb), p(nonces),
                                                   p(salts), C.byref(sc), flags))
         return C_
+
+    def ct_mul_redo_count(self):
+        """Fresh-shape pairs re-run on the general path because a key sum was 0 mod p."""
+        v = C.c_uint64(0)
+        self._check(self.lib.pvac_hip_ct_mul_redo_count(self.ctx, C.byref(v)))
+        return v.value
 
     def ct_add(self, A: DeviceBatch, B: DeviceBatch, negate=False, sigma=False):
         torch = self.torch

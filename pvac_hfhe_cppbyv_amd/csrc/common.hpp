@@ -148,6 +148,8 @@ struct mul_fresh_args {
     const uint32_t* nb_table;    // libstdc++ bucket count after reserve(n), n <= kFreshProdMax
     const uint64_t* nb_magic;    // fastmod64 multipliers for nb_table
     uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
+    uint64_t* redo_ids;          // pairs whose key sums cancelled to 0 mod p (re-run on the general path)
+    unsigned int* redo_cnt;      // their count (device, zeroed before the launch)
     uint64_t canon_tag;
     uint64_t edge_budget;
     uint32_t Bm;
@@ -155,6 +157,9 @@ struct mul_fresh_args {
     // launch sizing (maxima over the small pairs of the batch)
     uint32_t ks_max, prod_max, na_max, nb_max, buckets_max, layers_max;
 };
+// pair_status values of ct_mul (device array): 0 reference order, 1 canonical order, 2 rejected,
+// 3 = the fresh kernel found a key sum of 0 mod p and left the pair to the general path
+constexpr uint32_t kPairRedo = 3;
 hipError_t launch_mul_layers_fresh(const mul_fresh_args& a, hipStream_t st);
 // args_dev: device copy of `a` (the kernel reads its arguments from memory, see k_mul_fresh.hip)
 hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* args_dev, int num_cus, hipStream_t st);

@@ -220,6 +220,42 @@ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
     return fp{join32(y0, y1), join32(y2, y3)};
 }
 
+// 128-bit x -> 44/44/40-bit limbs. Up to 4096 of them sum without overflow into u64 limbs of
+// < 2^56, < 2^56 and < 2^52, so the top 12 bits of the third limb stay free (k_ct_mul_fresh keeps
+// the emit cell id there).
+__device__ __forceinline__ void fp_split3_44(uint64_t x0, uint64_t x1, uint64_t& l0, uint64_t& l1, uint64_t& l2) {
+    const uint32_t w0 = lo32(x0), w1 = hi32(x0), w2 = lo32(x1), w3 = hi32(x1);
+    l0 = join32(w0, w1 & 0xFFFu);                                 // bits 0..43
+    l1 = join32(funnel(w2, w1, 12), (w2 >> 12) & 0xFFFu);        // bits 44..87
+    l2 = join32(funnel(w3, w2, 24), w3 >> 24);                    // bits 88..127
+}
+
+// (l0 + l1 * 2^44 + l2 * 2^88) mod p, canonical, for l0, l1 < 2^56 and l2 < 2^52
+__device__ __forceinline__ fp fp_fold3_44(uint64_t l0, uint64_t l1, uint64_t l2) {
+    // V < 2^141 as five words
+    uint32_t c = 0;
+    const uint32_t v0 = lo32(l0);
+    const uint32_t v1 = addc(hi32(l0), lo32(l1) << 12, 0u, c);
+    uint32_t v2 = addc(funnel(hi32(l1), lo32(l1), 20), 0u, c, c);
+    uint32_t v3 = (hi32(l1) >> 20) + c;
+    v2 = addc(v2, lo32(l2) << 24, 0u, c);
+    v3 = addc(v3, funnel(hi32(l2), lo32(l2), 8), c, c);
+    const uint32_t v4 = (hi32(l2) >> 8) + c;
+    // x = (V mod 2^127) + (V >> 127) < 2^127 + 2^14
+    const uint32_t top = funnel(v4, v3, 31);
+    uint32_t x0 = addc(v0, top, 0u, c);
+    uint32_t x1 = addc(v1, 0u, c, c);
+    uint32_t x2 = addc(v2, 0u, c, c);
+    uint32_t x3 = (v3 & 0x7FFFFFFFu) + c;
+    // x >= 2^127 -> (x - 2^127) + 1 (< 2^14: no carry); x == p -> 0
+    const uint32_t t = x3 >> 31;
+    x3 &= 0x7FFFFFFFu;
+    x0 += t;
+    const uint32_t keep = ((x3 == 0x7FFFFFFFu) & ((x0 & x1 & x2) == 0xFFFFFFFFu)) ? 0u : ~0u;
+    x0 &= keep; x1 &= keep; x2 &= keep; x3 &= keep;
+    return fp{join32(x0, x1), join32(x2, x3)};
+}
+
 // ---- lazy register accumulators ---------------------------------------------------------
 // Sum of lazy products x < 2^128 (fp_mul_fold1 of canonical operands) as 128 bits + a carry
 // count: up to 2^32 addends, 5 VALU ops per add. acc_fold returns the canonical residue, equal to

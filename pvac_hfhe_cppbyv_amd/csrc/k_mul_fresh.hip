@@ -23,6 +23,10 @@
 //                        independent, no overflow below 2^21 addends). compact_layers is a
 //                        wave-wide bitmask closure over LDS-resident parent masks; edges are
 //                        staged in LDS at their emit positions and written out coalesced.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.hpp"
 #include "sha256.hpp"
 
@@ -30,6 +34,13 @@ namespace pvhip {
 
 // Diagnostic build only (make diag -> lib/libpvac_hip_diag.so): wave 0 of every workgroup
 // accumulates s_memtime deltas per phase into a debug array; never touches kernel outputs.
+#ifdef PVAC_CENSUS   // diagnostic build only: per-workgroup start / end s_memrealtime (100 MHz) + pairs done
+__device__ unsigned long long g_census[4096 * 4];
+extern "C" int pvac_hip_diag_census(unsigned long long* host, size_t n) {
+    if (n > sizeof(g_census) / 8) n = sizeof(g_census) / 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_census), n * 8) == hipSuccess ? 0 : -5;
+}
+#endif
 #ifdef PVAC_PHASE_STAMPS
 constexpr int kStampPhases = 18;
 __device__ unsigned long long g_fresh_stamps[4096 * kStampPhases];
@@ -861,6 +872,657 @@ __global__ __launch_bounds__(BS, MINW) void k_ct_mul_fresh(const mul_fresh_args*
 #endif
 }
 
+// ================================================================ k_ct_mul_fresh3
+// Positions before products. Three workgroups per CU (<= 53 KB LDS, <= 80 VGPRs):
+//   P1 key times : every product t = i|B.E| + j lands in cell 2 s + ch (s = key slot, ch = P/M);
+//                  one ds_min_u32 per product gives each cell's first-insert time (no multiply)
+//   P2 order     : slot owners read their two cells and the cells of their bucket's other slots:
+//                  key time, bucket first-insert time, rank in the bucket, bucket edge count
+//                  G[t_bkt]. A cell with products is assumed to emit (its sum is != 0).
+//                  Slots are dealt to threads sorted by the size of their bucket (static per
+//                  bucket count), so a wave loops only over as many bucket mates as it needs.
+//   P3 scan      : every wave suffix-scans one 256-time segment of G; wave 0 then runs
+//                  compact_layers
+//   P4 positions : each emitting cell gets its hash-order emit position p (segment offset added
+//                  from the segment totals); p goes into the cell word, the cell id into limb 2 of p
+//   P5 products  : fp_mul of every product, 44/44/40-bit limbs added into position p's
+//                  accumulators (3 ds_add_u64)
+//   P6 writer    : positions p = tid, tid + 448, ... fold their limbs (coalesced LDS reads), write
+//                  the edge records coalesced, clear. A folded sum of 0 (a cancelling key, or a
+//                  zero weight) means the optimistic emit in P2 was wrong, and guard_budget /
+//                  ORDER_CANONICAL want another order: such pairs are flagged (pair_status 3,
+//                  redo list) and the host re-runs them on the general path.
+// LDS word of cell c (tkey[c], u32): low half = first-insert time (0xFFFF none), then the emit
+// position; high half, indexed by product time t instead: G[t], then its in-segment suffix offset.
+// misc words of k_ct_mul_fresh3 (F3_INVALID is stage_pair's MF_INVALID)
+enum : int { F3_PART = 0 /* 16 scan segment totals / block-scan partials */, F3_INVALID = MF_INVALID,
+             F3_BIGOVF = 17, F3_IDENT = 18, F3_ZERO = 19, F3_KEEP = 20 /* u64 */,
+             F3_CLS = 24 /* 8 class counters while rebuilding */, F3_WAVELP = 24 /* 8 x u64 */,
+             F3_HDR = 40 /* 16: next pair's header record */, F3_WORDS = 56 };
+static_assert(F3_INVALID == 16, "stage_pair flags misc[F3_INVALID]");
+constexpr uint32_t kBigCap = 256;   // LDS entries for the slots of buckets with more than 4 slots
+
+struct fresh3_layout {
+    uint32_t tkey, lim, members, a_w, a_inf, b_w, b_inf, pm, remap, misc, total;
+    uint32_t tk_words, pmax, boff;
+};
+
+__host__ __device__ inline fresh3_layout fresh3_lds(uint32_t ks, uint32_t prod, uint32_t na, uint32_t nb, uint32_t nbk,
+                                                   uint32_t nl) {
+    fresh3_layout L;
+    uint32_t o = 0;
+    const uint32_t cells = 2u * ks;
+    L.tk_words = ((cells + 2u > prod ? cells + 2u : prod) + 3u) & ~3u;   // b128 scan chunks; a dummy slot
+    L.pmax = ((prod < cells ? prod : cells) + 1u) & ~1u;
+    L.tkey = o;    o = align16(o + L.tk_words * 4u);
+    L.lim = o;     o = align16(o + L.pmax * 24u);   // 3 u64 limbs per emit position, interleaved
+    L.members = o; o = align16(o + kBigCap * 2u);   // slots of buckets with more than 4 slots
+    L.a_w = o;     o = align16(o + na * 16u);
+    L.a_inf = o;   o = align16(o + na * 4u);
+    L.b_w = o;     o = align16(o + nb * 16u);
+    L.b_inf = o;   o = align16(o + nb * 4u);
+    L.pm = o;      o = align16(o + nl * 8u);   // parent masks and remap of C's layers (nl <= 64)
+    L.remap = o;   o = align16(o + nl * 4u);
+    L.misc = o;    o = align16(o + F3_WORDS * 4u);
+    // bucket-group rebuild scratch: nbk u32 CSR offsets, 2 ks u32 slot records, ks u16 CSR
+    // members; in the limb arrays when they fit (zero between pairs, zeroed again after a
+    // rebuild), else at the end
+    const uint32_t scratch = (nbk + 2u * ks) * 4u + ks * 2u;
+    if (scratch <= L.pmax * 24u) {
+        L.boff = L.lim;
+    } else {
+        L.boff = o;
+        o = align16(o + scratch);
+    }
+    L.total = o;
+    return L;
+}
+
+#ifndef PVAC_U5
+#define PVAC_U5 2
+#endif
+
+#ifdef PVAC_PHASE_STAMPS
+#define STAMP3(ph)                                                        \
+    do {                                                                  \
+        if (threadIdx.x == 0) {                                           \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+            st3_acc[ph] += now_ - st3_last;                               \
+            st3_last = now_;                                              \
+        }                                                                 \
+    } while (0)
+#define STAMP3_SYNC(ph)                                    \
+    do {                                                   \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        STAMP3(ph);                                        \
+    } while (0)
+#else
+#define STAMP3(ph) do {} while (0)
+#define STAMP3_SYNC(ph) do {} while (0)
+#endif
+#ifdef PVAC_ASM_MARKS
+#define M3(ph) asm volatile("; PVAC_MARK " #ph ::: "memory")
+#else
+#define M3(ph) do {} while (0)
+#endif
+
+// a value the compiler cannot see through: per-phase thread ids built from it keep per-thread LDS
+// addresses from being hoisted out of the pair loop (and spilled) at 80 VGPRs
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+template <int BS>
+__global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* __restrict__ gp, fresh3_layout Ls) {
+    constexpr int KI = (kFreshKeysMax + BS - 1) / BS;    // key slots owned per thread
+    constexpr int NW = BS / 64;
+    constexpr int U = 4;                                 // product rounds per pass
+    constexpr uint32_t kT16 = 0xFFFFu;                   // no first-insert time
+    constexpr uint32_t kBig = 7u;                        // slot record: more than 3 bucket mates
+    static_assert(BS == (int)kFreshThreads && BS >= (int)kFreshEdgesMax && NW <= 16, "fresh geometry");
+    static_assert(kFreshProdMax <= 16u * 256u, "16 scan segments of 256 product times");
+    argp gq = launder((uint64_t)gp);
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t* tkey = (uint32_t*)(lds + Ls.tkey);
+    uint16_t* tk16 = (uint16_t*)(lds + Ls.tkey);         // [2 c] = low half of cell c, [2 t + 1] = G[t]
+    const uint64_t* tk64 = (const uint64_t*)(lds + Ls.tkey);   // [s] = cells 2 s, 2 s + 1
+    unsigned long long* lim = (unsigned long long*)(lds + Ls.lim);   // [3 p + l] limb l of position p
+    uint32_t* boff = (uint32_t*)(lds + Ls.boff);
+    uint16_t* members = (uint16_t*)(lds + Ls.members);
+    ulonglong2* a_w = (ulonglong2*)(lds + Ls.a_w);
+    uint32_t* a_inf = (uint32_t*)(lds + Ls.a_inf);
+    ulonglong2* b_w = (ulonglong2*)(lds + Ls.b_w);
+    uint32_t* b_inf = (uint32_t*)(lds + Ls.b_inf);
+    uint64_t* pm = (uint64_t*)(lds + Ls.pm);
+    uint32_t* remap = (uint32_t*)(lds + Ls.remap);
+    uint32_t* misc = (uint32_t*)(lds + Ls.misc);
+    uint64_t* wave_lp = (uint64_t*)(misc + F3_WAVELP);
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t Bm = gq->Bm;
+    const uint32_t bdiv = (uint32_t)(0x100000000ull / Bm) + 1u;   // s / Bm = mulhi(s, bdiv) for s < 2^16
+    const uint32_t dummy = gq->ks_max;   // a slot whose two cell words are never set (tk_words > 2 ks_max + 1)
+    // Owned slots (static per bucket count and B): rec0 = slot | mates << 11 | m0 << 16,
+    // rec1 = m1 | m2 << 16, the other slots of its libstdc++ bucket (unused: dummy). mates = kBig:
+    // the bucket has more than 3 others; then m0 = CSR start into `members`, rec1 = their number.
+    // Slot k of a thread has rank tid + k*BS in mate-count order (descending), so lane 0 of a wave
+    // holds that wave's largest count for row k (cmax, wave-uniform).
+    uint32_t rec0[KI], rec1[KI], cmax[KI];
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+        rec0[k] = dummy | (dummy << 16);
+        rec1[k] = dummy | (dummy << 16);
+        cmax[k] = 0;
+    }
+    uint32_t nbk_c = 0, nB_c = 0, mdiv = 0;
+
+    {   // one-time clear: cell words empty, limbs zero
+        const uint32_t tid = threadIdx.x;
+        for (uint32_t w = tid; w < Ls.tk_words; w += BS) tkey[w] = kT16;
+        for (uint32_t w = tid; w < 3u * Ls.pmax; w += BS) lim[w] = 0;
+        if (tid < F3_WORDS) misc[tid] = 0;
+    }
+    __syncthreads();
+
+#ifdef PVAC_PHASE_STAMPS
+    // diagnostic build: phase times of thread 0 accumulated in LDS (registers would cost occupancy)
+    __shared__ unsigned long long st3_acc[kStampPhases];
+    if (threadIdx.x < kStampPhases) st3_acc[threadIdx.x] = 0;
+    unsigned long long st3_last = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef PVAC_CENSUS
+    const unsigned long long cen_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long cen_pairs = 0;
+#endif
+    const fresh_rec* const recs = gq->recs;
+    const uint64_t n_pairs = gq->A.n;
+    fresh_hdr cur = load_hdr(gq, next_small(gq, blockIdx.x));
+    stage_pair(prefetch_pair(gq, cur), cur, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+    __syncthreads();
+
+    while (cur.pr != kNoPair) {
+        gq = launder(gq);
+        const uint64_t qn = cur.pr + gridDim.x;
+        const uint32_t hv = wave == NW - 1 ? hdr_issue(recs, n_pairs, qn) : 0u;
+        const uint64_t pr = cur.pr;
+        const uint32_t LA = cur.LA, LB = cur.LB, nA = cur.nA, nB = cur.nB;
+        const uint32_t LP = LA * LB, KS = LP * Bm, n = nA * nB;
+        const uint32_t base = LA + LB, Lc = base + LP;
+        const uint32_t nbk = cur.nbk;
+
+        if (misc[F3_INVALID]) {   // invalid references: reject the pair (reference behaviour is UB)
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                gq->pair_status[pr] = 2;
+                gq->C.l_cnt[pr] = 0;
+                gq->C.e_cnt[pr] = 0;
+                misc[F3_INVALID] = 0;
+            }
+            if (wave == NW - 1 && lane < 16) misc[F3_HDR + lane] = hv;
+            __syncthreads();
+            const fresh_hdr nx = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs);
+            stage_pair(prefetch_pair(gq, nx), nx, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+            __syncthreads();
+            cur = nx;
+            continue;
+        }
+        if (nB != nB_c) {   // i = ((t << 8) * mdiv) >> 32, exact for t < 2^12
+            nB_c = nB;
+            mdiv = (1u << 24) / max(nB, 1u) + 1u;
+        }
+
+        // ---- static slot records for a new bucket count: bucket of every slot, the buckets as a
+        //      CSR (counting sort), each slot's mates, then the slots dealt to threads in
+        //      descending mate-count order. Scratch in the (zero) limb arrays, zeroed afterwards.
+        if (nbk != nbk_c) {
+            const uint32_t tid = opaque(threadIdx.x);
+            const uint32_t ksa = gq->ks_max;
+            uint32_t* srec = boff + nbk;   // [2 ksa]: slot records by rank
+            uint16_t* csr = (uint16_t*)(srec + 2u * ksa);   // [ksa]: slots in bucket order
+            const fastmod64 fm{nbk, cur.nb_magic};
+            uint32_t bk[KI];
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                const uint32_t lp = __umulhi(s, bdiv);
+                bk[k] = (uint32_t)fmod64((((uint64_t)lp << 32) | (s - lp * Bm)) * kGolden, fm);
+            }
+            for (uint32_t w = tid; w < nbk; w += BS) boff[w] = 0;
+            if (tid < 8) misc[F3_CLS + tid] = 0;
+            if (tid == 0) misc[F3_BIGOVF] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KI; ++k)
+                if (tid + (uint32_t)k * BS < ksa) atomicAdd(&boff[bk[k]], 1u);
+            __syncthreads();
+            {
+                const uint32_t per = (nbk + BS - 1) / BS, b0 = tid * per;
+                uint32_t local = 0;
+                for (uint32_t b = b0; b < b0 + per && b < nbk; ++b) local += boff[b];
+                uint32_t tot;
+                uint32_t run = block_exclusive_scan<BS>(local, misc + F3_PART, tot);
+                for (uint32_t b = b0; b < b0 + per && b < nbk; ++b) {
+                    const uint32_t v = boff[b];
+                    boff[b] = run;
+                    run += v;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                if (s < ksa) csr[atomicAdd(&boff[bk[k]], 1u)] = (uint16_t)s;
+            }
+            __syncthreads();   // boff[b] is now the END of bucket b's slots
+            uint32_t r0[KI], r1[KI], cls[KI], rank[KI];
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                const uint32_t b = bk[k];
+                uint32_t m[3] = {dummy, dummy, dummy}, c = 0, start = 0;
+                if (s < ksa) {
+                    const uint32_t end = boff[b];
+                    start = b ? boff[b - 1] : 0u;
+                    for (uint32_t q = start; q < end; ++q) {
+                        const uint32_t x = csr[q];
+                        if (x == s) continue;
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) m[j] = c == (uint32_t)j ? x : m[j];   // no dynamic index
+                        ++c;
+                    }
+                }
+                if (c > 3) {   // more than 3 mates: resolved through `members` below
+                    r0[k] = s | (kBig << 11) | (start << 16);
+                    r1[k] = c;
+                } else {
+                    r0[k] = s | (c << 11) | (m[0] << 16);
+                    r1[k] = m[1] | (m[2] << 16);
+                }
+                cls[k] = c > 3 ? 0u : 4u - c;   // descending mate count
+                rank[k] = s < ksa ? atomicAdd(&misc[F3_CLS + cls[k]], 1u) : 0u;
+            }
+            __syncthreads();   // every CSR end read
+            if (tid == 0) {    // class bases
+                uint32_t run = 0;
+                for (int c = 0; c < 5; ++c) {
+                    const uint32_t v = misc[F3_CLS + c];
+                    misc[F3_CLS + c] = run;
+                    run += v;
+                }
+            }
+            // a bucket of more than 4 slots: its first slot copies it into `members` and leaves the
+            // offset in boff[bucket]; past kBigCap entries the pairs of this bucket count take the
+            // general path
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                if (s < ksa && ((r0[k] >> 11) & 7u) == kBig && csr[r0[k] >> 16] == s) {
+                    const uint32_t c = r1[k], start = r0[k] >> 16;
+                    uint32_t at = atomicAdd(&misc[F3_CLS + 7], c + 1u);
+                    if (at + c + 1u <= kBigCap) {
+                        for (uint32_t q = 0; q <= c; ++q) members[at + q] = csr[start + q];
+                    } else {
+                        at = kBigCap;
+                        misc[F3_BIGOVF] = 1u;
+                    }
+                    boff[bk[k]] = at;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = tid + (uint32_t)k * BS;
+                if (s < ksa) {
+                    if (((r0[k] >> 11) & 7u) == kBig) {
+                        const uint32_t at = boff[bk[k]];
+                        r0[k] = s | (kBig << 11) | ((at < kBigCap ? at : 0u) << 16);
+                        if (at >= kBigCap) r1[k] = 0;   // stays in bounds; the pair is redone
+                    }
+                    const uint32_t q = misc[F3_CLS + cls[k]] + rank[k];
+                    srec[2u * q] = r0[k];
+                    srec[2u * q + 1u] = r1[k];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t q = tid + (uint32_t)k * BS;
+                if (q < ksa) {
+                    rec0[k] = srec[2u * q];
+                    rec1[k] = srec[2u * q + 1u];
+                } else {
+                    rec0[k] = dummy | (dummy << 16);
+                    rec1[k] = dummy | (dummy << 16);
+                }
+                cmax[k] = __builtin_amdgcn_readfirstlane((rec0[k] >> 11) & 7u);
+            }
+            nbk_c = nbk;
+            __syncthreads();
+            for (uint32_t w = tid; w < nbk + 2u * ksa + (ksa + 1u) / 2u; w += BS) boff[w] = 0;
+            __syncthreads();
+        }
+
+        // cell of a staged (A record + B record) sum: 2 * slot + (ch_i != ch_j)
+        auto cell_of = [&](uint32_t sum) {
+            uint32_t r = sum & 0xFFFu;
+            r = min(r, r - Bm);
+            return ((((sum >> 12) & 0xFFFu) + r) << 1) | ((sum >> 24) & 1u);
+        };
+        M3(1);
+        // ---- P1: first-insert time of every cell. The first pass's products stay in registers
+        //      for P5: i | j << 8 | cell << 16 (i, j < 256, cell < 4096); t >= n: ~0
+        uint32_t prod[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) prod[u] = ~0u;
+        {
+            const uint32_t tid = opaque(threadIdx.x);
+            for (uint32_t t0 = tid; t0 < n; t0 += U * BS) {
+                uint32_t sum[U], ij[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t t = min(t0 + (uint32_t)u * BS, n - 1u);
+                    const uint32_t i = __umulhi(t << 8, mdiv);
+                    const uint32_t j = t - i * nB;
+                    ij[u] = i | (j << 8);
+                    sum[u] = a_inf[i] + b_inf[j];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t t = t0 + (uint32_t)u * BS;
+                    const uint32_t c = cell_of(sum[u]);
+                    if (t < n) atomicMin(&tkey[c], t);
+                    if (t0 == tid) prod[u] = t < n ? ij[u] | (c << 16) : ~0u;
+                }
+            }
+        }
+        STAMP3_SYNC(1);
+        if (wave == NW - 1 && lane < 16) misc[F3_HDR + lane] = hv;   // its load has had P1 to land
+        __syncthreads();
+        STAMP3(2);
+        gq = launder(gq);
+        __builtin_amdgcn_s_setprio(1);
+        const fresh_hdr nxt = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs);
+
+        M3(2);
+        // ---- P2: key time, emit bits, bucket time, rank in the bucket, bucket edges
+        uint32_t ord[KI];   // tb (16) | within (14) << 16 | eb (2) << 30; eb = 0: nothing to emit
+        {
+            uint64_t own[KI];
+#pragma unroll
+            for (int k = 0; k < KI; ++k) own[k] = tk64[rec0[k] & 0x7FFu];
+            uint64_t myor = 0;
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = rec0[k] & 0x7FFu, c = (rec0[k] >> 11) & 7u;
+                const uint32_t tP = (uint32_t)own[k] & kT16, tM = (uint32_t)(own[k] >> 32) & kT16;
+                const uint32_t kt = s < KS ? min(tP, tM) : kT16;
+                const uint32_t eb = kt == kT16 ? 0u : (tP != kT16 ? 1u : 0u) | (tM != kT16 ? 2u : 0u);
+                uint32_t tb = kt, within = 0, cE = __popc(eb);
+                auto take = [&](uint64_t x) {
+                    const uint32_t x0 = (uint32_t)x & kT16, x1 = (uint32_t)(x >> 32) & kT16;
+                    const uint32_t t2 = min(x0, x1);
+                    const uint32_t e2 = (x0 != kT16 ? 1u : 0u) + (x1 != kT16 ? 1u : 0u);
+                    tb = min(tb, t2);
+                    within += t2 > kt && t2 != kT16 ? e2 : 0u;
+                    cE += e2;
+                };
+                const bool big = c == kBig;
+                if (cmax[k] > 0u) take(tk64[!big && c > 0u ? rec0[k] >> 16 : dummy]);
+                if (cmax[k] > 1u) take(tk64[!big && c > 1u ? rec1[k] & 0xFFFFu : dummy]);
+                if (cmax[k] > 2u) take(tk64[!big && c > 2u ? rec1[k] >> 16 : dummy]);
+                if (cmax[k] == kBig && big && kt != kT16) {   // more than 3 mates: the bucket from LDS
+                    const uint32_t q0 = rec0[k] >> 16, g = rec1[k];
+                    for (uint32_t q = q0; q <= q0 + g; ++q) {
+                        const uint32_t m = members[q];
+                        if (m != s) take(tk64[m]);
+                    }
+                }
+                if (kt != kT16 && tb == kt) tk16[2u * tb + 1u] = (uint16_t)cE;   // G[t_bkt]
+                ord[k] = tb | (within << 16) | (eb << 30);
+                myor |= eb ? 1ull << __umulhi(s, bdiv) : 0ull;
+            }
+            myor = wave_or_u64(myor);
+            if (lane == 0) wave_lp[wave] = myor;
+        }
+        STAMP3_SYNC(3);
+        __syncthreads();
+        STAMP3(4);
+        gq = launder(gq);
+
+        M3(3);
+        // ---- P3: every wave suffix-scans 256-time segments of G (in place, in-segment offsets;
+        //      segment totals into misc[F3_PART + g]); then wave 0 runs compact_layers
+        {
+            const uint32_t nseg = (n + 255u) >> 8;
+            uint4* gv = (uint4*)tkey;
+            for (uint32_t g = (uint32_t)wave; g < nseg; g += NW) {
+                const uint32_t q = g * 64u + (uint32_t)lane;   // b128 chunk: times 4q .. 4q + 3
+                const bool live = 4u * q < n;
+                const uint4 x = live ? gv[q] : make_uint4(0, 0, 0, 0);
+                const uint32_t local = (x.x >> 16) + (x.y >> 16) + (x.z >> 16) + (x.w >> 16);
+                const uint32_t incl = wave_incl_scan_u32(local);
+                const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+                uint32_t run = tot - incl;   // later chunks of the segment
+                uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int h = 3; h >= 0; --h) {
+                    const uint32_t gcur = w[h] >> 16;
+                    w[h] = (w[h] & 0xFFFFu) | (run << 16);
+                    run += gcur;
+                }
+                if (live) gv[q] = make_uint4(w[0], w[1], w[2], w[3]);
+                if (lane == 0) misc[F3_PART + g] = tot;
+            }
+        }
+        // compact_layers: when every product layer has an edge, every input layer is a direct
+        // parent of one, so nothing is removed (ident); only otherwise does wave 0 run the closure
+        uint64_t used_lp = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) used_lp |= wave_lp[w];
+        const bool all_lp = used_lp == (LP >= 64 ? ~0ull : ((1ull << LP) - 1ull));
+        if (wave == 0 && !all_lp) {
+            __builtin_amdgcn_s_setprio(3);
+            const uint64_t all = Lc >= 64 ? ~0ull : ((1ull << Lc) - 1ull);
+            uint64_t keep = (used_lp << base) & all;
+            const uint64_t mypm = (uint32_t)lane < Lc ? pm[lane] : 0ull;
+            for (;;) {
+                const uint64_t par = wave_or_u64(((keep >> lane) & 1ull) ? mypm : 0ull);
+                const uint64_t nk = keep | par;
+                if (nk == keep) break;
+                keep = nk;
+            }
+            if ((uint32_t)lane < Lc)
+                remap[lane] = ((keep >> lane) & 1ull)
+                                  ? __builtin_amdgcn_mbcnt_hi((uint32_t)(keep >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u))
+                                  : 0xFFFFFFFFu;
+            if (lane == 0) {
+                *(uint64_t*)(misc + F3_KEEP) = keep;
+                misc[F3_IDENT] = keep == all;
+            }
+            __builtin_amdgcn_s_setprio(1);
+        }
+        STAMP3_SYNC(5);
+        __syncthreads();
+        STAMP3(6);
+        gq = launder(gq);
+
+        M3(4);
+        // ---- P4: segment offsets (suffix over the segment totals, lane g holds segment g's),
+        //      then emit positions into the cell words and cell ids into limb 2
+        const uint32_t nseg = (n + 255u) >> 8;
+        uint32_t segsuf, total;
+        {
+            const uint32_t tl = (uint32_t)lane < nseg ? misc[F3_PART + lane] : 0u;
+            const uint32_t incl = wave_incl_scan_u32(tl);
+            total = __builtin_amdgcn_readlane(incl, 63);
+            segsuf = total - incl;   // segments after lane's
+        }
+        // guard_budget (encrypt.hpp:106-111) and ORDER_CANONICAL want (layer, idx, P<M) order: the
+        // general path produces it (redo); this kernel emits the reference hash order only
+        const bool canonical = (gq->flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > gq->edge_budget;
+        const uint64_t ceo = cur.ceo;
+        {
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const uint32_t s = rec0[k] & 0x7FFu;
+                const uint32_t eb = ord[k] >> 30;
+                const uint32_t tb = ord[k] & kT16;
+                // segment offset of t_bkt from lane tb >> 8 (ds_bpermute; every lane takes part)
+                const uint32_t so = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((eb ? tb >> 8 : 0u) << 2), (int)segsuf);
+                uint32_t p = eb ? (tkey[tb] >> 16) + so + ((ord[k] >> 16) & 0x3FFFu) : 0u;
+                if (eb & 1u) {
+                    tk16[4u * s] = (uint16_t)p;
+                    lim[3u * p + 2u] = (unsigned long long)(2u * s) << 52;
+                    ++p;
+                }
+                if (eb & 2u) {
+                    tk16[4u * s + 2u] = (uint16_t)p;
+                    lim[3u * p + 2u] = (unsigned long long)(2u * s + 1u) << 52;
+                }
+            }
+        }
+        const uint64_t keep = all_lp ? (Lc >= 64 ? ~0ull : ((1ull << Lc) - 1ull)) : *(const uint64_t*)(misc + F3_KEEP);
+        const bool ident = all_lp || misc[F3_IDENT] != 0;
+        if (!ident && wave == 1) {   // compact the identity-placed layer records in place
+            const uint32_t l = lane;
+            const uint64_t clo = cur.clo;
+            pvac_layer y{};
+            if (l < Lc) y = gq->C.layers[clo + l];
+            if (l < Lc && ((keep >> l) & 1ull)) {
+                if (y.rule == 1) {
+                    y.pa = y.pa < Lc ? remap[y.pa] : 0xFFFFFFFFu;
+                    y.pb = y.pb < Lc ? remap[y.pb] : 0xFFFFFFFFu;
+                }
+                gq->C.layers[clo + remap[l]] = y;
+            }
+        }
+        if (threadIdx.x == 0) {
+            gq->C.e_cnt[pr] = total;
+            gq->C.l_cnt[pr] = (uint64_t)__popcll(keep);
+            gq->pair_status[pr] = 0;
+        }
+        // next pair's raw inputs: in flight through P5 and the writer, staged after them
+        const fresh_pref pf = prefetch_pair(gq, nxt);
+        STAMP3_SYNC(7);
+        __syncthreads();
+        STAMP3(8);
+        gq = launder(gq);
+        __builtin_amdgcn_s_setprio(0);
+
+        M3(5);
+        // ---- P5: products into the limb accumulators of their emit positions
+        {
+            const uint32_t tid = opaque(threadIdx.x);
+            auto accumulate = [&](const ulonglong2& x, const ulonglong2& y, uint32_t p) {
+                uint64_t x0, x1, l0, l1, l2;
+                fp_mul_fold1(fp{x.x, x.y}, fp{y.x, y.y}, x0, x1);
+                fp_split3_44(x0, x1, l0, l1, l2);
+                unsigned long long* q = lim + 3u * p;
+                atomicAdd(q, (unsigned long long)l0);
+                atomicAdd(q + 1, (unsigned long long)l1);
+                atomicAdd(q + 2, (unsigned long long)l2);
+            };
+            // first pass from the registers of P1, two products at a time
+#pragma unroll
+            for (int u0 = 0; u0 < U; u0 += 2) {
+                if (__builtin_amdgcn_ballot_w64(prod[u0] != ~0u) == 0) continue;   // none in this wave's rounds
+                ulonglong2 x[2], y[2];
+                uint32_t p[2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const uint32_t pk = prod[u0 + v] == ~0u ? 0u : prod[u0 + v];
+                    x[v] = a_w[pk & 0xFFu];
+                    y[v] = b_w[(pk >> 8) & 0xFFu];
+                    p[v] = tk16[2u * (pk >> 16)];
+                }
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+                    if (prod[u0 + v] != ~0u) accumulate(x[v], y[v], p[v]);
+            }
+            // further passes (n > U * BS): recompute
+            for (uint32_t t = tid + U * BS; t < n; t += BS) {
+                const uint32_t i = __umulhi(t << 8, mdiv);
+                const uint32_t j = t - i * nB;
+                const ulonglong2 x = a_w[i], y = b_w[j];
+                const uint32_t p = tk16[2u * cell_of(a_inf[i] + b_inf[j])];
+                accumulate(x, y, p);
+            }
+        }
+        STAMP3_SYNC(9);
+        __syncthreads();
+        STAMP3(10);
+        gq = launder(gq);
+
+        M3(7);
+        // ---- P6: stage the next pair first (its loads were issued before P5; a wait after the
+        //      writer's stores would have to wait for those too: vmcnt counts both in order), then
+        //      the coalesced writer over emit positions (not the control wave: its vector-memory
+        //      queue stays free of stores), then clear the cell words
+        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+        {
+            const uint32_t tid = opaque(threadIdx.x);
+            uint64_t* cm = gq->C.meta + ceo;
+            uint64_t* cl = gq->C.w_lo + ceo;
+            uint64_t* chh = gq->C.w_hi + ceo;
+            uint32_t* sp = gq->salt_pos ? gq->salt_pos + ceo : nullptr;
+            uint32_t zero = canonical || misc[F3_BIGOVF] ? 1u : 0u;
+            for (uint32_t p = tid; p < total && wave != NW - 1; p += BS - 64) {
+                unsigned long long* q = lim + 3u * p;
+                const uint64_t l0 = q[0], l1 = q[1], l2c = q[2];
+                q[0] = 0;
+                q[1] = 0;
+                q[2] = 0;
+                const uint32_t cell = (uint32_t)(l2c >> 52);
+                const fp w = fp_fold3_44(l0, l1, l2c & ((1ull << 52) - 1ull));
+                zero |= fp_nonzero(w) ? 0u : 1u;
+                const uint32_t s = cell >> 1;
+                const uint32_t lp = __umulhi(s, bdiv);
+                const uint32_t r = s - lp * Bm;
+                const uint32_t lid = ident ? base + lp : remap[base + lp];
+                cm[p] = make_meta(lid, r, cell & 1u);
+                cl[p] = w.lo;
+                chh[p] = w.hi;
+                if (sp) sp[p] = p;   // hash order == emit order here
+            }
+            if (zero) misc[F3_ZERO] = 1u;
+            STAMP3_SYNC(11);
+            const uint32_t used = (max(2u * KS, n) + 3u) >> 2;   // b128 words of this pair's cells and G
+            uint4* tv = (uint4*)tkey;
+            for (uint32_t q = tid; q < used; q += BS) tv[q] = make_uint4(kT16, kT16, kT16, kT16);
+        }
+        M3(8);
+        STAMP3_SYNC(12);
+        __syncthreads();
+        STAMP3(13);
+        if (threadIdx.x == 0 && misc[F3_ZERO]) {   // the general path redoes the pair
+            gq->pair_status[pr] = kPairRedo;
+            gq->redo_ids[atomicAdd(gq->redo_cnt, 1u)] = pr;
+            misc[F3_ZERO] = 0;
+        }
+        cur = nxt;
+        STAMP3(0);
+#ifdef PVAC_CENSUS
+        ++cen_pairs;
+#endif
+    }
+#ifdef PVAC_CENSUS
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_census[4 * blockIdx.x] = cen_t0;
+        g_census[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        g_census[4 * blockIdx.x + 2] = cen_pairs;
+        g_census[4 * blockIdx.x + 3] = hw;
+    }
+#endif
+#ifdef PVAC_PHASE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 4096)
+        for (int p = 0; p < kStampPhases; ++p) g_fresh_stamps[blockIdx.x * kStampPhases + p] = st3_acc[p];
+#endif
+}
+
 }  // namespace
 
 #ifdef PVAC_PHASE_STAMPS
@@ -882,6 +1544,39 @@ hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* ar
     if (a.ks_max > kFreshKeysMax || a.layers_max > kFreshLayersMax || a.na_max > kFreshEdgesMax ||
         a.nb_max > kFreshEdgesMax)
         return hipErrorInvalidValue;
+    static const bool v1 = [] {
+        const char* e = std::getenv("PVAC_FRESH_KERNEL");
+        return e && e[0] == '1';
+    }();
+    if (!v1) {
+        // 12-bit product times and cell ids, 16-bit positions (see k_ct_mul_fresh3)
+        if (a.prod_max > kFreshProdMax || 2u * a.ks_max > 4096u) return hipErrorInvalidValue;
+        const fresh3_layout L = fresh3_lds(a.ks_max, a.prod_max, a.na_max, a.nb_max, a.buckets_max, a.layers_max);
+        if (L.total > 160u * 1024u) return hipErrorInvalidValue;
+        // resident workgroups per CU as the runtime counts them (LDS granules, registers): the
+        // grid is persistent, so a workgroup that is not resident would run after the others
+        static int occ_cache[2] = {-1, 0};   // {LDS bytes, blocks per CU}
+        if (occ_cache[0] != (int)L.total) {
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ct_mul_fresh3<kFreshThreads>, kFreshThreads,
+                                                              L.total) != hipSuccess || nb < 1)
+                nb = 1;
+            occ_cache[0] = (int)L.total;
+            occ_cache[1] = nb;
+            if (std::getenv("PVAC_DEBUG_OCC"))
+                std::fprintf(stderr, "[pvac] k_ct_mul_fresh3: %u B LDS per workgroup, %d resident per CU\n", L.total, nb);
+        }
+        // the API counts LDS in 128-byte steps; measured residency (tools/res_probe.hip) follows
+        // 2 KiB granules: 53,248 B gives 3 workgroups per CU, 53,888 B only 2
+        const int lds_fit = (int)((160u * 1024u) / ((L.total + 2047u) & ~2047u));
+        int per_cu = std::min(std::min(occ_cache[1], lds_fit), 3);
+        if (const char* e = std::getenv("PVAC_FRESH_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
+        uint64_t blocks = (uint64_t)num_cus * per_cu;
+        if (blocks > a.A.n) blocks = a.A.n;
+        hipLaunchKernelGGL((k_ct_mul_fresh3<kFreshThreads>), dim3((unsigned)blocks), dim3(kFreshThreads), L.total, st,
+                           args_dev, L);
+        return hipGetLastError();
+    }
     const fresh_layout L = fresh_lds(a.ks_max, a.na_max, a.nb_max, a.buckets_max);
     // G (one u16 per product time) lives in the slot tails: 4 per slot (the plan keeps |A.E||B.E|
     // <= 3 |A.L||B.L|B for fresh-path pairs)

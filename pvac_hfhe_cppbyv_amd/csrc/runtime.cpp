@@ -73,11 +73,14 @@ struct pvac_hip_ctx {
     size_t enc_arena_cap = 0;
     uint64_t* large_ids = nullptr;
     uint64_t* large_info = nullptr;
+    uint64_t* redo_ids = nullptr;        // fresh-kernel pairs left to the general path (a key sum of 0)
+    unsigned int* redo_cnt = nullptr;
     size_t pair_cap = 0;
     // general ct_mul path: host descriptors of the last plan, device copies, scratch arena
     std::vector<large_desc> large_host;
     std::vector<large_desc> large_exec;
     uint32_t plan_stamp = 0;
+    uint64_t redo_total = 0;           // pairs re-run by redo_fresh_pairs since the context was created
     large_desc* desc_dev = nullptr;
     size_t desc_cap = 0;
     uint32_t* arena = nullptr;
@@ -162,8 +165,10 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
         hipFree(c->pair_status);
         hipFree(c->large_ids);
         hipFree(c->large_info);
+        hipFree(c->redo_ids);
         hipFree(c->fresh_recs);
         c->fresh_recs = nullptr;
+        c->redo_ids = nullptr;
         c->pair_class = nullptr;
         c->pair_status = nullptr;
         c->large_ids = nullptr;
@@ -174,6 +179,8 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
         if (e == hipSuccess) e = hipMalloc(&c->large_ids, cap * 8);
         if (e == hipSuccess) e = hipMalloc(&c->large_info, cap * 64);   // 5 (mul) or 8 (add merge) words per pair
         if (e == hipSuccess) e = hipMalloc(&c->fresh_recs, cap * sizeof(fresh_rec));
+        if (e == hipSuccess) e = hipMalloc(&c->redo_ids, cap * 8);
+        if (e == hipSuccess && !c->redo_cnt) e = hipMalloc(&c->redo_cnt, 16);
         if (e != hipSuccess) { c->pair_cap = 0; return hip_fail(c, e, "alloc pair scratch"); }
         c->pair_cap = cap;
     }
@@ -335,6 +342,8 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->fresh_recs);
     hipFree(c->large_ids);
     hipFree(c->large_info);
+    hipFree(c->redo_ids);
+    hipFree(c->redo_cnt);
     hipFree(c->desc_dev);
     hipFree(c->arena);
     hipFree(c->grp);
@@ -379,6 +388,12 @@ void* pvac_hip_ctx_stream(pvac_hip_ctx* c) { return c ? (void*)c->stream : nullp
 int pvac_hip_ctx_synchronize(pvac_hip_ctx* c) {
     if (!c) return PVAC_EINVAL;
     return hip_fail(c, hipStreamSynchronize(c->stream), "synchronize");
+}
+
+int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* c, uint64_t* out) {
+    if (!c || !out) return PVAC_EINVAL;
+    *out = c->redo_total;
+    return PVAC_OK;
 }
 
 const char* pvac_hip_last_error(pvac_hip_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -608,6 +623,42 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
     return PVAC_OK;
 }
 
+// The fresh kernel emits every key cell that received a product; a cell whose sum is 0 mod p
+// (cancelling products or a zero weight, arithmetic.hpp:98-99) makes it flag the pair instead.
+// Those pairs are re-run here on the general path, which folds every sum before it orders keys.
+int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, const uint64_t* nonces,
+                     pvac_ct_batch* C, uint32_t flags, uint32_t* salt_pos) {
+    unsigned int cnt = 0;
+    hipError_t e = hipMemcpyAsync(&cnt, c->redo_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "ct_mul_exec (redo count)");
+    if (!cnt) return PVAC_OK;
+    std::vector<uint64_t> info(5 * (size_t)cnt);
+    e = launch_gather_large(*A, *B, c->redo_ids, cnt, c->large_info, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(info.data(), c->large_info, info.size() * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "ct_mul_exec (redo shapes)");
+    std::vector<large_desc> redo(cnt);
+    for (size_t k = 0; k < cnt; ++k) {
+        std::string why;
+        const int rc = build_large_desc(redo[k], info[5 * k], info[5 * k + 1], info[5 * k + 2], info[5 * k + 3],
+                                        info[5 * k + 4], c->prm.B, why);
+        if (rc) return fail(c, rc, why);
+    }
+    std::sort(redo.begin(), redo.end(), [](const large_desc& x, const large_desc& y) { return x.pair < y.pair; });
+    // run them as the context's large-pair set, then restore the plan's own set and its tables
+    std::vector<large_desc> plan_set;
+    plan_set.swap(c->large_host);
+    c->large_host.swap(redo);
+    int rc = plan_static_groups(c);
+    if (!rc) rc = run_large(c, A, B, nonces, C, flags, salt_pos);
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = hip_fail(c, hipErrorUnknown, "ct_mul_exec (redo)");
+    c->large_host.swap(plan_set);
+    if (rc) return rc;
+    c->redo_total += cnt;
+    return c->large_host.empty() ? PVAC_OK : plan_static_groups(c);
+}
+
 }  // namespace
 
 int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_ct_batch* A, const pvac_ct_batch* B,
@@ -639,6 +690,8 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         a.nb_table = c->nb_table;
         a.nb_magic = c->nb_magic;
         a.salt_pos = salt_pos;
+        a.redo_ids = c->redo_ids;
+        a.redo_cnt = c->redo_cnt;
         a.canon_tag = c->prm.canon_tag;
         a.edge_budget = c->prm.edge_budget;
         a.Bm = c->prm.B;
@@ -661,6 +714,7 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         // stream-ordered copy from the ctx's host mirror (kept alive until the next exec)
         c->fresh_args_host = a;
         hipError_t e = hipMemcpyAsync(c->fresh_args, &c->fresh_args_host, sizeof a, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->redo_cnt, 0, sizeof(unsigned int), c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "upload fresh args");
         scoped_timer t(c, "ct_mul_fresh");
         e = launch_ct_mul_fresh(a, c->fresh_args, c->num_cus, c->stream);
@@ -669,6 +723,10 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
     if (plan->n_large) {
         scoped_timer t(c, "ct_mul_large");
         int rc = run_large(c, A, B, nonces, C, flags, salt_pos);
+        if (rc) return rc;
+    }
+    if (plan->n_small) {
+        int rc = redo_fresh_pairs(c, A, B, nonces, C, flags, salt_pos);
         if (rc) return rc;
     }
     if (with_sigma) {

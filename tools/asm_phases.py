@@ -18,7 +18,8 @@ def main():
            "-S", "-DPVAC_ASM_MARKS", *sys.argv[1:], SRC, "-o", OUT]
     subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
     lines = open(OUT).read().splitlines()
-    start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*k_ct_mul_fresh\S*:", l))
+    kern = os.environ.get("KERNEL", "k_ct_mul_fresh3")
+    start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + kern + r"I\S*:", l))
     end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
     cur = "entry"
     cnt = collections.OrderedDict()
