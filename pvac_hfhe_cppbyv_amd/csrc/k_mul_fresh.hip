@@ -256,12 +256,11 @@ struct fresh_pref {
     uint32_t rule, pa, pb;
 };
 
-__device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h) {
+__device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h, uint32_t t = threadIdx.x) {
     // branch-free and unconditional: every lane loads a valid address (a clamped index, or the
     // argument block itself when there is no pair / no edge), so the waitcnt pass never has to
     // drain earlier loads (or the previous pair's output stores) before issuing these; lanes past
     // the counts ignore what they loaded
-    const uint32_t t = threadIdx.x;
     const bool live = h.pr != kNoPair;
     using gp64 = const __attribute__((address_space(1))) uint64_t*;   // global: never a flat load
     using gpl = const __attribute__((address_space(1))) uint32_t*;
@@ -292,8 +291,7 @@ __device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h) 
 // compact_layers parent mask of every C layer. Flags invalid references in misc[MF_INVALID].
 __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr& h, uint32_t Bm, ulonglong2* a_w,
                                            uint32_t* a_inf, ulonglong2* b_w, uint32_t* b_inf, uint64_t* pm,
-                                           uint32_t* misc) {
-    const uint32_t t = threadIdx.x;
+                                           uint32_t* misc, uint32_t t = threadIdx.x) {
     if (h.pr == kNoPair) return;
     if (t < h.nA) {
         const uint32_t la = meta_layer(f.am), idx = meta_idx(f.am), ch = meta_ch(f.am);
@@ -1404,7 +1402,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
             gq->pair_status[pr] = 0;
         }
         // next pair's raw inputs: in flight through P5 and the writer, staged after them
-        const fresh_pref pf = prefetch_pair(gq, nxt);
+        const fresh_pref pf = prefetch_pair(gq, nxt, opaque(threadIdx.x));
         STAMP3_SYNC(7);
         __syncthreads();
         STAMP3(8);
@@ -1460,7 +1458,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         //      writer's stores would have to wait for those too: vmcnt counts both in order), then
         //      the coalesced writer over emit positions (not the control wave: its vector-memory
         //      queue stays free of stores), then clear the cell words
-        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+        stage_pair(pf, nxt, Bm, a_w, a_inf, b_w, b_inf, pm, misc, opaque(threadIdx.x));
         {
             const uint32_t tid = opaque(threadIdx.x);
             uint64_t* cm = gq->C.meta + ceo;
