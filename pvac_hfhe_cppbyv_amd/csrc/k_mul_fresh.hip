@@ -925,7 +925,7 @@ __host__ __device__ inline fresh3_layout fresh3_lds(uint32_t ks, uint32_t prod, 
     // bucket-group rebuild scratch: nbk u32 CSR offsets, 2 ks u32 slot records, ks u16 CSR
     // members; in the limb arrays when they fit (zero between pairs, zeroed again after a
     // rebuild), else at the end
-    const uint32_t scratch = (nbk + 2u * ks) * 4u + ks * 2u;
+    const uint32_t scratch = (2u * nbk + 2u * ks) * 4u + ks * 2u;
     if (scratch <= L.pmax * 24u) {
         L.boff = L.lim;
     } else {
@@ -938,6 +938,15 @@ __host__ __device__ inline fresh3_layout fresh3_lds(uint32_t ks, uint32_t prod, 
 
 #ifndef PVAC_U5
 #define PVAC_U5 2
+#endif
+#ifndef PVAC_REP_P1   // experiment builds repeat a phase (idempotent) to measure its cost
+#define PVAC_REP_P1 1
+#endif
+#ifndef PVAC_REP_P2
+#define PVAC_REP_P2 1
+#endif
+#ifndef PVAC_REP_P4
+#define PVAC_REP_P4 1
 #endif
 
 #ifdef PVAC_PHASE_STAMPS
@@ -973,7 +982,10 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
 
 template <int BS>
 __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* __restrict__ gp, fresh3_layout Ls) {
-    constexpr int KI = (kFreshKeysMax + BS - 1) / BS;    // key slots owned per thread
+    constexpr int KI = (kFreshKeysMax + BS - 1) / BS;    // key slots per thread (rebuild)
+    // bins per thread: a bin holds 2 or 3 slots except when size-2 buckets are left without a
+    // size-1 partner, so there are at most kFreshKeysMax / 2 bins
+    constexpr int KR = (kFreshKeysMax / 2 + BS - 1) / BS;
     constexpr int NW = BS / 64;
     constexpr int U = 4;                                 // product rounds per pass
     constexpr uint32_t kT16 = 0xFFFFu;                   // no first-insert time
@@ -1006,9 +1018,9 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
     // the bucket has more than 3 others; then m0 = CSR start into `members`, rec1 = their number.
     // Slot k of a thread has rank tid + k*BS in mate-count order (descending), so lane 0 of a wave
     // holds that wave's largest count for row k (cmax, wave-uniform).
-    uint32_t rec0[KI], rec1[KI], cmax[KI];
+    uint32_t rec0[KR], rec1[KR], cmax[KR];
 #pragma unroll
-    for (int k = 0; k < KI; ++k) {
+    for (int k = 0; k < KR; ++k) {
         rec0[k] = dummy | (dummy << 16);
         rec1[k] = dummy | (dummy << 16);
         cmax[k] = 0;
@@ -1076,8 +1088,9 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         if (nbk != nbk_c) {
             const uint32_t tid = opaque(threadIdx.x);
             const uint32_t ksa = gq->ks_max;
-            uint32_t* srec = boff + nbk;   // [2 ksa]: slot records by rank
-            uint16_t* csr = (uint16_t*)(srec + 2u * ksa);   // [ksa]: slots in bucket order
+            uint32_t* rnk = boff + nbk;                  // [nbk] rank of a bucket inside its size class
+            uint32_t* drec = rnk + nbk;                  // [2 ksa] bin records
+            uint16_t* csr = (uint16_t*)(drec + 2u * ksa);   // [ksa] slots in bucket order
             const fastmod64 fm{nbk, cur.nb_magic};
             uint32_t bk[KI];
 #pragma unroll
@@ -1087,7 +1100,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 bk[k] = (uint32_t)fmod64((((uint64_t)lp << 32) | (s - lp * Bm)) * kGolden, fm);
             }
             for (uint32_t w = tid; w < nbk; w += BS) boff[w] = 0;
-            if (tid < 8) misc[F3_CLS + tid] = 0;
+            if (tid < 8) misc[F3_CLS + tid] = 0;   // size classes 0 (big), 1, 2, 3; [7] = big-member allocation
             if (tid == 0) misc[F3_BIGOVF] = 0;
             __syncthreads();
 #pragma unroll
@@ -1113,91 +1126,78 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 if (s < ksa) csr[atomicAdd(&boff[bk[k]], 1u)] = (uint16_t)s;
             }
             __syncthreads();   // boff[b] is now the END of bucket b's slots
-            uint32_t r0[KI], r1[KI], cls[KI], rank[KI];
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t s = tid + (uint32_t)k * BS;
-                const uint32_t b = bk[k];
-                uint32_t m[3] = {dummy, dummy, dummy}, c = 0, start = 0;
-                if (s < ksa) {
-                    const uint32_t end = boff[b];
-                    start = b ? boff[b - 1] : 0u;
-                    for (uint32_t q = start; q < end; ++q) {
-                        const uint32_t x = csr[q];
-                        if (x == s) continue;
-#pragma unroll
-                        for (int j = 0; j < 3; ++j) m[j] = c == (uint32_t)j ? x : m[j];   // no dynamic index
-                        ++c;
-                    }
-                }
-                if (c > 3) {   // more than 3 mates: resolved through `members` below
-                    r0[k] = s | (kBig << 11) | (start << 16);
-                    r1[k] = c;
-                } else {
-                    r0[k] = s | (c << 11) | (m[0] << 16);
-                    r1[k] = m[1] | (m[2] << 16);
-                }
-                cls[k] = c > 3 ? 0u : 4u - c;   // descending mate count
-                rank[k] = s < ksa ? atomicAdd(&misc[F3_CLS + cls[k]], 1u) : 0u;
+            // Buckets packed into bins of at most 3 slots (a bucket never splits): every size-3
+            // bucket alone, each size-2 bucket with one size-1 bucket while they last, the other
+            // size-1 buckets by three; a bucket of more than 3 slots gets a bin of its own and
+            // its slots go to `members`. Bin record: rec0 = m0 | m1 << 16, rec1 = m2 | flags << 16
+            // (flags: bit 0 m0~m1 share a bucket, bit 1 m0~m2, bit 2 m1~m2, bit 3 big); unused
+            // slots are the dummy. Bin q belongs to thread q % BS, row q / BS.
+            const uint32_t nbr = (nbk + BS - 1) / BS;
+            for (uint32_t j = 0; j < nbr; ++j) {   // pass 1: rank inside the size class
+                const uint32_t b = tid + j * BS;
+                if (b >= nbk) break;
+                const uint32_t z = boff[b] - (b ? boff[b - 1] : 0u);
+                if (z) rnk[b] = atomicAdd(&misc[F3_CLS + (z > 3 ? 0u : z)], 1u);
             }
-            __syncthreads();   // every CSR end read
-            if (tid == 0) {    // class bases
-                uint32_t run = 0;
-                for (int c = 0; c < 5; ++c) {
-                    const uint32_t v = misc[F3_CLS + c];
-                    misc[F3_CLS + c] = run;
-                    run += v;
-                }
-            }
-            // a bucket of more than 4 slots: its first slot copies it into `members` and leaves the
-            // offset in boff[bucket]; past kBigCap entries the pairs of this bucket count take the
-            // general path
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t s = tid + (uint32_t)k * BS;
-                if (s < ksa && ((r0[k] >> 11) & 7u) == kBig && csr[r0[k] >> 16] == s) {
-                    const uint32_t c = r1[k], start = r0[k] >> 16;
-                    uint32_t at = atomicAdd(&misc[F3_CLS + 7], c + 1u);
-                    if (at + c + 1u <= kBigCap) {
-                        for (uint32_t q = 0; q <= c; ++q) members[at + q] = csr[start + q];
+            for (uint32_t q = tid; q < 2u * ksa; q += BS) drec[q] = q & 1u ? dummy : dummy | (dummy << 16);
+            __syncthreads();
+            const uint32_t nbig = misc[F3_CLS + 0], n1 = misc[F3_CLS + 1], n2 = misc[F3_CLS + 2], n3 = misc[F3_CLS + 3];
+            const uint32_t pair1 = min(n1, n2);                    // size-1 buckets that join a size-2 one
+            const uint32_t b3 = nbig, b2 = b3 + n3, b1 = b2 + n2;  // first bin of each kind
+            const uint32_t nbins = b1 + (n1 - pair1 + 2u) / 3u;
+            uint16_t* dh = (uint16_t*)drec;                        // [4 q + f]: field f of bin q
+            for (uint32_t j = 0; j < nbr; ++j) {   // pass 2: slots into bins
+                const uint32_t b = tid + j * BS;
+                if (b >= nbk) break;
+                const uint32_t end = boff[b], start = b ? boff[b - 1] : 0u, z = end - start;
+                if (z == 0) continue;
+                const uint32_t r = rnk[b];
+                if (z == 3) {
+                    const uint32_t q = b3 + r;
+                    dh[4u * q] = csr[start];
+                    dh[4u * q + 1u] = csr[start + 1];
+                    dh[4u * q + 2u] = csr[start + 2];
+                    dh[4u * q + 3u] = 7u;
+                } else if (z == 2) {
+                    const uint32_t q = b2 + r;
+                    dh[4u * q] = csr[start];
+                    dh[4u * q + 1u] = csr[start + 1];
+                    dh[4u * q + 3u] = 1u;
+                } else if (z == 1) {
+                    if (r < pair1) {
+                        dh[4u * (b2 + r) + 2u] = csr[start];
                     } else {
-                        at = kBigCap;
+                        const uint32_t x = r - pair1;
+                        dh[4u * (b1 + x / 3u) + x % 3u] = csr[start];
+                    }
+                } else {   // more than 3 slots
+                    const uint32_t q = r;
+                    uint32_t at = atomicAdd(&misc[F3_CLS + 7], z);
+                    uint32_t zz = z;
+                    if (at + z <= kBigCap) {
+                        for (uint32_t x = 0; x < z; ++x) members[at + x] = csr[start + x];
+                    } else {   // pairs of this bucket count go to the general path
+                        at = 0;
+                        zz = 1;
                         misc[F3_BIGOVF] = 1u;
                     }
-                    boff[bk[k]] = at;
+                    dh[4u * q] = (uint16_t)at;
+                    dh[4u * q + 1u] = (uint16_t)zz;
+                    dh[4u * q + 3u] = 8u;
                 }
             }
             __syncthreads();
+            if (tid == 0 && nbins > (uint32_t)(KR * BS)) misc[F3_BIGOVF] = 1u;   // cannot happen (see KR)
 #pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t s = tid + (uint32_t)k * BS;
-                if (s < ksa) {
-                    if (((r0[k] >> 11) & 7u) == kBig) {
-                        const uint32_t at = boff[bk[k]];
-                        r0[k] = s | (kBig << 11) | ((at < kBigCap ? at : 0u) << 16);
-                        if (at >= kBigCap) r1[k] = 0;   // stays in bounds; the pair is redone
-                    }
-                    const uint32_t q = misc[F3_CLS + cls[k]] + rank[k];
-                    srec[2u * q] = r0[k];
-                    srec[2u * q + 1u] = r1[k];
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
+            for (int k = 0; k < KR; ++k) {
                 const uint32_t q = tid + (uint32_t)k * BS;
-                if (q < ksa) {
-                    rec0[k] = srec[2u * q];
-                    rec1[k] = srec[2u * q + 1u];
-                } else {
-                    rec0[k] = dummy | (dummy << 16);
-                    rec1[k] = dummy | (dummy << 16);
-                }
-                cmax[k] = __builtin_amdgcn_readfirstlane((rec0[k] >> 11) & 7u);
+                rec0[k] = q < nbins ? drec[2u * q] : dummy | (dummy << 16);
+                rec1[k] = q < nbins ? drec[2u * q + 1u] : dummy;
+                cmax[k] = __builtin_amdgcn_readfirstlane(q < nbins ? 1u : 0u);   // row has bins in this wave
             }
             nbk_c = nbk;
             __syncthreads();
-            for (uint32_t w = tid; w < nbk + 2u * ksa + (ksa + 1u) / 2u; w += BS) boff[w] = 0;
+            for (uint32_t w = tid; w < 2u * nbk + 2u * ksa + (ksa + 1u) / 2u; w += BS) boff[w] = 0;
             __syncthreads();
         }
 
@@ -1213,6 +1213,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         uint32_t prod[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) prod[u] = ~0u;
+        for (int rep_ = 0; rep_ < PVAC_REP_P1; ++rep_) {   // experiment builds only (tools/exp_fresh3.py)
         {
             const uint32_t tid = opaque(threadIdx.x);
             for (uint32_t t0 = tid; t0 < n; t0 += U * BS) {
@@ -1234,6 +1235,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 }
             }
         }
+        }
         STAMP3_SYNC(1);
         if (wave == NW - 1 && lane < 16) misc[F3_HDR + lane] = hv;   // its load has had P1 to land
         __syncthreads();
@@ -1243,45 +1245,67 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         const fresh_hdr nxt = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs);
 
         M3(2);
-        // ---- P2: key time, emit bits, bucket time, rank in the bucket, bucket edges
-        uint32_t ord[KI];   // tb (16) | within (14) << 16 | eb (2) << 30; eb = 0: nothing to emit
+        // ---- P2: per bin (up to 3 slots whose buckets lie wholly in the bin): key time and emit
+        //      bits of each slot, its bucket's first-insert time t_bkt, its rank in the bucket
+        //      (edges of later keys) and the bucket's edge count G[t_bkt]
+        uint32_t ordA[KR], ordB[KR];   // t_bkt of slots 0, 1 | t_bkt of slot 2, rank 3 bits x 3, emit 2 bits x 3
+        for (int rep_ = 0; rep_ < PVAC_REP_P2; ++rep_) {   // experiment builds only (tools/exp_fresh3.py)
         {
-            uint64_t own[KI];
-#pragma unroll
-            for (int k = 0; k < KI; ++k) own[k] = tk64[rec0[k] & 0x7FFu];
             uint64_t myor = 0;
+            auto cells = [&](uint64_t x, uint32_t& t, uint32_t& e) {
+                const uint32_t x0 = (uint32_t)x & kT16, x1 = (uint32_t)(x >> 32) & kT16;
+                t = min(x0, x1);
+                e = (x0 != kT16 ? 1u : 0u) | (x1 != kT16 ? 2u : 0u);
+            };
 #pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t s = rec0[k] & 0x7FFu, c = (rec0[k] >> 11) & 7u;
-                const uint32_t tP = (uint32_t)own[k] & kT16, tM = (uint32_t)(own[k] >> 32) & kT16;
-                const uint32_t kt = s < KS ? min(tP, tM) : kT16;
-                const uint32_t eb = kt == kT16 ? 0u : (tP != kT16 ? 1u : 0u) | (tM != kT16 ? 2u : 0u);
-                uint32_t tb = kt, within = 0, cE = __popc(eb);
-                auto take = [&](uint64_t x) {
-                    const uint32_t x0 = (uint32_t)x & kT16, x1 = (uint32_t)(x >> 32) & kT16;
-                    const uint32_t t2 = min(x0, x1);
-                    const uint32_t e2 = (x0 != kT16 ? 1u : 0u) + (x1 != kT16 ? 1u : 0u);
-                    tb = min(tb, t2);
-                    within += t2 > kt && t2 != kT16 ? e2 : 0u;
-                    cE += e2;
-                };
-                const bool big = c == kBig;
-                if (cmax[k] > 0u) take(tk64[!big && c > 0u ? rec0[k] >> 16 : dummy]);
-                if (cmax[k] > 1u) take(tk64[!big && c > 1u ? rec1[k] & 0xFFFFu : dummy]);
-                if (cmax[k] > 2u) take(tk64[!big && c > 2u ? rec1[k] >> 16 : dummy]);
-                if (cmax[k] == kBig && big && kt != kT16) {   // more than 3 mates: the bucket from LDS
-                    const uint32_t q0 = rec0[k] >> 16, g = rec1[k];
-                    for (uint32_t q = q0; q <= q0 + g; ++q) {
+            for (int k = 0; k < KR; ++k) {
+                ordA[k] = kT16 | (kT16 << 16);
+                ordB[k] = kT16;
+                if (cmax[k] == 0u) continue;   // wave-uniform: no bin in this row
+                const uint32_t fl = rec1[k] >> 16;
+                const bool big = (fl & 8u) != 0;
+                const uint32_t m0 = big ? dummy : rec0[k] & 0xFFFFu, m1 = big ? dummy : rec0[k] >> 16;
+                const uint32_t m2 = rec1[k] & 0xFFFFu;
+                uint32_t t0, t1, t2, e0, e1, e2;
+                cells(tk64[m0], t0, e0);
+                cells(tk64[m1], t1, e1);
+                cells(tk64[m2], t2, e2);
+                const uint32_t p0 = __popc(e0), p1 = __popc(e1), p2 = __popc(e2);
+                const bool f01 = fl & 1u, f02 = fl & 2u, f12 = fl & 4u;
+                // times are distinct when present; an absent slot has no edges (p = 0)
+                const uint32_t wi0 = (f01 && t1 > t0 ? p1 : 0u) + (f02 && t2 > t0 ? p2 : 0u);
+                const uint32_t wi1 = (f01 && t0 > t1 ? p0 : 0u) + (f12 && t2 > t1 ? p2 : 0u);
+                const uint32_t wi2 = (f02 && t0 > t2 ? p0 : 0u) + (f12 && t1 > t2 ? p1 : 0u);
+                uint32_t tb0 = min(t0, min(f01 ? t1 : kT16, f02 ? t2 : kT16));
+                const uint32_t tb1 = min(t1, min(f01 ? t0 : kT16, f12 ? t2 : kT16));
+                const uint32_t tb2 = min(t2, min(f02 ? t0 : kT16, f12 ? t1 : kT16));
+                uint32_t cE0 = p0 + (f01 ? p1 : 0u) + (f02 ? p2 : 0u);
+                const uint32_t cE1 = p1 + (f01 ? p0 : 0u) + (f12 ? p2 : 0u);
+                const uint32_t cE2 = p2 + (f02 ? p0 : 0u) + (f12 ? p1 : 0u);
+                myor |= (e0 ? 1ull << __umulhi(m0, bdiv) : 0ull) | (e1 ? 1ull << __umulhi(m1, bdiv) : 0ull) |
+                        (e2 ? 1ull << __umulhi(m2, bdiv) : 0ull);
+                if (big) {   // a bucket of more than 3 slots (rare): t_bkt and edges from `members`
+                    const uint32_t q0 = rec0[k] & 0xFFFFu, g = rec0[k] >> 16;
+                    for (uint32_t q = q0; q < q0 + g; ++q) {
                         const uint32_t m = members[q];
-                        if (m != s) take(tk64[m]);
+                        uint32_t t, e;
+                        cells(tk64[m], t, e);
+                        tb0 = min(tb0, t);
+                        cE0 += __popc(e);
+                        myor |= e ? 1ull << __umulhi(m, bdiv) : 0ull;
                     }
                 }
-                if (kt != kT16 && tb == kt) tk16[2u * tb + 1u] = (uint16_t)cE;   // G[t_bkt]
-                ord[k] = tb | (within << 16) | (eb << 30);
-                myor |= eb ? 1ull << __umulhi(s, bdiv) : 0ull;
+                // G[t_bkt] from the bucket's leader (duplicates of one bucket write the same value)
+                if (tb0 != kT16 && tb0 == t0) tk16[2u * tb0 + 1u] = (uint16_t)cE0;
+                if (tb1 != kT16 && tb1 == t1) tk16[2u * tb1 + 1u] = (uint16_t)cE1;
+                if (tb2 != kT16 && tb2 == t2) tk16[2u * tb2 + 1u] = (uint16_t)cE2;
+                if (big && tb0 != kT16) tk16[2u * tb0 + 1u] = (uint16_t)cE0;
+                ordA[k] = tb0 | (tb1 << 16);
+                ordB[k] = tb2 | (wi0 << 16) | (wi1 << 19) | (wi2 << 22) | (e0 << 25) | (e1 << 27) | (e2 << 29);
             }
             myor = wave_or_u64(myor);
             if (lane == 0) wave_lp[wave] = myor;
+        }
         }
         STAMP3_SYNC(3);
         __syncthreads();
@@ -1361,25 +1385,58 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         // general path produces it (redo); this kernel emits the reference hash order only
         const bool canonical = (gq->flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > gq->edge_budget;
         const uint64_t ceo = cur.ceo;
+        for (int rep_ = 0; rep_ < PVAC_REP_P4; ++rep_) {   // experiment builds only (tools/exp_fresh3.py)
         {
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const uint32_t s = rec0[k] & 0x7FFu;
-                const uint32_t eb = ord[k] >> 30;
-                const uint32_t tb = ord[k] & kT16;
-                // segment offset of t_bkt from lane tb >> 8 (ds_bpermute; every lane takes part)
-                const uint32_t so = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((eb ? tb >> 8 : 0u) << 2), (int)segsuf);
-                uint32_t p = eb ? (tkey[tb] >> 16) + so + ((ord[k] >> 16) & 0x3FFFu) : 0u;
-                if (eb & 1u) {
-                    tk16[4u * s] = (uint16_t)p;
-                    lim[3u * p + 2u] = (unsigned long long)(2u * s) << 52;
+            auto emit = [&](uint32_t m, uint32_t e, uint32_t p) {   // slot m's cells at p (P), p + (P present) (M)
+                if (e & 1u) {
+                    tk16[4u * m] = (uint16_t)p;
+                    lim[3u * p + 2u] = (unsigned long long)(2u * m) << 52;
                     ++p;
                 }
-                if (eb & 2u) {
-                    tk16[4u * s + 2u] = (uint16_t)p;
-                    lim[3u * p + 2u] = (unsigned long long)(2u * s + 1u) << 52;
+                if (e & 2u) {
+                    tk16[4u * m + 2u] = (uint16_t)p;
+                    lim[3u * p + 2u] = (unsigned long long)(2u * m + 1u) << 52;
+                }
+            };
+            // emit offset of bucket time tb: in-segment suffix offset + segment offset (from lane
+            // tb >> 8 by ds_bpermute, in which every lane takes part)
+            auto offset = [&](uint32_t tb) {
+                const bool has = tb != kT16;
+                const uint32_t so = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((has ? tb >> 8 : 0u) << 2), (int)segsuf);
+                return has ? (tkey[tb] >> 16) + so : 0u;
+            };
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                if (cmax[k] == 0u) continue;   // wave-uniform
+                const uint32_t fl = rec1[k] >> 16;
+                const bool big = (fl & 8u) != 0;
+                const uint32_t tb0 = ordA[k] & kT16, tb1 = ordA[k] >> 16, tb2 = ordB[k] & kT16;
+                const uint32_t o0 = offset(tb0), o1 = offset(tb1), o2 = offset(tb2);
+                if (!big) {
+                    emit(rec0[k] & 0xFFFFu, (ordB[k] >> 25) & 3u, o0 + ((ordB[k] >> 16) & 7u));
+                    emit(rec0[k] >> 16, (ordB[k] >> 27) & 3u, o1 + ((ordB[k] >> 19) & 7u));
+                    emit(rec1[k] & 0xFFFFu, (ordB[k] >> 29) & 3u, o2 + ((ordB[k] >> 22) & 7u));
+                } else if (tb0 != kT16) {   // big bucket: each slot's rank from the others' times (O(z^2), rare)
+                    const uint32_t q0 = rec0[k] & 0xFFFFu, g = rec0[k] >> 16;
+                    for (uint32_t q = q0; q < q0 + g; ++q) {
+                        const uint32_t m = members[q];
+                        const uint64_t x = tk64[m];
+                        const uint32_t x0 = (uint32_t)x & kT16, x1 = (uint32_t)(x >> 32) & kT16;
+                        const uint32_t t = min(x0, x1);
+                        const uint32_t e = (x0 != kT16 ? 1u : 0u) | (x1 != kT16 ? 2u : 0u);
+                        if (!e) continue;
+                        uint32_t within = 0;
+                        for (uint32_t r = q0; r < q0 + g; ++r) {
+                            const uint64_t y = tk64[members[r]];
+                            const uint32_t y0 = (uint32_t)y & kT16, y1 = (uint32_t)(y >> 32) & kT16;
+                            const uint32_t t2 = min(y0, y1);
+                            within += t2 != kT16 && t2 > t ? (y0 != kT16 ? 1u : 0u) + (y1 != kT16 ? 1u : 0u) : 0u;
+                        }
+                        emit(m, e, o0 + within);
+                    }
                 }
             }
+        }
         }
         const uint64_t keep = all_lp ? (Lc >= 64 ? ~0ull : ((1ull << Lc) - 1ull)) : *(const uint64_t*)(misc + F3_KEEP);
         const bool ident = all_lp || misc[F3_IDENT] != 0;
@@ -1415,7 +1472,12 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
             const uint32_t tid = opaque(threadIdx.x);
             auto accumulate = [&](const ulonglong2& x, const ulonglong2& y, uint32_t p) {
                 uint64_t x0, x1, l0, l1, l2;
+#ifdef PVAC_EXP_NOMUL3
+                x0 = x.x ^ y.x;
+                x1 = (x.y ^ y.y) & 0x7FFFFFFFFFFFFFFFull;
+#else
                 fp_mul_fold1(fp{x.x, x.y}, fp{y.x, y.y}, x0, x1);
+#endif
                 fp_split3_44(x0, x1, l0, l1, l2);
                 unsigned long long* q = lim + 3u * p;
                 atomicAdd(q, (unsigned long long)l0);
