@@ -97,7 +97,7 @@ typedef struct pvac_hip_plan {
     uint64_t n_pairs;
     uint64_t n_small;             /* pairs served by the LDS-resident fresh-shape kernel */
     uint64_t n_large;             /* pairs served by the layer-dense path */
-    uint64_t n_invalid;           /* pairs rejected (bad layer/idx refs) */
+    uint64_t n_invalid;           /* reserved, always 0: rejections are per pair, see pvac_hip_ct_mul_status */
     uint32_t max_keys, max_prod, max_na, max_nb, max_buckets, max_layers;  /* launch sizing */
     uint32_t kind;                /* 1 = mul, 2 = add, 3 = sub */
     uint32_t reserved[5];
@@ -159,6 +159,13 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pva
                          const uint64_t* nonces, const uint64_t* salts, pvac_ct_batch* C, uint32_t flags);
 /* Pairs that ct_mul_exec re-ran on the general path (see above) since the context was created. */
 int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* ctx, uint64_t* out);
+/* Per-pair outcome of the last ct_mul_exec, copied (stream-ordered) to the DEVICE array out[n]:
+ * 0 = reference hash order, 1 = canonical (layer, idx, P<M) order (guard_budget or
+ * PVAC_MUL_ORDER_CANONICAL), 2 = rejected. Rejection is stricter than the reference: an edge with
+ * layer_id >= |X.L| (undefined behaviour there: C.L[lid] out of range), idx >= B or ch > 1
+ * (defined there, out of the Cipher contract: dec_value indexes powg_B[idx]) makes the pair's
+ * output empty (l_cnt = e_cnt = 0) instead. */
+int pvac_hip_ct_mul_status(pvac_hip_ctx* ctx, uint32_t* out, size_t n);
 
 /* ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45; combine_ciphers ops/encrypt.hpp:260-279).
  * negate_b != 0 gives ct_sub (B's weights scaled by p-1). Dense CSR output: the plan writes

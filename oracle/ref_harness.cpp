@@ -1,4 +1,9 @@
-// ref_harness.cpp — TEST INFRASTRUCTURE ONLY (never shipped, never measured as the product).
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY: the reference itself, never the product.
+//
+// Two uses, nothing else: (1) minting the golden fixtures under tests/golden/ in this container;
+// (2) the `kind: "reference"` CPU baseline legs of bench.py (time_mul / time_enc), for which the
+// binary built here travels to the GPU box under oracle/_ref/ (git-ignored, not gpurun-ignored).
+// The engine never links, loads or calls it.
 //
 // Compiles the UNMODIFIED header-only reference (pvac-hfhe 0.1.0) from
 // /root/reference/include and drives it deterministically to mint the golden fixtures
@@ -389,6 +394,82 @@ static void cmd_fixtures(const std::string& dir, int npairs, int chain_steps, in
     std::ofstream(dir + "/manifest.json") << js.str();
 }
 
+// ---------------------------------------------------------------- full-range ct_mul fixtures
+// ct_mul on weights outside [0, p): fp_mul (core/field.hpp:113-213) takes any 128-bit operand.
+// Case k (x, y from enc_value, then weights overwritten):
+//   0, 1 : every weight full-range random (both words any u64)
+//   2    : weights cycled over special values (p, p-1, 2^127, 2^128-1, 0, 1, ...)
+//   3    : cancellation: x's edge 1 copies edge 0's (layer, idx, ch) with weight p - w0 (sum 0 mod
+//          p for every key those two reach alone), x's edge 2 weight p (== 0), y's edge 0 weight 0
+//   4    : general-path shape: (x0 * y0) with full-range weights, times a fresh full-range y
+static void cmd_fullrange(const std::string& dir) {
+    reseed(0x5EED0C00ULL);   // the same key as cmd_fixtures
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    reseed(0x5EED0F00ULL);
+    const std::vector<Fp> special = {
+        {MAXU, MASK63} /* p */,          {MAXU - 1, MASK63} /* p-1 */, {0, 1ULL << 63} /* 2^127 */,
+        {MAXU, MAXU} /* 2^128-1 */,      {0, 0},                       {1, 0},
+        {MAXU, 1ULL << 63},              {1, 1ULL << 63} /* p+2 */,    {MAXU, 0},
+        {0x8000000000000000ULL, 0xC000000000000000ULL}, {MAXU - 2, MAXU}, {12345, 0xFFFFFFFF00000000ULL}};
+    auto full = [&](Cipher& C) {
+        for (auto& e : C.E) e.w = Fp{splitmix64_next(), splitmix64_next()};
+    };
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ",\n  \"cases\": [\n";
+    const int ncase = 5;
+    for (int k = 0; k < ncase; ++k) {
+        g_logging = false;
+        Cipher X = enc_value(pk, sk, 11 + (uint64_t)k), Y = enc_value(pk, sk, 17 + (uint64_t)k);
+        if (k <= 1) {
+            full(X);
+            full(Y);
+        } else if (k == 2) {
+            for (size_t i = 0; i < X.E.size(); ++i) X.E[i].w = special[i % special.size()];
+            for (size_t i = 0; i < Y.E.size(); ++i) Y.E[i].w = special[(i * 5 + 3) % special.size()];
+        } else if (k == 3) {
+            full(X);
+            X.E[1].layer_id = X.E[0].layer_id;
+            X.E[1].idx = X.E[0].idx;
+            X.E[1].ch = X.E[0].ch;
+            X.E[1].w = fp_neg(fp_from_words(X.E[0].w.lo, X.E[0].w.hi & MASK63));
+            X.E[2].w = Fp{MAXU, MASK63};
+            Y.E[0].w = Fp{0, 0};
+        } else {
+            full(X);
+            full(Y);
+            Cipher P = ct_mul(pk, X, Y);
+            full(P);
+            for (auto& L : P.L)   // as after a .ct round trip, which drops PROD seeds
+                if (L.rule == RRule::PROD) L.seed = RSeed{};
+            X = std::move(P);
+            Y = enc_value(pk, sk, 23);
+            full(Y);
+        }
+        for (auto& e : X.E) e.s = BitVec::make(0);
+        for (auto& e : Y.E) e.s = BitVec::make(0);
+        g_logging = true;
+        const std::string pre = dir + "/fr" + std::to_string(k);
+        write_ct(pre + "_x.ct", {X}, false);
+        write_ct(pre + "_y.ct", {Y}, false);
+        std::vector<uint64_t> st;
+        Cipher M = run_logged([&] { return ct_mul(pk, X, Y); }, st);
+        write_ct(pre + "_mul_w.ct", {M}, false);
+        write_layers(pre + "_mul_layers.u64", M);
+        write_u64(pre + "_mul_stream.u64", st);
+        js << "    {\"case\": " << k << ", \"nx\": " << X.E.size() << ", \"ny\": " << Y.E.size() << ", \"lx\": "
+           << X.L.size() << ", \"ly\": " << Y.L.size() << ", \"mul_edges\": " << M.E.size() << ", \"mul_layers\": "
+           << M.L.size() << ", \"stream\": " << st.size() << "}" << (k + 1 < ncase ? "," : "") << "\n";
+        std::printf("fullrange case %d: %zu x %zu edges -> %zu\n", k, X.E.size(), Y.E.size(), M.E.size());
+        std::fflush(stdout);
+    }
+    js << "  ],\n  \"generator\": \"oracle/ref_harness.cpp fullrange (reference pvac-hfhe 0.1.0)\"\n}\n";
+    std::ofstream(dir + "/fr_manifest.json") << js.str();
+}
+
 // ---------------------------------------------------------------- timing (CPU baseline leg)
 // Times the reference's own ct_mul (WITH sigma, arithmetic.hpp:47-106) on fresh pairs.
 static void cmd_time_mul(int npairs, int threads) {
@@ -507,6 +588,10 @@ int main(int argc, char** argv) {
         int cs = argc > 4 ? std::atoi(argv[4]) : 3;
         int ss = argc > 5 ? std::atoi(argv[5]) : 2;
         cmd_fixtures(argv[2], np, cs, ss);
+        return 0;
+    }
+    if (cmd == "fullrange" && argc >= 3) {
+        cmd_fullrange(argv[2]);
         return 0;
     }
     if (cmd == "enc" && argc >= 3) {

@@ -79,6 +79,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_ct_mul_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
                                   C.POINTER(CtBatch), u32], i32),
         "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
+        "pvac_hip_ct_mul_status": ([vp, vp, C.c_size_t], i32),
         "pvac_hip_ct_add_plan": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch),
                                   C.POINTER(Plan)], i32),
         "pvac_hip_ct_add_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), i32,
@@ -366,6 +367,12 @@ class Engine:
         v = C.c_uint64(0)
         self._check(self.lib.pvac_hip_ct_mul_redo_count(self.ctx, C.byref(v)))
         return v.value
+
+    def ct_mul_status(self, n):
+        """Per-pair outcome of the last ct_mul (0 hash order, 1 canonical order, 2 rejected)."""
+        out = self.torch.zeros(max(n, 1), dtype=self.torch.int32, device=self.device)
+        self._check(self.lib.pvac_hip_ct_mul_status(self.ctx, C.c_void_p(out.data_ptr()), n))
+        return out.cpu().numpy().view(np.uint32)[:n]
 
     def ct_add(self, A: DeviceBatch, B: DeviceBatch, negate=False, sigma=False):
         torch = self.torch

@@ -64,8 +64,8 @@ inline unsigned plan_grid(uint64_t n) {
 __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_ct_batch B, pvac_ct_batch C,
                                                         uint8_t* pair_class, uint64_t* large_ids, plan_stats* stats,
                                                         const uint32_t* nb_table, uint32_t nb_len, uint32_t Bm) {
-    __shared__ uint32_t red[(kPlanBlock / 64) * 7];
-    uint32_t small = 0, mk = 0, mp = 0, ma = 0, mb = 0, mbk = 0, ml = 0;
+    __shared__ uint32_t red[(kPlanBlock / 64) * 6];
+    uint32_t mk = 0, mp = 0, ma = 0, mb = 0, mbk = 0, ml = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * kPlanBlock) {
         const uint64_t LA = A.l_cnt[i], LB = B.l_cnt[i], nA = A.e_cnt[i], nB = B.e_cnt[i];
         const uint64_t keys = LA * LB * Bm;
@@ -79,7 +79,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
                         nb_table[prod < nb_len ? prod : 0] + prod + 3 <= 3 * keys;   // chains + key sums fit in LDS
         pair_class[i] = sm ? PAIR_SMALL : PAIR_LARGE;
         if (sm) {
-            ++small;
             mk = max(mk, (uint32_t)keys); mp = max(mp, (uint32_t)prod); ma = max(ma, (uint32_t)nA);
             mb = max(mb, (uint32_t)nB); mbk = max(mbk, nb_table[prod]); ml = max(ml, (uint32_t)capL);
         } else {
@@ -87,17 +86,17 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
             large_ids[slot] = i;
         }
     }
-    uint32_t v[7] = {small, mk, mp, ma, mb, mbk, ml};
-    const bool is_sum[7] = {true, false, false, false, false, false, false};
-    block_reduce_stats<7>(v, is_sum, red);
+    // n_small = n - n_large on the host: no per-block count
+    uint32_t v[6] = {mk, mp, ma, mb, mbk, ml};
+    const bool is_sum[6] = {false, false, false, false, false, false};
+    block_reduce_stats<6>(v, is_sum, red);
     if (threadIdx.x == 0) {
-        // n_small = n - n_large on the host: no per-block count
-        max_if_greater(&stats->max_keys, v[1]);
-        max_if_greater(&stats->max_prod, v[2]);
-        max_if_greater(&stats->max_na, v[3]);
-        max_if_greater(&stats->max_nb, v[4]);
-        max_if_greater(&stats->max_buckets, v[5]);
-        max_if_greater(&stats->max_layers, v[6]);
+        max_if_greater(&stats->max_keys, v[0]);
+        max_if_greater(&stats->max_prod, v[1]);
+        max_if_greater(&stats->max_na, v[2]);
+        max_if_greater(&stats->max_nb, v[3]);
+        max_if_greater(&stats->max_buckets, v[4]);
+        max_if_greater(&stats->max_layers, v[5]);
     }
 }
 

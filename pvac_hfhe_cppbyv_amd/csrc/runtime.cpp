@@ -396,6 +396,14 @@ int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* c, uint64_t* out) {
     return PVAC_OK;
 }
 
+int pvac_hip_ct_mul_status(pvac_hip_ctx* c, uint32_t* out, size_t n) {
+    if (!c || (!out && n)) return fail(c, PVAC_EINVAL, "ct_mul_status: bad arguments");
+    if (!n) return PVAC_OK;
+    if (n > c->pair_cap) return fail(c, PVAC_EINVAL, "ct_mul_status: more pairs than the last plan held");
+    const hipError_t e = hipMemcpyAsync(out, c->pair_status, n * 4, hipMemcpyDeviceToDevice, c->stream);
+    return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "ct_mul_status");
+}
+
 const char* pvac_hip_last_error(pvac_hip_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int pvac_hip_timing_enable(pvac_hip_ctx* c, int on) {
@@ -499,8 +507,13 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     plan->n_pairs = A->n;
     C->n = A->n;
     c->large_host.clear();
-    plan->reserved[0] = ++c->plan_stamp;
-    if (!A->n) return PVAC_OK;
+    // every earlier plan goes stale now; this one is stamped valid only once it has succeeded, so
+    // exec rejects a plan whose device work or descriptor build failed
+    const uint32_t stamp = ++c->plan_stamp;
+    if (!A->n) {
+        plan->reserved[0] = stamp;
+        return PVAC_OK;
+    }
     int rc = ensure_pairs(c, A->n);
     if (rc) return rc;
     hipError_t e = hipMemsetAsync(c->stats, 0, sizeof(plan_stats), c->stream);
@@ -547,8 +560,12 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
         std::sort(c->large_host.begin(), c->large_host.end(),
                   [](const large_desc& x, const large_desc& y) { return x.pair < y.pair; });
         rc = plan_static_groups(c);
-        if (rc) return rc;
+        if (rc) {
+            c->large_host.clear();
+            return rc;
+        }
     }
+    plan->reserved[0] = stamp;
     return PVAC_OK;
 }
 

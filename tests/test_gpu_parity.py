@@ -221,6 +221,127 @@ def test_ct_mul_synthetic_vs_oracle(engine, oracle):
             _assert_same(out[p], ref, layers_view=False)
 
 
+def test_ct_mul_full_range_golden(engine):
+    """The reference's own ct_mul outputs on weights anywhere in [0, 2^128) (oracle/ref_harness.cpp
+    fullrange): full-range words, p, p-1, 2^127, 2^128-1, 0, a cancelling key pair (fresh kernel ->
+    redo on the general path) and a general-path shape, all in one batch, byte-exact."""
+    import json
+    from pvac_hfhe_cppbyv_amd import Engine
+    with open(os.path.join(REF, "fr_manifest.json")) as f:
+        fm = json.load(f)
+    eng = Engine(device=0, canon_tag=fm["canon_tag"])
+    ks = range(len(fm["cases"]))
+    xs = [read_ct(os.path.join(REF, f"fr{k}_x.ct"))[0] for k in ks]
+    ys = [read_ct(os.path.join(REF, f"fr{k}_y.ct"))[0] for k in ks]
+    streams = [read_u64(f"fr{k}_mul_stream.u64") for k in ks]
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    assert plan.n_small == 4 and plan.n_large == 1
+    nonces = _nonce_buffer(eng, Cb, xs, ys, streams)
+    redo0 = eng.ct_mul_redo_count()
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+    assert eng.ct_mul_redo_count() - redo0 >= 2   # cases 2 (zero weights) and 3 (cancelling keys)
+    for k in ks:
+        _assert_same(out[k], read_ct(os.path.join(REF, f"fr{k}_mul_w.ct"))[0])
+        full = read_layers_u64(f"fr{k}_mul_layers.u64")
+        for f in ("rule", "pa", "pb", "ztag", "nonce_lo", "nonce_hi"):
+            assert np.array_equal(out[k].layers[f], full[f]), (k, f)
+
+
+_SPECIAL_W = [(2**64 - 1, 2**63 - 1), (2**64 - 2, 2**63 - 1), (0, 2**63), (2**64 - 1, 2**64 - 1), (0, 0), (1, 0),
+              (1, 2**63), (2**64 - 1, 2**63), (2**63, 2**62), (5, 2**64 - 16)]
+
+
+def _full_range_cipher(rng, nl, ne, special_frac=0.15, dup_frac=0.1):
+    """A random cipher whose weights cover [0, 2^128): both words uniform, a share replaced by the
+    special values, and a share of edges that repeat an earlier edge's (layer, idx, ch) with the
+    negated weight (keys whose sums cancel)."""
+    from helpers import LAYER_DT
+    L = np.zeros(nl, LAYER_DT)
+    L["ztag"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+    L["nonce_lo"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+    lay = rng.integers(0, nl, ne).astype(np.uint64)
+    idx = rng.integers(0, 337, ne).astype(np.uint64)
+    ch = rng.integers(0, 2, ne).astype(np.uint64)
+    lo = rng.integers(0, 2**64, ne, dtype=np.uint64)
+    hi = rng.integers(0, 2**64, ne, dtype=np.uint64)
+    for e in np.flatnonzero(rng.random(ne) < special_frac):
+        lo[e], hi[e] = _SPECIAL_W[rng.integers(0, len(_SPECIAL_W))]
+    for e in np.flatnonzero(rng.random(ne) < dup_frac):
+        if e == 0:
+            continue
+        s = int(rng.integers(0, e))
+        lay[e], idx[e], ch[e] = lay[s], idx[s], ch[s]
+        w = ((int(hi[s]) << 64) | int(lo[s])) % P
+        nw = (P - w) % P
+        lo[e], hi[e] = nw & (2**64 - 1), nw >> 64
+    meta = lay | (idx << np.uint64(32)) | (ch << np.uint64(48))
+    return Cipher(L, meta, lo, hi)
+
+
+@pytest.mark.parametrize("shape", ["fresh", "general"])
+def test_ct_mul_full_range_vs_oracle(engine, oracle, shape):
+    """Synthetic full-range weights (lo and hi uniform over u64, the special values p, p-1, 2^127,
+    2^128-1, 0, 1 and cancelling duplicates) through the fresh kernel (2 x 20-edge layers) and the
+    general path (3 x 60 by 2 x 70 edges) vs the oracle, bit-exact incl. emit order."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    rng = np.random.default_rng(0xF011 if shape == "fresh" else 0xF012)
+    eng = Engine(device=0, canon_tag=0x77)
+    if shape == "fresh":
+        n, sa, sb = 1024, (2, 40), (2, 40)
+    else:
+        n, sa, sb = 24, (3, 60), (2, 70)
+    xs = [_full_range_cipher(rng, *sa) for _ in range(n)]
+    ys = [_full_range_cipher(rng, *sb) for _ in range(n)]
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    assert (plan.n_small, plan.n_large) == ((n, 0) if shape == "fresh" else (0, n))
+    nonces = eng.torch.empty(2 * plan.total_layer_slots, dtype=eng.torch.int64, device=eng.device)
+    eng.fill_random(nonces, 0xF00)
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+    nz = nonces.cpu().numpy().view(np.uint64)
+    loff = Cb.l_off.cpu().numpy().view(np.uint64)
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        base = int(loff[p]) + x.nL + y.nL
+        ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0x77)
+        _assert_same(out[p], ref, layers_view=False)
+
+
+def test_ct_mul_rejects_out_of_contract_edges(engine, oracle):
+    """Edges outside the Cipher contract (layer_id >= |X.L|, idx >= B, ch > 1) reject their pair on
+    both paths: status 2 and an empty output (include/pvac_hip.h, pvac_hip_ct_mul_status); the
+    valid pairs of the same batch are unaffected and bit-exact vs the oracle."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    rng = np.random.default_rng(0xBAD)
+    eng = Engine(device=0, canon_tag=0x99)
+    shapes = [((2, 40), (2, 40))] * 4 + [((3, 60), (2, 70))] * 3
+    xs = [_full_range_cipher(rng, *a, dup_frac=0) for a, _ in shapes]
+    ys = [_full_range_cipher(rng, *b, dup_frac=0) for _, b in shapes]
+    u = np.uint64
+    xs[1].meta[5] = (xs[1].meta[5] & ~(u(0xFFFF) << u(32))) | (u(337) << u(32))   # idx == B
+    ys[2].meta[7] = (ys[2].meta[7] & ~(u(0xFF) << u(48))) | (u(2) << u(48))        # ch == 2
+    xs[3].meta[0] = (xs[3].meta[0] & ~u(0xFFFFFFFF)) | u(2)                           # layer_id == |A.L|
+    ys[5].meta[3] = (ys[5].meta[3] & ~(u(0xFFFF) << u(32))) | (u(4000) << u(32))  # idx >> B (general path)
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    assert (plan.n_small, plan.n_large) == (4, 3)
+    nonces = eng.torch.empty(2 * plan.total_layer_slots, dtype=eng.torch.int64, device=eng.device)
+    eng.fill_random(nonces, 0xBAD)
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+    st = eng.ct_mul_status(len(shapes))
+    assert list(st) == [0, 2, 2, 2, 0, 2, 0]
+    host = out.to_host()
+    nz = nonces.cpu().numpy().view(np.uint64)
+    loff = Cb.l_off.cpu().numpy().view(np.uint64)
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        if st[p] == 2:
+            assert host[p].nE == 0 and host[p].nL == 0
+            continue
+        base = int(loff[p]) + x.nL + y.nL
+        ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0x99)
+        _assert_same(host[p], ref, layers_view=False)
+
+
 def test_ct_mul_edge_cases(engine, oracle):
     """Empty ciphers, single-edge ciphers, 1-layer ciphers, and a tiny edge_budget that triggers
     guard_budget -> compact_edges ordering (encrypt.hpp:106-111)."""

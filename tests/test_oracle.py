@@ -109,6 +109,34 @@ def test_ct_add_sub_golden(oracle, manifest, p):
         assert oracle.commit(got, manifest["canon_tag"], H_digest).hex() == manifest["pairs"][p][f"commit_{op}"]
 
 
+def _fr_manifest():
+    import json
+    with open(os.path.join(REF, "fr_manifest.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_ct_mul_full_range_golden(oracle, k):
+    """ct_mul on weights anywhere in [0, 2^128) (fp_mul takes any operand, core/field.hpp:113-213):
+    full-range random words, the special values p, p-1, 2^127, 2^128-1, 0, 1, a cancelling key pair
+    (w, p - w on one key) and a general-path shape; the oracle equals the reference's own output
+    (oracle/ref_harness.cpp fullrange)."""
+    fm = _fr_manifest()
+    x = read_ct(os.path.join(REF, f"fr{k}_x.ct"))[0]
+    y = read_ct(os.path.join(REF, f"fr{k}_y.ct"))[0]
+    stream = read_u64(f"fr{k}_mul_stream.u64")
+    nn = 2 * x.nL * y.nL
+    got = oracle.ct_mul(x, y, stream[:nn], stream[nn:], canon_tag=fm["canon_tag"])
+    ref = read_ct(os.path.join(REF, f"fr{k}_mul_w.ct"))[0]
+    _same(_ct_layers_view(got), ref)
+    full_layers = read_layers_u64(f"fr{k}_mul_layers.u64")
+    for f in ("rule", "pa", "pb", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(got.layers[f], full_layers[f]), f
+    assert len(stream) == nn + got.nE
+    if k <= 1:   # full-range inputs: lo top bits and hi >= 2^63 both occur
+        assert (x.w_hi >= np.uint64(1 << 63)).any() and (x.w_lo >= np.uint64(1 << 63)).any()
+
+
 @pytest.mark.parametrize("p", range(8))
 def test_ct_mul_weights_golden(oracle, manifest, p):
     x, y = _pair(p)
