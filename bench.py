@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
     ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc", "add"], default=None,
                     help="run one side measurement alone (profiling) and print its JSON")
+    ap.add_argument("--check-window", type=int, default=4096,
+                    help="pairs per rank whose digests rank 0 recomputes from global indices (shard check)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     return ap.parse_args()
@@ -193,22 +195,42 @@ def main():
         },
         "cpu_baseline": None,
     }
+    # HBM traffic and VALU instruction count of the same kernel from the committed PMC summary
+    # (tools/prof_pmc.sh), used only when it was taken on this kernel and this batch shape
+    pm = {}
     pmc = os.path.join(ROOT, "profiles", "pmc_ct_mul_fresh.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("pairs") == n and pm.get("epl") == args.epl:
-                result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-                result["roofline"]["traffic_source"] = pm.get("source")
-                # the integer-ALU side of the same kernel (PMC): share of SIMD cycles issuing VALU
-                if pm.get("valu_busy_frac") is not None:
-                    result["roofline"]["valu_busy_frac"] = pm.get("valu_busy_frac")
-                    result["roofline"]["valu_insts_per_pair"] = pm.get("valu_insts_per_launch", 0) / n
+            if pm.get("pairs") != n or pm.get("epl") != args.epl or pm.get("kernel") != FRESH_KERNEL:
+                pm = {}
         except Exception:
-            pass
+            pm = {}
+    if pm:
+        result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+        result["roofline"]["traffic_source"] = pm.get("source")
+    # the integer-ALU roofline of the same kernel: VALU wave-instructions per second (PMC count per
+    # launch / HIP-event kernel time) against the ceiling measured now on this GPU (k_ubench.hip)
+    try:
+        ceil_w = eng.alu_ceiling(0)
+    except Exception:
+        ceil_w = None
+    vi = pm.get("valu_insts_per_launch")
+    if ceil_w and vi and avg_kernel_ms > 0:
+        ach = vi / (avg_kernel_ms / 1000.0)
+        result["roofline"]["valu"] = {
+            "achieved": ach, "peak": ceil_w, "unit": "wave64 VALU inst/s", "frac": ach / ceil_w,
+            "insts_per_pair": vi / n, "lds_bank_conflict_frac": pm.get("lds_bank_conflict_frac"),
+            "source": "SQ_INSTS_VALU per launch (profiles/pmc_ct_mul_fresh.json) / kernel time; peak: "
+                      "pvac_hip_alu_ceiling(0), a v_mad_u64_u32 / v_add_co_u32 / v_alignbit_b32 probe "
+                      "at 8 waves per SIMD on this GPU"}
+    elif ceil_w:
+        result["roofline"]["valu"] = {"peak": ceil_w, "unit": "wave64 VALU inst/s", "achieved": None,
+                                      "note": "no PMC summary for this kernel / batch in profiles/"}
 
-    if rank == 0 and world == 1 and not args.no_cpu:
+    result["checks"] = self_checks(eng, args, A, B, out, nonces, n, first, seed, world, rank)
+    if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(eng, A, B, out, n, args)
     # the cfg-3 batch (~35 GB of inputs, outputs and nonces) is done with: release it so the side
     # measurements (chains size their sub-batches from free HBM) run on an empty device
@@ -226,6 +248,55 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+FRESH_KERNEL = "k_ct_mul_fresh3"   # the fresh-pair kernel launch_ct_mul_fresh runs (k_mul_fresh.hip)
+
+
+def self_checks(eng, args, A, B, out, nonces, n, first, seed, world, rank):
+    """Outside the timed region, on the last step's output of every rank:
+    * the reference's gsum invariant check_mul_gsum_all (utils/metrics.hpp:88-113) on EVERY pair;
+    * shard digests: each rank's index-keyed digest sum (their sum over ranks is the digest of a
+      one-GPU run of the whole global batch) and the per-pair digests of its last `check_window`
+      pairs, all_gathered; rank 0 recomputes every rank's window from the global pair indices and
+      compares (inputs and nonces are keyed by the global index, so a sharded run must match)."""
+    import numpy as np
+    import torch
+    from pvac_hfhe_cppbyv_amd import powg_table
+    from pvac_hfhe_cppbyv_amd.shard import all_gather_u64, combine_digests, shard_digest
+    dev = eng.device
+    eng.set_powg(powg_table(eng.params.B))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    bad = eng.check_mul_gsum(A, B, out, nonces)
+    inv_ms = 1000.0 * (time.perf_counter() - t0)
+    dig = eng.digest(out)[:n].cpu().numpy().view(np.uint64).copy()
+    K = max(1, min(args.check_window, n))
+    edges = int(out.e_cnt[:n].sum().item())
+    head = all_gather_u64([shard_digest(dig, first), bad, edges, first, n], device=dev)
+    wins = all_gather_u64(dig[n - K:], device=dev)
+    failed = int(sum(int(h[1]) for h in head))
+    res = {"gsum_invariant": {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113), every pair of "
+                                       "every rank, on the device (k_check.hip)",
+                              "pairs": int(sum(int(h[4]) for h in head)), "failed": failed, "ok": failed == 0,
+                              "ms_rank0": inv_ms},
+           "global_digest": "%016x" % combine_digests(h[0] for h in head),
+           "global_output_edges": int(sum(int(h[2]) for h in head))}
+    if rank == 0:
+        match = True
+        for r, h in enumerate(head):
+            g0 = int(h[3]) + int(h[4]) - K
+            Aw = eng.gen_fresh(K, seed, args.epl, first_index=g0)
+            Bw = eng.gen_fresh(K, seed + 1, args.epl, first_index=g0)
+            Cw, pw = eng.ct_mul_plan(Aw, Bw)
+            nw = eng.fill_nonces(Aw, Bw, Cw, pw, seed + 2, first_index=g0)
+            ow = eng.ct_mul(Aw, Bw, nonces=nw, C_=Cw, plan=pw)
+            dw = eng.digest(ow)[:K].cpu().numpy().view(np.uint64)
+            match = match and bool(np.array_equal(dw, wins[r]))
+            del Aw, Bw, Cw, ow, nw
+        res["shard_windows"] = {"pairs_per_rank": K, "ranks": world, "recomputed_on": "rank 0", "match": match}
+        res["shard_digests_ok"] = bool(match and failed == 0)
+    return res
 
 
 def cpu_baseline(eng, A, B, out, n, args):
@@ -461,19 +532,14 @@ ENC_STRIDE = 256   # random words per enc_value (the reference draws ~170; statu
 
 def _enc_keys(eng):
     """Synthetic key material for enc_value: random prf_k / LPN secret, H from canon_tag,
-    powg_B = powers of a random element."""
+    powg_B = powers of an element of order B, as keygen makes it (so the gsum invariant holds)."""
     import numpy as np
     P = (1 << 127) - 1
     rng = np.random.default_rng(0xE1C)
     eng.gen_H()
     eng.set_secret(rng.integers(0, 2**64, 4, dtype=np.uint64), rng.integers(0, 2**64, 64, dtype=np.uint64))
-    g = int(rng.integers(2, 2**62)) | 1
-    pg = np.zeros(2 * 337, np.uint64)
-    x = 1
-    for i in range(337):
-        pg[2 * i], pg[2 * i + 1] = x & (2**64 - 1), x >> 64
-        x = x * g % P
-    eng.set_powg(pg)
+    from pvac_hfhe_cppbyv_amd import powg_table
+    eng.set_powg(powg_table(eng.params.B, int(rng.integers(2, 2**62))))
 
 
 def enc_bench(eng, args, with_cpu):
@@ -534,7 +600,7 @@ def chain_bench(eng, args):
     VALU-bound products overlap another chunk's atomic / memory-bound ordering kernels."""
     import threading
     import torch
-    from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine, powg_table
     dev = eng.device
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
     S = max(1, args.chain_streams)
@@ -555,7 +621,8 @@ def chain_bench(eng, args):
         return DeviceBatch(k, X_all.l_off[c0:c0 + k], X_all.l_cnt[c0:c0 + k], X_all.layers, X_all.e_off[c0:c0 + k],
                            X_all.e_cnt[c0:c0 + k], X_all.meta, X_all.w_lo, X_all.w_hi)
 
-    results = [dict(step_ms=[0.0] * depth, step_edges=[0.0] * depth, products=0.0, last_ms=[]) for _ in range(S)]
+    results = [dict(step_ms=[0.0] * depth, step_edges=[0.0] * depth, products=0.0, last_ms=[], gsum_failed=0,
+                    gsum_pairs=0, check_s=0.0) for _ in range(S)]
     ready = threading.Barrier(S + 1)
 
     def warm(e2, stream):
@@ -579,6 +646,7 @@ def chain_bench(eng, args):
             stream = torch.cuda.Stream(dev)
             with torch.cuda.device(dev), torch.cuda.stream(stream):
                 e2 = Engine(device=dev.index, canon_tag=eng.params.canon_tag)   # binds to `stream`
+                e2.set_powg(powg_table(e2.params.B))
                 warm(e2, stream)
                 ready.wait()
                 released = True
@@ -596,6 +664,11 @@ def chain_bench(eng, args):
                         r["step_ms"][d] += 1000.0 * (time.perf_counter() - ts)
                         if d == depth - 1:
                             r["last_ms"].append(round(1000.0 * (time.perf_counter() - ts), 1))
+                        # the gsum invariant on every pair of every step (its time is taken out)
+                        tc = time.perf_counter()
+                        r["gsum_failed"] += e2.check_mul_gsum(cur, X, out, nonces)
+                        r["gsum_pairs"] += k
+                        r["check_s"] += time.perf_counter() - tc
                         r["products"] += float((cur.e_cnt[:k].to(torch.float64) *
                                                 X.e_cnt[:k].to(torch.float64)).sum().item())
                         r["step_edges"][d] += float(out.e_cnt[:k].sum().item())
@@ -622,7 +695,9 @@ def chain_bench(eng, args):
     for t in threads:
         t.join()
     torch.cuda.synchronize(dev)
-    chain_s = time.perf_counter() - t1
+    # minus the untimed invariant checks (workers run them in turn on their own stream)
+    check_s = max(r["check_s"] for r in results)
+    chain_s = time.perf_counter() - t1 - check_s
     del X_all, vals
     errors = [r["error"] for r in results if "error" in r]
     step_ms = [sum(r["step_ms"][d] for r in results) for d in range(depth)]
@@ -636,6 +711,19 @@ def chain_bench(eng, args):
            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
            "edges_per_input_by_step": [e / n for e in step_edges],
            "stream_ms_by_step": step_ms, "last_step_ms_by_chunk": [r["last_ms"] for r in results]}
+    gf, gp = sum(r["gsum_failed"] for r in results), sum(r["gsum_pairs"] for r in results)
+    out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
+                                 "step, on the device (untimed)", "pair_steps": gp, "failed": gf,
+                        "invariant_ok": gf == 0 and gp == n * depth, "check_seconds": check_s}
+    # ALU roofline: lazy products per second against the fp_mul_fold1 ceiling measured on this GPU
+    # (register-resident probe, k_ubench.hip); per product the general path also adds the sum
+    try:
+        ceil = eng.alu_ceiling(1)
+        out["roofline"] = {"bound": "valu", "achieved": products / chain_s, "peak": ceil, "unit": "fp_mul_fold1/s",
+                           "frac": products / chain_s / ceil,
+                           "peak_source": "pvac_hip_alu_ceiling(1): register-resident fp_mul_fold1, 8 waves/SIMD"}
+    except Exception as ex:
+        out["roofline"] = {"error": repr(ex)}
     if errors:
         out["errors"] = errors
     return out

@@ -122,6 +122,10 @@ int pvac_hip_ctx_set_H(pvac_hip_ctx* ctx, const uint64_t* H_dense_host, uint32_t
  * return its H_digest (host, 32 bytes). */
 int pvac_hip_ctx_gen_H(pvac_hip_ctx* ctx, uint8_t digest_out[32]);
 
+/* Measured integer-ALU ceilings of this device for the roofline report (k_ubench.hip), per second:
+ * kind 0 = wave64 integer VALU instructions (v_mad_u64_u32 / v_add_co_u32 / v_alignbit_b32 mix),
+ * 1 = lazy fp_mul_fold1 products (general path), 2 = full fp_mul products. Synchronous. */
+int pvac_hip_alu_ceiling(pvac_hip_ctx* ctx, int kind, double* per_s);
 /* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */
 int pvac_hip_timing_enable(pvac_hip_ctx* ctx, int on);
 /* kernel_name: "fp_binop", "ct_mul_small", "ct_mul_large", "ct_add", "sigma", ... ; returns
@@ -166,6 +170,16 @@ int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* ctx, uint64_t* out);
  * (defined there, out of the Cipher contract: dec_value indexes powg_B[idx]) makes the pair's
  * output empty (l_cnt = e_cnt = 0) instead. */
 int pvac_hip_ct_mul_status(pvac_hip_ctx* ctx, uint32_t* out, size_t n);
+/* The reference's ct_mul invariant check_mul_gsum_all (utils/metrics.hpp:88-113) on every pair of
+ * a batch: gsum(C, product layer of (la, lb)) == gsum(A, la) * gsum(B, lb) with
+ * gsum(X, l) = sum of +/- w * powg_B[idx] over X's edges in layer l (metrics.hpp:70-86). C is a
+ * ct_mul_exec output of (A, B) with `nonces`: a product layer is identified by the nonce it
+ * carries (compact_layers renumbers C's layers); a dropped product layer must have a zero product.
+ * Needs pvac_hip_ctx_set_powg. status (nullable, DEVICE, n u32): 0 holds, 1 violated, 2 an edge
+ * idx >= B, 3 a cipher of more than 2^21 edges (not checked). *n_bad (host) = pairs with status != 0.
+ * Synchronous. */
+int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, const pvac_ct_batch* C,
+                            const uint64_t* nonces, uint32_t* status, uint64_t* n_bad);
 
 /* ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45; combine_ciphers ops/encrypt.hpp:260-279).
  * negate_b != 0 gives ct_sub (B's weights scaled by p-1). Dense CSR output: the plan writes

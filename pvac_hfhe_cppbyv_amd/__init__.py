@@ -35,6 +35,25 @@ class PvacError(RuntimeError):
     pass
 
 
+def powg_table(B: int = 337, h: int = 3):
+    """powg_B of a key as keygen builds it (crypto/keygen.hpp:67-95): g = h^((p-1)/B) for the first
+    h >= `h` with g != 1, powg[i] = g^i, as B (lo, hi) u64 pairs. g^B == 1, which the gsum invariant
+    (check_mul_gsum) relies on."""
+    if (P - 1) % B:
+        raise ValueError("B must divide p - 1")
+    while True:
+        g = pow(h, (P - 1) // B, P)
+        if g != 1:
+            break
+        h += 1
+    out = np.zeros(2 * B, np.uint64)
+    x = 1
+    for i in range(B):
+        out[2 * i], out[2 * i + 1] = x & (2**64 - 1), x >> 64
+        x = x * g % P
+    return out
+
+
 class Params(C.Structure):
     _fields_ = [("B", C.c_uint32), ("m_bits", C.c_uint32), ("n_bits", C.c_uint32), ("h_col_wt", C.c_uint32),
                 ("x_col_wt", C.c_uint32), ("err_wt", C.c_uint32), ("edge_budget", C.c_uint64),
@@ -80,6 +99,9 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
                                   C.POINTER(CtBatch), u32], i32),
         "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ct_mul_status": ([vp, vp, C.c_size_t], i32),
+        "pvac_hip_alu_ceiling": ([vp, i32, C.POINTER(C.c_double)], i32),
+        "pvac_hip_check_mul_gsum": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
+                                     C.POINTER(u64)], i32),
         "pvac_hip_ct_add_plan": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch),
                                   C.POINTER(Plan)], i32),
         "pvac_hip_ct_add_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), i32,
@@ -373,6 +395,26 @@ class Engine:
         out = self.torch.zeros(max(n, 1), dtype=self.torch.int32, device=self.device)
         self._check(self.lib.pvac_hip_ct_mul_status(self.ctx, C.c_void_p(out.data_ptr()), n))
         return out.cpu().numpy().view(np.uint32)[:n]
+
+    def alu_ceiling(self, kind):
+        """Measured ops/s: 0 wave64 integer VALU instructions, 1 fp_mul_fold1, 2 fp_mul products."""
+        v = C.c_double(0)
+        self._check(self.lib.pvac_hip_alu_ceiling(self.ctx, kind, C.byref(v)))
+        return v.value
+
+    def check_mul_gsum(self, A: DeviceBatch, B: DeviceBatch, C_: DeviceBatch, nonces, status=False):
+        """The reference's gsum invariant (utils/metrics.hpp:88-113) on every pair of a ct_mul
+        batch; needs set_powg. Returns the number of failing pairs (and per-pair status)."""
+        torch = self.torch
+        st = torch.zeros(max(A.n, 1), dtype=torch.int32, device=self.device) if status else None
+        bad = C.c_uint64(0)
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        self._check(self.lib.pvac_hip_check_mul_gsum(self.ctx, C.byref(sa), C.byref(sb), C.byref(sc),
+                                                     C.c_void_p(nonces.data_ptr()),
+                                                     C.c_void_p(st.data_ptr()) if status else None, C.byref(bad)))
+        if status:
+            return bad.value, st.cpu().numpy().view(np.uint32)[:A.n]
+        return bad.value
 
     def ct_add(self, A: DeviceBatch, B: DeviceBatch, negate=False, sigma=False):
         torch = self.torch

@@ -297,6 +297,14 @@ struct mul_large_args {
     uint64_t max_S, max_zero, max_tasks, max_capE, max_lay;
 };
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
+// measured integer-ALU ceilings (k_ubench.hip)
+hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s);
+// ct_mul gsum invariant (k_check.hip, utils/metrics.hpp:70-113)
+hipError_t launch_check_sizes(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C, unsigned int* mx,
+                              hipStream_t st);
+hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C, const uint64_t* nonces,
+                             const uint64_t* powg, uint32_t Bm, const unsigned int* mx_host, uint32_t* status,
+                             unsigned long long* n_bad, int num_cus, hipStream_t st);
 constexpr uint64_t kNoGrp = ~0ull;
 // static bucket groups of key slots [0, S) for one bucket count: head[s] = 0 when s is alone in
 // its bucket, else the first slot + 1 of the bucket's chain; next[s] = the following slot + 1

@@ -1,0 +1,129 @@
+// k_ubench.hip — measured integer-ALU ceilings for the roofline report (bench.py).
+//
+// The hot kernels are integer-VALU work, so their roofline needs an ALU ceiling next to the HBM
+// one. Rather than a cycles-per-instruction constant, the ceiling is measured on the device that
+// runs the bench, in the same process:
+//   kind 0: wave64 integer VALU instructions per second, chip-wide: 8 independent chains of
+//           v_mad_u64_u32 / v_add_co_u32 / v_alignbit_b32 (the fp_mul mix) in inline asm, so the
+//           count per iteration is exact; loop control is scalar (SALU)
+//   kind 1: lazy products fp_mul_fold1 (the general path's per-product multiply) per second,
+//           register resident, 4 independent chains per lane
+//   kind 2: full fp_mul (two folds + canonical form) per second, as kind 1
+// Grids fill every CU at 8 waves per SIMD. Used by measurement only, never by the ct_* ops.
+#include "common.hpp"
+
+namespace pvhip {
+namespace {
+
+constexpr int kUB = 256;
+
+__global__ __launch_bounds__(kUB) void k_probe_valu(uint64_t* out, uint32_t iters, uint32_t seed) {
+    const uint32_t a = threadIdx.x ^ seed, b = a * 2654435761u + 1u;
+    uint64_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = ((uint64_t)(a + k) << 32) | (b ^ k);
+    uint32_t y[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = a * (k + 3);
+    for (uint32_t i = 0; i < iters; ++i) {
+        // 24 VALU instructions per iteration: 8 x (mad, add_co, alignbit), independent chains
+        asm volatile(
+            "v_mad_u64_u32 %0, vcc, %16, %17, %0\n\t"
+            "v_mad_u64_u32 %1, vcc, %16, %17, %1\n\t"
+            "v_mad_u64_u32 %2, vcc, %16, %17, %2\n\t"
+            "v_mad_u64_u32 %3, vcc, %16, %17, %3\n\t"
+            "v_mad_u64_u32 %4, vcc, %16, %17, %4\n\t"
+            "v_mad_u64_u32 %5, vcc, %16, %17, %5\n\t"
+            "v_mad_u64_u32 %6, vcc, %16, %17, %6\n\t"
+            "v_mad_u64_u32 %7, vcc, %16, %17, %7\n\t"
+            "v_add_co_u32 %8, vcc, %8, %16\n\t"
+            "v_add_co_u32 %9, vcc, %9, %16\n\t"
+            "v_add_co_u32 %10, vcc, %10, %16\n\t"
+            "v_add_co_u32 %11, vcc, %11, %16\n\t"
+            "v_add_co_u32 %12, vcc, %12, %17\n\t"
+            "v_add_co_u32 %13, vcc, %13, %17\n\t"
+            "v_add_co_u32 %14, vcc, %14, %17\n\t"
+            "v_add_co_u32 %15, vcc, %15, %17\n\t"
+            "v_alignbit_b32 %8, %9, %8, 7\n\t"
+            "v_alignbit_b32 %9, %10, %9, 7\n\t"
+            "v_alignbit_b32 %10, %11, %10, 7\n\t"
+            "v_alignbit_b32 %11, %12, %11, 7\n\t"
+            "v_alignbit_b32 %12, %13, %12, 7\n\t"
+            "v_alignbit_b32 %13, %14, %13, 7\n\t"
+            "v_alignbit_b32 %14, %15, %14, 7\n\t"
+            "v_alignbit_b32 %15, %8, %15, 7"
+            : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+              "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7])
+            : "v"(a), "v"(b)
+            : "vcc");
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r ^= x[k] ^ y[k];
+    out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
+}
+
+template <bool FULL>
+__global__ __launch_bounds__(kUB) void k_probe_mul(uint64_t* out, uint32_t iters, uint32_t seed) {
+    const uint64_t s = ((uint64_t)(threadIdx.x ^ seed) << 17) | blockIdx.x;
+    fp y{s * 0x9E3779B97F4A7C15ull, (s * 0xBF58476D1CE4E5B9ull) & kM63};
+    fp x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = fp{s + k, (s >> 3) & kM63};
+    for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (FULL) {
+                x[k] = fp_mul(x[k], y);
+            } else {
+                uint64_t l, h;
+                fp_mul_fold1(x[k], y, l, h);
+                x[k] = fp{l, h & kM63};   // keep the operand below 2^127 (one VALU op)
+            }
+        }
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r ^= x[k].lo ^ x[k].hi;
+    out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
+}
+
+}  // namespace
+
+// ops per second of probe `kind` (see above), timed with HIP events on `st` (synchronises)
+hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s) {
+    const uint32_t blocks = (uint32_t)num_cus * 8u;   // 8 waves per SIMD (4 SIMDs, 4 waves per block)
+    uint64_t* buf = nullptr;
+    hipError_t e = hipMalloc(&buf, (size_t)blocks * kUB * 8);
+    if (e != hipSuccess) return e;
+    hipEvent_t t0, t1;
+    hipEventCreate(&t0);
+    hipEventCreate(&t1);
+    const uint32_t iters = kind == 0 ? 4096u : 512u;
+    double ops = 0;
+    float ms = 0;
+    for (int rep = 0; rep < 2; ++rep) {   // the first launch warms clocks and code
+        hipEventRecord(t0, st);
+        if (kind == 0) {
+            hipLaunchKernelGGL(k_probe_valu, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
+            ops = (double)blocks * (kUB / 64) * iters * 24.0;   // wave64 instructions
+        } else if (kind == 1) {
+            hipLaunchKernelGGL(k_probe_mul<false>, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
+            ops = (double)blocks * kUB * iters * 4.0;           // lane products
+        } else {
+            hipLaunchKernelGGL(k_probe_mul<true>, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
+            ops = (double)blocks * kUB * iters * 4.0;
+        }
+        hipEventRecord(t1, st);
+    }
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventSynchronize(t1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    hipFree(buf);
+    if (e == hipSuccess) *per_s = ms > 0 ? ops / (ms / 1000.0) : 0.0;
+    return e;
+}
+
+}  // namespace pvhip

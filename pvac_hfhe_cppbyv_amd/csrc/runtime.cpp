@@ -97,6 +97,7 @@ struct pvac_hip_ctx {
     uint64_t* scan_scratch = nullptr;
     size_t scan_cap = 0;
     plan_stats* stats = nullptr;
+    unsigned int* check_buf = nullptr;   // gsum check: 4 layer maxima, then a u64 failure count
     unsigned long long* totals = nullptr;   // [2]
     sigma_tables H;
     // timing
@@ -361,6 +362,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->dec_roff);
     hipFree(c->scan_scratch);
     hipFree(c->stats);
+    hipFree(c->check_buf);
     hipFree(c->totals);
     sigma_tables_free(c->H);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -1122,6 +1124,41 @@ int pvac_hip_base_R(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* R_out) {
     if (rc) return rc;
     scoped_timer t(c, "base_R");
     return hip_fail(c, launch_base_R(k, *X, slots, c->prf_req, c->prf_core, R_out, c->stream), "base_R");
+}
+
+// ---------------------------------------------------------------- measured ALU ceilings
+int pvac_hip_alu_ceiling(pvac_hip_ctx* c, int kind, double* per_s) {
+    if (!c || !per_s || kind < 0 || kind > 2) return fail(c, PVAC_EINVAL, "alu_ceiling: bad arguments");
+    const hipError_t e = run_alu_probe(kind, c->num_cus, c->stream, per_s);
+    return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "alu_ceiling");
+}
+
+// ---------------------------------------------------------------- gsum invariant
+int pvac_hip_check_mul_gsum(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, const pvac_ct_batch* C,
+                            const uint64_t* nonces, uint32_t* status, uint64_t* n_bad) {
+    if (!c || !n_bad || !batch_ok(A) || !batch_ok(B) || !batch_ok(C) || !nonces)
+        return fail(c, PVAC_EINVAL, "check_mul_gsum: bad arguments");
+    if (A->n != B->n || A->n != C->n) return fail(c, PVAC_EINVAL, "check_mul_gsum: batch sizes differ");
+    if (!c->powg) return fail(c, PVAC_EINVAL, "check_mul_gsum: powg_B not set (pvac_hip_ctx_set_powg)");
+    *n_bad = 0;
+    if (!A->n) return PVAC_OK;
+    hipError_t e = hipSuccess;
+    if (!c->check_buf) e = hipMalloc(&c->check_buf, 32);
+    if (e == hipSuccess) e = hipMemsetAsync(c->check_buf, 0, 32, c->stream);
+    if (e == hipSuccess) e = launch_check_sizes(*A, *B, *C, c->check_buf, c->stream);
+    unsigned int mx[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(mx, c->check_buf, sizeof mx, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "check_mul_gsum (sizes)");
+    unsigned long long* cnt = (unsigned long long*)(c->check_buf + 4);
+    e = launch_check_gsum(*A, *B, *C, nonces, c->powg, c->prm.B, mx, status, cnt, c->num_cus, c->stream);
+    if (e == hipErrorInvalidValue) return fail(c, PVAC_ERANGE, "check_mul_gsum: a pair's layer tables exceed LDS");
+    unsigned long long bad = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, cnt, sizeof bad, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "check_mul_gsum");
+    *n_bad = bad;
+    return PVAC_OK;
 }
 
 // ---------------------------------------------------------------- dec_value

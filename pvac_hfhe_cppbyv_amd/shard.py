@@ -7,6 +7,11 @@ Engine.fill_nonces(first_index=...)), so the union of the shards equals a single
 collective is the all_gather of per-rank output-edge totals, which places each shard in the global
 (sharded) CSR of the result — BASELINE cfg 5's "gather-only". Works on any torch.distributed backend
 (RCCL "nccl" on the GPU node, "gloo" in CPU tests).
+
+Self-check of a sharded run (bench.py): every rank folds its per-pair output digests into one
+order-independent, index-keyed sum (shard_digest), so the sum over ranks equals the digest of one
+single-GPU run of the whole global batch; ranks all_gather those sums and the digests of a window of
+their pairs, which rank 0 recomputes from the global pair indices (all_gather_u64).
 """
 from __future__ import annotations
 
@@ -57,3 +62,43 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+_M64 = (1 << 64) - 1
+
+
+def shard_digest(pair_digests, first_index: int) -> int:
+    """sum_i mix(d_i, first_index + i) mod 2^64 over a shard's per-pair digests (numpy u64): keyed by
+    the GLOBAL pair index and additive over disjoint shards."""
+    import numpy as np
+    d = np.ascontiguousarray(pair_digests, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        g = np.arange(first_index, first_index + len(d), dtype=np.uint64)
+        z = d + g * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return int(z.sum(dtype=np.uint64))
+
+
+def combine_digests(ds) -> int:
+    return sum(int(x) for x in ds) & _M64
+
+
+def all_gather_u64(values, device=None):
+    """all_gather of an equal-length u64 vector from every rank -> list (per rank) of numpy u64.
+    Single process: [values]."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    v = np.ascontiguousarray(values, dtype=np.uint64)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [v.copy()]
+    world = dist.get_world_size()
+    if dist.get_backend() == "gloo":
+        device = "cpu"
+    mine = torch.from_numpy(v.view(np.int64).copy()).to(device)
+    allt = torch.zeros(world * len(v), dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(allt, mine)
+    a = allt.cpu().numpy().view(np.uint64)
+    return [a[r * len(v):(r + 1) * len(v)].copy() for r in range(world)]

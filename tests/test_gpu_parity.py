@@ -246,6 +246,14 @@ def test_ct_mul_full_range_golden(engine):
         full = read_layers_u64(f"fr{k}_mul_layers.u64")
         for f in ("rule", "pa", "pb", "ztag", "nonce_lo", "nonce_hi"):
             assert np.array_equal(out[k].layers[f], full[f]), (k, f)
+    # the reference's gsum invariant (utils/metrics.hpp:88-113) on the device, with the fixture
+    # key's powg_B; then one corrupted output weight must be caught at its pair
+    eng.set_powg(read_u64("powg_B.u64"))
+    assert eng.check_mul_gsum(A, B, Cb, nonces) == 0
+    eo = int(Cb.e_off[3].item())
+    Cb.w_lo[eo + 7] ^= 1
+    bad, st = eng.check_mul_gsum(A, B, Cb, nonces, status=True)
+    assert bad == 1 and list(st) == [0, 0, 0, 1, 0]
 
 
 _SPECIAL_W = [(2**64 - 1, 2**63 - 1), (2**64 - 2, 2**63 - 1), (0, 2**63), (2**64 - 1, 2**64 - 1), (0, 0), (1, 0),
@@ -432,9 +440,9 @@ def _pair_host(X, p):
 
 def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     """BASELINE cfg 3 at its full size (2^20 fresh-shaped pairs, the bench's batch and generator):
-    512 pairs spread over the whole batch bit-exact vs the oracle (weights, emit order, layers incl.
-    ztags), every pair within its planned capacity with status 0, and a second run of the same
-    batch identical (per-pair device digests)."""
+    the reference's gsum invariant on every pair, 512 pairs spread over the whole batch bit-exact
+    vs the oracle (weights, emit order, layers incl. ztags), every pair within its planned capacity
+    with status 0, and a second run of the same batch identical (per-pair device digests)."""
     from pvac_hfhe_cppbyv_amd import Engine
     eng = Engine(device=0, canon_tag=0x5EED0003)
     n = 1 << 20
@@ -448,6 +456,9 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     cap = np.diff(np.append(eoff, np.uint64(plan.total_edge_slots)))
     assert (ecnt <= cap).all() and ecnt.min() > 0
     dig1 = u(eng.digest(out)[:n]).copy()
+    # the reference's gsum invariant (utils/metrics.hpp:88-113) on every one of the 2^20 pairs
+    eng.set_powg(read_u64("powg_B.u64"))
+    assert eng.check_mul_gsum(A, B, out, nonces) == 0
     rng = np.random.default_rng(3)
     picks = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 510)]))
     nz = nonces.cpu().numpy().view(np.uint64)

@@ -26,3 +26,37 @@ def test_two_shards_equal_one_batch():
     d1, l1 = run(n // 2, n - n // 2)
     assert np.array_equal(np.concatenate([d0, d1]), d_all)
     assert l0 + l1 == l_all
+
+
+def _bench_json(args, world, port=None):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PVAC_BENCH_BACKEND="gloo")
+    if world == 1:
+        cmd = [sys.executable, os.path.join(root, "bench.py")] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py")] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_world2_shard_digests_equal_one_gpu():
+    """bench.py's N>1 path on one GPU: two ranks (gloo for the gathers, both on cuda:0) each run
+    their shard of the global batch; rank 0 recomputes both ranks' pair windows from the global
+    indices, the gsum invariant holds on every pair, and the gathered digest equals a one-rank run
+    of the same 2 x 4096 pairs."""
+    from test_shard_dist import _free_port
+    common = ["--steps", "1", "--warmup", "0", "--no-cpu", "--no-extras", "--check-window", "512"]
+    two = _bench_json(["--gpus", "2", "--pairs", "4096"] + common, 2, _free_port())
+    one = _bench_json(["--gpus", "1", "--pairs", "8192"] + common, 1)
+    c2, c1 = two["checks"], one["checks"]
+    assert two["n_gpus"] == 2 and c2["shard_digests_ok"] and c2["shard_windows"]["ranks"] == 2
+    assert c2["gsum_invariant"]["ok"] and c2["gsum_invariant"]["pairs"] == 8192
+    assert c1["shard_digests_ok"] and c1["gsum_invariant"]["pairs"] == 8192
+    assert c2["global_digest"] == c1["global_digest"]
+    assert c2["global_output_edges"] == c1["global_output_edges"]

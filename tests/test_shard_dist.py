@@ -41,7 +41,11 @@ def _worker(rank, world, port, n_total, q):
     sizes = [1190 + (g * 7919) % 53 for g in range(start, start + count)]
     off, total, per = global_edge_offsets(sum(sizes))
     slow = max_over_ranks(0.5 + rank)
-    q.put((rank, start, count, off, total, per, slow))
+    from pvac_hfhe_cppbyv_amd.shard import all_gather_u64, shard_digest
+    import numpy as np
+    dig = np.array([(g * 0x9E3779B97F4A7C15) & (2**64 - 1) for g in range(start, start + count)], np.uint64)
+    heads = all_gather_u64([shard_digest(dig, start), count, 2**64 - 1 - rank])
+    q.put((rank, start, count, off, total, per, slow, [list(map(int, h)) for h in heads]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,8 +65,14 @@ def test_gloo_world2_global_offsets():
         assert p.exitcode == 0
     full = [1190 + (g * 7919) % 53 for g in range(n_total)]
     offs, total = exclusive_offsets([sum(full[s:s + c]) for _, s, c, *_ in res])
-    for (rank, s, c, off, tot, per, slow), want in zip(res, offs):
+    import numpy as np
+    from pvac_hfhe_cppbyv_amd.shard import combine_digests, shard_digest
+    dig_all = np.array([(g * 0x9E3779B97F4A7C15) & (2**64 - 1) for g in range(n_total)], np.uint64)
+    for (rank, s, c, off, tot, per, slow, heads), want in zip(res, offs):
         assert off == want                 # this shard's place in the global edge CSR
         assert tot == total == sum(full)   # grand total agrees on every rank
         assert slow == 1.5                 # max over ranks
+        # u64 all_gather (full 64-bit range) and the index-keyed shard digests add up to the whole
+        assert [h[2] for h in heads] == [2**64 - 1, 2**64 - 2] and [h[1] for h in heads] == [res[0][2], res[1][2]]
+        assert combine_digests(h[0] for h in heads) == shard_digest(dig_all, 0)
     assert res[0][1] == 0 and res[1][1] == res[0][2]

@@ -4,7 +4,10 @@
 FETCH_SIZE/WRITE_SIZE are reported in KB by rocprofv3; HBM bytes per launch follow the
 MI355X guide's correction: FETCH_SIZE counts 64 B per 128-B request for wide streaming reads,
 so the read side is doubled (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is taken as is.
-valu_busy_frac = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x kernel cycles): the integer-ALU roofline."""
+No cycles-per-instruction constant: the VALU roofline divides SQ_INSTS_VALU per launch by the kernel
+time and by the ceiling measured on the device (pvac_hip_alu_ceiling, bench.py roofline.valu).
+lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / (256 CUs x kernel cycles), wait_frac =
+SQ_WAIT_ANY / SQ_WAVE_CYCLES."""
 import csv
 import glob
 import json
@@ -39,10 +42,14 @@ def main(root):
             m["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             m["hbm_bytes_per_launch"] = m["hbm_read_bytes_corrected"] + m["hbm_write_bytes"]
-        if "SQ_INSTS_VALU" in m and m.get("GRBM_GUI_ACTIVE"):
-            # a wave64 VALU instruction holds its 16-lane SIMD for 4 cycles; GRBM_GUI_ACTIVE sums the
-            # 8 XCDs' clocks; 256 CUs x 4 SIMDs
-            m["valu_busy_frac"] = m["SQ_INSTS_VALU"] * 4.0 / (1024.0 * m["GRBM_GUI_ACTIVE"] / 8.0)
+        if m.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE sums the 8 XCDs' clocks: kernel cycles = GRBM_GUI_ACTIVE / 8
+            cyc = m["GRBM_GUI_ACTIVE"] / 8.0
+            m["kernel_cycles"] = cyc
+            if "SQ_LDS_BANK_CONFLICT" in m:
+                m["lds_bank_conflict_frac"] = m["SQ_LDS_BANK_CONFLICT"] / (256.0 * cyc)
+        if m.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in m:
+            m["wait_frac"] = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
 

@@ -47,14 +47,17 @@ python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.json" && cat "$OUT/s
 python3 - "$OUT/summary.json" "$OUT/pmc_ct_mul_fresh.json" "$@" <<'PY'
 import json, sys
 summ = json.load(open(sys.argv[1]))
-k = summ.get("k_ct_mul_fresh")
+name = next((x for x in ("k_ct_mul_fresh3", "k_ct_mul_fresh") if x in summ), None)
+k = summ.get(name) if name else None
 args = sys.argv[3:]
 pairs = int(args[args.index("--pairs") + 1]) if "--pairs" in args else 1 << 20
 epl = int(args[args.index("--epl") + 1]) if "--epl" in args else 20
 if k and "hbm_bytes_per_launch" in k:
-    json.dump({"pairs": pairs, "epl": epl, "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
+    json.dump({"kernel": name, "pairs": pairs, "epl": epl, "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
                "hbm_read_bytes": k["hbm_read_bytes_corrected"], "hbm_write_bytes": k["hbm_write_bytes"],
-               "valu_busy_frac": k.get("valu_busy_frac"), "valu_insts_per_launch": k.get("SQ_INSTS_VALU"),
+               "valu_insts_per_launch": k.get("SQ_INSTS_VALU"), "lds_insts_per_launch": k.get("SQ_INSTS_LDS"),
+               "lds_bank_conflict_frac": k.get("lds_bank_conflict_frac"), "wait_frac": k.get("wait_frac"),
+               "kernel_cycles": k.get("kernel_cycles"),
                "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) / WRITE_SIZE, "
                          "mean per dispatch; tools/prof_pmc.sh"}, open(sys.argv[2], "w"), indent=1)
 PY
