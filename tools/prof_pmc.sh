@@ -12,7 +12,16 @@ shift || true
 OUT="$ROOT/gpurun_out/pmc"
 mkdir -p "$OUT"
 BENCH=(python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu --no-extras "$@")
-if [ "${PMC_SET:-}" = "detail" ]; then
+if [ "${PMC_SET:-}" = "cache" ]; then
+  # memory-side view: L2 hits / misses, HBM-side fetch, LDS and VALU issue
+  passes=(
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD"
+    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_SMEM"
+    "FETCH_SIZE"
+    "TCC_HIT_sum TCC_MISS_sum"
+    "GRBM_GUI_ACTIVE GRBM_COUNT"
+  )
+elif [ "${PMC_SET:-}" = "detail" ]; then
   # issue/stall attribution (no HBM passes)
   passes=(
     "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS"
