@@ -180,7 +180,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_ct_mul_fresh",
+            "kernel": FRESH_KERNEL,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
