@@ -440,7 +440,8 @@ def _pair_host(X, p):
 
 def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     """BASELINE cfg 3 at its full size (2^20 fresh-shaped pairs, the bench's batch and generator):
-    the reference's gsum invariant on every pair, 512 pairs spread over the whole batch bit-exact
+    every reported output slot written by this launch (sentinel-filled outputs), the reference's
+    gsum invariant on every pair, 512 pairs spread over the whole batch bit-exact
     vs the oracle (weights, emit order, layers incl. ztags), every pair within its planned capacity
     with status 0, and a second run of the same batch identical (per-pair device digests)."""
     from pvac_hfhe_cppbyv_amd import Engine
@@ -450,7 +451,17 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     B = eng.gen_fresh(n, 0x5EED0004, 20)
     Cb, plan = eng.ct_mul_plan(A, B)
     nonces = eng.fill_nonces(A, B, Cb, plan, 0x5EED0005)
+    # outputs pre-filled with a sentinel no record can hold (meta ch byte, w_hi top bit): every
+    # reported edge and layer slot must have been written by this launch, not left from an earlier one
+    torch = eng.torch
+    es, ls = plan.total_edge_slots, plan.total_layer_slots
+    Cb.layers = torch.full((ls, 5), -1, dtype=torch.int64, device=eng.device)
+    Cb.meta, Cb.w_lo, Cb.w_hi = (torch.full((es,), -1, dtype=torch.int64, device=eng.device) for _ in range(3))
     out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+    tot_e, tot_l = int(out.e_cnt[:n].sum().item()), int(out.l_cnt[:n].sum().item())
+    for t in (out.meta, out.w_lo, out.w_hi):
+        assert int((t != -1).sum().item()) == tot_e
+    assert int((out.layers[:, 1] != -1).sum().item()) == tot_l
     u = lambda t: t.cpu().numpy().view(np.uint64)
     ecnt, eoff = u(out.e_cnt[:n]), u(out.e_off[:n])
     cap = np.diff(np.append(eoff, np.uint64(plan.total_edge_slots)))
