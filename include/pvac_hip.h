@@ -246,6 +246,16 @@ int pvac_hip_prf(pvac_hip_ctx* ctx, int kind, size_t n, const uint64_t* seeds, u
 int pvac_hip_enc_caps(pvac_hip_ctx* ctx, uint32_t* layers_per_value, uint32_t* edges_per_value, uint32_t* draws_hint);
 int pvac_hip_enc_value(pvac_hip_ctx* ctx, size_t n, const uint64_t* values, const uint64_t* rnd, uint32_t rnd_stride,
                        pvac_ct_batch* C, uint32_t flags, uint32_t* status);
+/* enc_value_depth(pk, sk, v, depth_hint) (ops/encrypt.hpp:281-287): as pvac_hip_enc_value with the
+ * noise plan of depth_hint (plan_noise, encrypt.hpp:16-27: more Z2 / Z3 groups as the hint grows;
+ * supported while 8 + 2 Z2 + 3 Z3 <= 48, i.e. depth_hint <= 15 with the default Params, else
+ * PVAC_ENOSYS). values[i] = 0 gives enc_zero_depth(pk, sk, depth_hint) (encrypt.hpp:293-298)
+ * byte for byte: fp_add(0, mask) is mask and the draws are the same. Size outputs and rnd_stride with
+ * pvac_hip_enc_caps_depth. */
+int pvac_hip_enc_caps_depth(pvac_hip_ctx* ctx, int depth_hint, uint32_t* layers_per_value, uint32_t* edges_per_value,
+                            uint32_t* draws_hint);
+int pvac_hip_enc_value_depth(pvac_hip_ctx* ctx, size_t n, const uint64_t* values, const uint64_t* rnd, uint32_t rnd_stride,
+                             int depth_hint, pvac_ct_batch* C, uint32_t flags, uint32_t* status);
 /* prf_R of every BASE layer of X (ops/decrypt.hpp:44-46): R_out device, 2 words per layer SLOT
  * (slots addressed by l_off/l_cnt; PROD slots get 0) — the R_base input of pvac_hip_dec_value. */
 int pvac_hip_base_R(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* R_out);

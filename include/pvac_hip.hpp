@@ -418,19 +418,20 @@ public:
     // value encrypted from a replayed getrandom stream is byte-identical to the reference's; the
     // source is advanced by the whole stride. A value whose rejection sampling outruns its stride
     // (status 1, never seen in practice) is re-run with its own draws extended, prefix kept.
+    // depth_hint > 0: enc_value_depth (encrypt.hpp:281-287); a value of 0 is enc_zero_depth (:293-298).
     template <class PubKeyT, class SecKeyT, class CipherT>
     std::vector<CipherT> enc_value(const PubKeyT& pk, const SecKeyT& sk, const std::vector<uint64_t>& vs,
-                                   bool with_sigma, const RandomSource& rnd) {
+                                   bool with_sigma, const RandomSource& rnd, int depth_hint = 0) {
         const size_t n = vs.size();
         if (!n) return {};
         ensure_keys(pk, sk);
         if (with_sigma) ensure_H(pk);
         uint32_t lpv = 0, epv = 0, stride = 0;
-        check(pvac_hip_enc_caps(ctx_, &lpv, &epv, &stride));
+        check(pvac_hip_enc_caps_depth(ctx_, depth_hint, &lpv, &epv, &stride));
         std::vector<uint64_t> draws((size_t)n * stride);
         for (auto& x : draws) x = rnd();
         std::vector<uint32_t> status;
-        std::vector<CipherT> out = enc_run<CipherT>(vs, draws, stride, lpv, epv, with_sigma, status);
+        std::vector<CipherT> out = enc_run<CipherT>(vs, draws, stride, lpv, epv, with_sigma, status, depth_hint);
         for (uint32_t grow = stride; ; grow *= 2) {
             std::vector<size_t> redo;
             for (size_t i = 0; i < n; ++i) {
@@ -447,7 +448,7 @@ public:
                 for (uint32_t j = stride; j < s2; ++j) d2[k * s2 + j] = rnd();
             }
             std::vector<uint32_t> st2;
-            std::vector<CipherT> o2 = enc_run<CipherT>(v2, d2, s2, lpv, epv, with_sigma, st2);
+            std::vector<CipherT> o2 = enc_run<CipherT>(v2, d2, s2, lpv, epv, with_sigma, st2, depth_hint);
             // the redone values' draws become their prefix for a further round
             std::vector<uint64_t> nd((size_t)n * s2, 0);
             for (size_t i = 0; i < n; ++i) std::memcpy(&nd[i * s2], &draws[i * stride], (size_t)stride * 8);
@@ -507,7 +508,8 @@ private:
     // one pvac_hip_enc_value launch over (vs, draws) with a fixed stride; status per value
     template <class CipherT>
     std::vector<CipherT> enc_run(const std::vector<uint64_t>& vs, const std::vector<uint64_t>& draws, uint32_t stride,
-                                 uint32_t lpv, uint32_t epv, bool with_sigma, std::vector<uint32_t>& status) {
+                                 uint32_t lpv, uint32_t epv, bool with_sigma, std::vector<uint32_t>& status,
+                                 int depth_hint = 0) {
         const size_t n = vs.size();
         detail::dev_array<uint64_t> d_v(n), d_r(draws.size());
         d_v.upload(vs.data(), n, stream_);
@@ -519,7 +521,8 @@ private:
         pvac_ct_batch vc = c.view(with_sigma);
         vc.n = n;
         detail::dev_array<uint32_t> st(n);
-        check(pvac_hip_enc_value(ctx_, n, d_v.p, d_r.p, stride, &vc, with_sigma ? PVAC_ENC_WITH_SIGMA : 0, st.p));
+        check(pvac_hip_enc_value_depth(ctx_, n, d_v.p, d_r.p, stride, depth_hint, &vc,
+                                       with_sigma ? PVAC_ENC_WITH_SIGMA : 0, st.p));
         status.resize(n);
         st.download(status.data(), n, stream_);
         return detail::from_device<CipherT>(c, n, lslots, eslots, prm_.m_bits, with_sigma, stream_);
@@ -597,6 +600,19 @@ std::vector<CipherT> ct_add_batch(const PubKeyT& pk, const std::vector<CipherT>&
 template <class CipherT, class PubKeyT, class SecKeyT>
 CipherT enc_value(const PubKeyT& pk, const SecKeyT& sk, uint64_t v, const RandomSource& rnd = os_random_u64) {
     return engine_for(pk).template enc_value<PubKeyT, SecKeyT, CipherT>(pk, sk, std::vector<uint64_t>{v}, true, rnd)[0];
+}
+
+// enc_value_depth / enc_zero_depth (ops/encrypt.hpp:281-287, 293-298): the noise plan of depth_hint
+template <class CipherT, class PubKeyT, class SecKeyT>
+CipherT enc_value_depth(const PubKeyT& pk, const SecKeyT& sk, uint64_t v, int depth_hint,
+                        const RandomSource& rnd = os_random_u64) {
+    return engine_for(pk).template enc_value<PubKeyT, SecKeyT, CipherT>(pk, sk, std::vector<uint64_t>{v}, true, rnd,
+                                                                         depth_hint)[0];
+}
+
+template <class CipherT, class PubKeyT, class SecKeyT>
+CipherT enc_zero_depth(const PubKeyT& pk, const SecKeyT& sk, int depth_hint, const RandomSource& rnd = os_random_u64) {
+    return enc_value_depth<CipherT>(pk, sk, 0, depth_hint, rnd);
 }
 
 template <class CipherT, class PubKeyT, class SecKeyT>

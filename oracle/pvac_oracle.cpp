@@ -842,9 +842,17 @@ static void plan_noise(uint32_t B, int depth, int& z2, int& z3) {
 
 int orc_enc_value(const orc_params* prm, const orc_secret* sk, const uint64_t* H, const uint64_t* powg, uint64_t v,
                   const uint64_t* stream, size_t n, int order, orc_cipher* out, size_t* consumed) {
+    return orc_enc_value_depth(prm, sk, H, powg, v, 0, stream, n, order, out, consumed);
+}
+
+// enc_value_depth (ops/encrypt.hpp:281-287); v = 0 is enc_zero_depth (:293-298): fp_add(0, mask) is
+// mask, and the draws are the same
+int orc_enc_value_depth(const orc_params* prm, const orc_secret* sk, const uint64_t* H, const uint64_t* powg,
+                        uint64_t v, int depth_hint, const uint64_t* stream, size_t n, int order, orc_cipher* out,
+                        size_t* consumed) {
     Stream rs{stream, n};
     int Z2, Z3;
-    plan_noise(prm->B, 0, Z2, Z3);
+    plan_noise(prm->B, depth_hint, Z2, Z3);
     const F val{v, 0};
     const F mask = rand_fp_nonzero(rs);   // encrypt.hpp:281-287
     Ct a, b;

@@ -104,6 +104,11 @@ void orc_prf_noise_delta(const orc_secret* sk, uint64_t canon, uint64_t ztag, ui
 int orc_enc_value(const orc_params* prm, const orc_secret* sk, const uint64_t* H_dense, const uint64_t* powg,
                   uint64_t v, const uint64_t* stream, size_t stream_len, int order, orc_cipher* out,
                   size_t* consumed);
+/* enc_value_depth(v, depth_hint) (ops/encrypt.hpp:281-287): the noise plan of depth_hint
+ * (plan_noise, encrypt.hpp:16-27); v = 0 gives enc_zero_depth (:293-298) exactly. */
+int orc_enc_value_depth(const orc_params* prm, const orc_secret* sk, const uint64_t* H_dense, const uint64_t* powg,
+                        uint64_t v, int depth_hint, const uint64_t* stream, size_t n, int order, orc_cipher* out,
+                        size_t* consumed);
 /* libstdc++ bucket count after unordered_map::reserve(n) (the emit-order pin) */
 uint64_t orc_bucket_count_after_reserve(uint64_t n);
 

@@ -470,6 +470,46 @@ static void cmd_fullrange(const std::string& dir) {
     std::ofstream(dir + "/fr_manifest.json") << js.str();
 }
 
+// ---------------------------------------------------------------- enc_value_depth / enc_zero_depth
+// The other encryption entry points (ops/encrypt.hpp:281-298): depth hints change the noise plan
+// (plan_noise, encrypt.hpp:16-27). Same key as cmd_fixtures; each case logs the stream it consumed.
+static void cmd_encdepth(const std::string& dir) {
+    reseed(0x5EED0C00ULL);
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    (void)enc_value(pk, sk, 1);   // warm-up: the Toeplitz autotuner draws random words once
+    struct Case { int kind; uint64_t v; int depth; };   // kind 0: enc_value_depth, 1: enc_zero_depth
+    const Case cases[] = {{0, 2016733, 1}, {0, 5, 3}, {0, 7083881, 8}, {0, 42, 15}, {1, 0, 0}, {1, 0, 5}};
+    const int nc = (int)(sizeof cases / sizeof cases[0]);
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ",\n  \"cases\": [\n";
+    for (int i = 0; i < nc; ++i) {
+        const Case& c = cases[i];
+        reseed(0x5EED0D10ULL + (uint64_t)i);
+        g_logging = true;
+        std::vector<uint64_t> stream;
+        Cipher X = run_logged([&] { return c.kind ? enc_zero_depth(pk, sk, c.depth) : enc_value_depth(pk, sk, c.v, c.depth); },
+                              stream);
+        g_logging = false;
+        const std::string pre = dir + "/encd" + std::to_string(i);
+        write_ct(pre + ".ct", {X}, true);
+        write_u64(pre + "_stream.u64", stream);
+        dump_R(pre + "_R.u64", base_layer_R(pk, sk, X));
+        const Fp dv = dec_value(pk, sk, X);
+        const auto z = plan_noise(pk, c.depth);
+        js << "    {\"kind\": \"" << (c.kind ? "zero" : "value") << "\", \"v\": " << c.v << ", \"depth\": " << c.depth
+           << ", \"Z2\": " << z.first << ", \"Z3\": " << z.second << ", \"edges\": " << X.E.size()
+           << ", \"layers\": " << X.L.size() << ", \"stream\": " << stream.size() << ", \"dec\": " << fpjson(dv)
+           << "}" << (i + 1 < nc ? "," : "") << "\n";
+        std::printf("encdepth case %d: depth %d edges %zu stream %zu\n", i, c.depth, X.E.size(), stream.size());
+    }
+    js << "  ],\n  \"generator\": \"oracle/ref_harness.cpp encdepth (reference pvac-hfhe 0.1.0)\"\n}\n";
+    std::ofstream(dir + "/encd_manifest.json") << js.str();
+}
+
 // ---------------------------------------------------------------- timing (CPU baseline leg)
 // Times the reference's own ct_mul (WITH sigma, arithmetic.hpp:47-106) on fresh pairs.
 static void cmd_time_mul(int npairs, int threads) {
@@ -588,6 +628,10 @@ int main(int argc, char** argv) {
         int cs = argc > 4 ? std::atoi(argv[4]) : 3;
         int ss = argc > 5 ? std::atoi(argv[5]) : 2;
         cmd_fixtures(argv[2], np, cs, ss);
+        return 0;
+    }
+    if (cmd == "encdepth" && argc >= 3) {
+        cmd_encdepth(argv[2]);
         return 0;
     }
     if (cmd == "fullrange" && argc >= 3) {

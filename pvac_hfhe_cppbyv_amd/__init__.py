@@ -120,6 +120,8 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_prf": ([vp, i32, C.c_size_t, vp, vp], i32),
         "pvac_hip_enc_caps": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], i32),
         "pvac_hip_enc_value": ([vp, C.c_size_t, vp, vp, u32, C.POINTER(CtBatch), u32, vp], i32),
+        "pvac_hip_enc_caps_depth": ([vp, i32, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], i32),
+        "pvac_hip_enc_value_depth": ([vp, C.c_size_t, vp, vp, u32, i32, C.POINTER(CtBatch), u32, vp], i32),
         "pvac_hip_base_R": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_dec_value": ([vp, C.POINTER(CtBatch), vp, vp, vp], i32),
         "pvac_ct_scan": ([vp, C.c_size_t, vp], i32),
@@ -291,14 +293,15 @@ class Engine:
         return [int(o[2 * i]) | (int(o[2 * i + 1]) << 64) for i in range(n)]
 
     # ---- encryption (ops/encrypt.hpp:281-287)
-    def enc_caps(self):
+    def enc_caps(self, depth=0):
         lp, ep, dh = C.c_uint32(), C.c_uint32(), C.c_uint32()
-        self._check(self.lib.pvac_hip_enc_caps(self.ctx, C.byref(lp), C.byref(ep), C.byref(dh)))
+        self._check(self.lib.pvac_hip_enc_caps_depth(self.ctx, int(depth), C.byref(lp), C.byref(ep), C.byref(dh)))
         return lp.value, ep.value, dh.value
 
-    def enc_value(self, values, rnd, sigma=False):
+    def enc_value(self, values, rnd, sigma=False, depth=0):
         """values: n u64 (host array or device tensor); rnd: (n, stride) u64 draws per value (the
-        reference's csprng_u64 stream). Returns (DeviceBatch, status numpy u32)."""
+        reference's csprng_u64 stream). depth > 0: enc_value_depth (ops/encrypt.hpp:281-287); a value
+        of 0 is enc_zero_depth (:293-298). Returns (DeviceBatch, status numpy u32)."""
         torch = self.torch
         if isinstance(values, np.ndarray) or isinstance(values, list):
             values = _t(np.ascontiguousarray(np.asarray(values, dtype=np.uint64))).to(self.device)
@@ -306,16 +309,16 @@ class Engine:
             rnd = _t(np.ascontiguousarray(rnd, np.uint64)).to(self.device)
         n = values.numel()
         stride = rnd.numel() // max(n, 1)
-        lp, ep, _ = self.enc_caps()
+        lp, ep, _ = self.enc_caps(depth)
         z = lambda k: torch.zeros(max(k, 1), dtype=torch.int64, device=self.device)
         C_ = DeviceBatch(n, z(n), z(n), torch.zeros((max(lp * n, 1), 5), dtype=torch.int64, device=self.device), z(n),
                          z(n), z(ep * n), z(ep * n), z(ep * n),
                          torch.zeros((max(ep * n, 1), 128), dtype=torch.int64, device=self.device) if sigma else None)
         status = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
         sc = C_.struct()
-        self._check(self.lib.pvac_hip_enc_value(self.ctx, n, C.c_void_p(values.data_ptr()), C.c_void_p(rnd.data_ptr()),
-                                                stride, C.byref(sc), ENC_WITH_SIGMA if sigma else 0,
-                                                C.c_void_p(status.data_ptr())))
+        self._check(self.lib.pvac_hip_enc_value_depth(self.ctx, n, C.c_void_p(values.data_ptr()),
+                                                      C.c_void_p(rnd.data_ptr()), stride, int(depth), C.byref(sc),
+                                                      ENC_WITH_SIGMA if sigma else 0, C.c_void_p(status.data_ptr())))
         return C_, status.cpu().numpy().view(np.uint32)[:n]
 
     def base_R(self, X: DeviceBatch):

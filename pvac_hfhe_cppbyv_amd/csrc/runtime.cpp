@@ -1024,9 +1024,15 @@ void plan_noise(uint32_t B, int depth, uint32_t& z2, uint32_t& z3) {
 }  // namespace
 
 int pvac_hip_enc_caps(pvac_hip_ctx* c, uint32_t* layers_per_value, uint32_t* edges_per_value, uint32_t* draws_hint) {
+    return pvac_hip_enc_caps_depth(c, 0, layers_per_value, edges_per_value, draws_hint);
+}
+
+int pvac_hip_enc_caps_depth(pvac_hip_ctx* c, int depth_hint, uint32_t* layers_per_value, uint32_t* edges_per_value,
+                            uint32_t* draws_hint) {
     if (!c) return PVAC_EINVAL;
     uint32_t z2, z3;
-    plan_noise(c->prm.B, 0, z2, z3);
+    plan_noise(c->prm.B, depth_hint, z2, z3);
+    if (8 + 2 * z2 + 3 * z3 > kEncPreMax) return fail(c, PVAC_ENOSYS, "enc_caps: noise plan beyond the supported group counts");
     const uint32_t npre = 8 + 2 * z2 + 3 * z3;
     if (layers_per_value) *layers_per_value = 2;
     if (edges_per_value) *edges_per_value = 2 * npre;
@@ -1037,6 +1043,11 @@ int pvac_hip_enc_caps(pvac_hip_ctx* c, uint32_t* layers_per_value, uint32_t* edg
 
 int pvac_hip_enc_value(pvac_hip_ctx* c, size_t n, const uint64_t* values, const uint64_t* rnd, uint32_t rnd_stride,
                        pvac_ct_batch* C, uint32_t flags, uint32_t* status) {
+    return pvac_hip_enc_value_depth(c, n, values, rnd, rnd_stride, 0, C, flags, status);
+}
+
+int pvac_hip_enc_value_depth(pvac_hip_ctx* c, size_t n, const uint64_t* values, const uint64_t* rnd, uint32_t rnd_stride,
+                             int depth_hint, pvac_ct_batch* C, uint32_t flags, uint32_t* status) {
     if (!c || !C || (n && (!values || !rnd || !status))) return fail(c, PVAC_EINVAL, "enc_value: arguments");
     if (!C->l_off || !C->l_cnt || !C->layers || !C->e_off || !C->e_cnt || !C->meta || !C->w_lo || !C->w_hi)
         return fail(c, PVAC_EINVAL, "enc_value: output arrays");
@@ -1054,7 +1065,7 @@ int pvac_hip_enc_value(pvac_hip_ctx* c, size_t n, const uint64_t* values, const 
     a.rnd = rnd;
     a.stride = rnd_stride;
     a.B = c->prm.B;
-    plan_noise(c->prm.B, 0, a.Z2, a.Z3);
+    plan_noise(c->prm.B, depth_hint, a.Z2, a.Z3);
     a.n = n;
     a.canon = c->prm.canon_tag;
     a.powg = c->powg;

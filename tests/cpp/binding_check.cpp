@@ -23,6 +23,10 @@ Cipher ct_mul(const PubKey& pk, const Cipher& A, const Cipher& B) { return pvac_
 Cipher enc_value(const PubKey& pk, const SecKey& sk, uint64_t v) {                                          // encrypt.hpp:289
     return pvac_hip::enc_value<Cipher>(pk, sk, v);
 }
+Cipher enc_value_depth(const PubKey& pk, const SecKey& sk, uint64_t v, int d) {                           // encrypt.hpp:281
+    return pvac_hip::enc_value_depth<Cipher>(pk, sk, v, d);
+}
+Cipher enc_zero_depth(const PubKey& pk, const SecKey& sk, int d) { return pvac_hip::enc_zero_depth<Cipher>(pk, sk, d); } // :293
 Fp dec_value(const PubKey& pk, const SecKey& sk, const Cipher& C) { return pvac_hip::dec_value(pk, sk, C); } // decrypt.hpp:62
 std::vector<Cipher> load_cts(const std::vector<uint8_t>& b) { return pvac_hip::load_cts_bytes<Cipher>(b); }
 std::vector<uint8_t> save_cts(const std::vector<Cipher>& c) { return pvac_hip::save_cts_bytes(c); }
@@ -38,6 +42,7 @@ int main(int argc, char**) {
     // link check only: reference every binding so nothing is discarded
     volatile void* keep[] = {(void*)&binding::ct_add,    (void*)&binding::ct_sub,    (void*)&binding::ct_scale,
                              (void*)&binding::ct_mul,    (void*)&binding::enc_value, (void*)&binding::dec_value,
-                             (void*)&binding::load_cts,  (void*)&binding::save_cts};
+                             (void*)&binding::load_cts,  (void*)&binding::save_cts,
+                             (void*)&binding::enc_value_depth, (void*)&binding::enc_zero_depth};
     return argc > 99 ? (int)(uintptr_t)keep[0] : 0;
 }

@@ -367,6 +367,26 @@ int main(int argc, char** argv) {
             const auto m = pvac_hip::dec_value(pk, sk, c);
             MUST(m.lo == vs[i] && m.hi == 0, "dec_value(enc %zu)", i);
         }
+        // enc_value_depth / enc_zero_depth (encrypt.hpp:281-298) from the harness's encdepth streams:
+        // argv[5] = "kind:v:depth,..." (kind 0 value, 1 zero), case i replays encd<i>_stream.u64
+        if (argc > 5) {
+            size_t i = 0;
+            for (const char* p = argv[5]; *p; ++i) {
+                char* e = nullptr;
+                const unsigned long kind = std::strtoul(p, &e, 10);
+                const unsigned long long v = std::strtoull(e + 1, &e, 10);
+                const int d = (int)std::strtol(e + 1, &e, 10);
+                p = *e ? e + 1 : e;
+                const std::string base = ref + "/encd" + std::to_string(i);
+                replay_pad rs{read_u64(base + "_stream.u64")};
+                const Cipher c = kind ? pvac_hip::enc_zero_depth<Cipher>(pk, sk, d, std::ref(rs))
+                                      : pvac_hip::enc_value_depth<Cipher>(pk, sk, v, d, std::ref(rs));
+                MUST(rs.k >= rs.s.size(), "encd %zu consumed %zu of %zu words", i, rs.k, rs.s.size());
+                MUST(write_ct({c}) == slurp(base + ".ct"), "enc depth case %zu .ct bytes", i);
+                MUST(pvac_hip::dec_value(pk, sk, c).lo == v, "dec_value(enc depth case %zu)", i);
+            }
+            MUST(i > 0, "no enc depth cases");
+        }
         // fresh randomness, batched both ways
         const auto cs = pvac_hip::enc_value_batch<Cipher>(pk, sk, vs);
         const auto ms = pvac_hip::dec_value_batch(pk, sk, cs);

@@ -241,6 +241,9 @@ class Oracle:
         lib.orc_prf_noise_delta.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_uint32, C.c_uint32, u64p]
         lib.orc_enc_value.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSecret), u64p, u64p, C.c_uint64, u64p,
                                       C.c_size_t, C.c_int, C.POINTER(OrcCipher), C.POINTER(C.c_size_t)]
+        lib.orc_enc_value_depth.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSecret), u64p, u64p, C.c_uint64,
+                                            C.c_int, u64p, C.c_size_t, C.c_int, C.POINTER(OrcCipher),
+                                            C.POINTER(C.c_size_t)]
 
     # ---- Fp
     def fp(self, op, a_lo, a_hi, b_lo=None, b_hi=None):
@@ -357,13 +360,14 @@ class Oracle:
                                      _p(out))
         return int(out[0]), int(out[1])
 
-    def enc_value(self, sk, v, stream, powg, H=None, canon_tag=0, order=1):
+    def enc_value(self, sk, v, stream, powg, H=None, canon_tag=0, order=1, depth=0):
+        """enc_value_depth(v, depth) (ops/encrypt.hpp:281-287); depth 0 is enc_value, v = 0 enc_zero_depth."""
         prm = default_params(canon_tag)
-        oc, ov = self._out(4, 64, H is not None)
+        oc, ov = self._out(4, 128, H is not None)
         used = C.c_size_t()
         st = np.ascontiguousarray(stream, np.uint64)
-        rc = self.lib.orc_enc_value(C.byref(prm), C.byref(sk), _p(H), _p(np.ascontiguousarray(powg, np.uint64)),
-                                    int(v), _p(st), len(st), order, C.byref(ov), C.byref(used))
+        rc = self.lib.orc_enc_value_depth(C.byref(prm), C.byref(sk), _p(H), _p(np.ascontiguousarray(powg, np.uint64)),
+                                          int(v), int(depth), _p(st), len(st), order, C.byref(ov), C.byref(used))
         assert rc == 0, rc
         return self._trim(oc, ov), used.value
 

@@ -29,7 +29,9 @@ def test_adapter_against_golden():
         man = json.load(f)
     with open(os.path.join(GOLD, "ref", "enc_manifest.json")) as f:
         vs = ",".join(str(e["v"]) for e in json.load(f)["enc"])
-    r = subprocess.run([EXE, GOLD, str(man["canon_tag"]), man["H_digest"], vs], capture_output=True, text=True,
+    with open(os.path.join(GOLD, "ref", "encd_manifest.json")) as f:
+        ds = ",".join(f"{int(c['kind'] == 'zero')}:{c['v']}:{c['depth']}" for c in json.load(f)["cases"])
+    r = subprocess.run([EXE, GOLD, str(man["canon_tag"]), man["H_digest"], vs, ds], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "checks passed" in r.stdout

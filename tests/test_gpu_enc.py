@@ -130,3 +130,41 @@ def test_enc_dec_roundtrip_with_gpu_prf():
     got, st2 = eng.dec_value(C_, eng.base_R(C_))
     assert not st2.any()
     assert got == [int(v) for v in vals]
+
+
+@pytest.mark.parametrize("sigma", [False, True])
+def test_enc_value_depth_and_zero_fixtures(sigma):
+    """enc_value_depth (hints 1, 3, 8, 15) and enc_zero_depth (0, 5) on the GPU from the reference's
+    streams: byte-exact .ct output (with sigma), every case decrypting to its value."""
+    import json
+    from helpers import write_ct
+    eng, _, man, _ = _eng()
+    with open(os.path.join(REF, "encd_manifest.json")) as f:
+        fm = json.load(f)
+    for i, c in enumerate(fm["cases"]):
+        st = read_u64(f"encd{i}_stream.u64")
+        _, ep, dh = eng.enc_caps(c["depth"])
+        assert len(st) <= dh and c["edges"] <= ep
+        rnd = np.zeros((1, dh), np.uint64)
+        rnd[0, :len(st)] = st
+        C_, status = eng.enc_value(np.array([c["v"]], np.uint64), rnd, sigma=sigma, depth=c["depth"])
+        assert not status.any(), i
+        got = C_.to_host()[0]
+        ref = read_ct(os.path.join(REF, f"encd{i}.ct"))[0]
+        assert np.array_equal(got.meta, ref.meta) and np.array_equal(got.w_lo, ref.w_lo), i
+        assert np.array_equal(got.w_hi, ref.w_hi), i
+        if sigma:
+            from helpers import Cipher
+            L = got.layers
+            with open(os.path.join(REF, f"encd{i}.ct"), "rb") as f:
+                assert write_ct([Cipher(L, got.meta, got.w_lo, got.w_hi, got.sigma)]) == f.read(), i
+        R = eng.base_R(C_)
+        vals, dst = eng.dec_value(C_, R)
+        assert vals[0] == c["v"] and not dst.any(), i
+
+
+def test_enc_depth_beyond_supported_plan_is_refused():
+    from pvac_hfhe_cppbyv_amd import PvacError
+    eng, _, _, _ = _eng()
+    with pytest.raises(PvacError):
+        eng.enc_caps(16)

@@ -70,3 +70,20 @@ def test_enc_value_fixture_with_sigma_bytes(oracle, key):
     c, _ = oracle.enc_value(sk, em["enc"][i]["v"], st, powg, H=H, canon_tag=man["canon_tag"])
     with open(os.path.join(REF, f"enc{i}.ct"), "rb") as f:
         assert write_ct([c]) == f.read()
+
+
+def test_enc_value_depth_and_zero_fixtures(oracle, key):
+    """enc_value_depth (depth hints 1, 3, 8, 15) and enc_zero_depth (0, 5): the oracle reproduces the
+    reference's .ct bytes, sigmas included, from the streams it consumed (ref_harness encdepth)."""
+    import json
+    sk, man, _ = key
+    H, _ = oracle.gen_H(man["canon_tag"])
+    powg = read_u64("powg_B.u64")
+    with open(os.path.join(REF, "encd_manifest.json")) as f:
+        fm = json.load(f)
+    for i, c in enumerate(fm["cases"]):
+        st = read_u64(f"encd{i}_stream.u64")
+        got, used = oracle.enc_value(sk, c["v"], st, powg, H=H, canon_tag=man["canon_tag"], depth=c["depth"])
+        assert used == len(st) == c["stream"] and got.nE == c["edges"], i
+        with open(os.path.join(REF, f"encd{i}.ct"), "rb") as f:
+            assert write_ct([got]) == f.read(), i
