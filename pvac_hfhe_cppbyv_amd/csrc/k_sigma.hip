@@ -18,6 +18,7 @@
 // lane.
 #include <algorithm>
 #include <vector>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.hpp"
@@ -192,6 +193,8 @@ struct sig_args {
     const uint64_t* salts;
     const uint32_t* salt_pos;
     const uint16_t* rows;
+    const uint16_t* rows_fast;   // bank-sorted encoded rows (sigma_tables::rows_fast) or null
+    const uint8_t* rows_delta;   // byte-delta rows (sigma_tables::rows_delta) or null
     const uint32_t* counts;
     uint32_t width;
     uint32_t full;   // every column has exactly width rows
@@ -205,9 +208,139 @@ struct sig_args {
 // 6 blocks per CU (6 waves per SIMD): the compiler keeps the pass loop within 80 VGPRs without
 // spills instead of hoisting the whole SHA-256 message schedule (149 VGPRs, 3 waves per SIMD)
 constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compression per lane covers
-__host__ __device__ inline uint32_t sigma_wave_words(uint32_t m_bits, uint32_t n_bits, uint32_t x_col_wt) {
-    const uint32_t w = m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2;
-    return ((w + 3) & ~3u) + kMidBatch * 2 * 8;
+__host__ __device__ constexpr uint32_t sigma_wave_words(uint32_t m_bits, uint32_t n_bits, uint32_t x_col_wt) {
+    return ((m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2 + 3) & ~3u) + kMidBatch * 2 * 8;
+}
+
+// Fast column expansion (default Params: m_bits 8192, n_bits 16384, x_col_wt <= 128, full
+// columns). Wave WV's sigma image sits at a compile-time LDS address, and rows_fast encodes a row
+// r as (r & 31) | (r >> 5) << 7, so a flip is one bit-field extract (or shift) for the byte
+// offset, folded into the ds_xor's immediate base, and one shift for the bit: two VALU per flip.
+// Each column's rows are sorted by LDS bank, starting at bank c mod 32, and the caller deals the
+// columns to lanes so that the 32 lanes of one LDS cycle start at distinct banks: the lanes of one
+// ds_xor then spread over the banks instead of hitting them at random.
+constexpr uint32_t kFastWaveWords = sigma_wave_words(8192, 16384, 128);
+// LDS atomic XOR at an absolute LDS byte address (the dynamic LDS of k_sigma starts at 0: it has
+// no static __shared__ data; the kernel checks this before taking the fast path)
+using lds_u32 = __attribute__((address_space(3))) uint32_t;
+__device__ __forceinline__ void lds_xor(uint32_t byte_addr, uint32_t v) {
+    __hip_atomic_fetch_xor((lds_u32*)(size_t)byte_addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int WV>
+__device__ __forceinline__ void flip_cols_fast(const uint16_t* rows_fast, uint32_t W, uint32_t c0, uint32_t c1,
+                                               uint32_t ncols, int lane) {
+    constexpr uint32_t img = WV * kFastWaveWords * 4u;   // byte address of wave WV's image
+    const uint32_t nch = W / 8u;   // 16-byte chunks (8 rows) per column
+    auto flip2 = [&](uint32_t x) {   // rows x & 0xFFFF and x >> 16
+        lds_xor(img + __builtin_amdgcn_ubfe(x, 5, 10), 1u << (x & 31u));
+        lds_xor(img + (x >> 21), 1u << ((x >> 16) & 31u));
+    };
+#ifdef PVAC_EXP_SIG_PAIR   // A/B: both columns' chunks in one batch (4 + 4 loads in flight)
+    if (ncols == 128u) {
+        const uint4* r0 = (const uint4*)(rows_fast + (size_t)c0 * W);
+        const uint4* r1 = (const uint4*)(rows_fast + (size_t)c1 * W);
+        for (uint32_t q4 = 0; q4 < nch; q4 += 4) {
+            uint4 v[8];
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                v[b] = q4 + b < nch ? r0[q4 + b] : make_uint4(0, 0, 0, 0);
+                v[4 + b] = q4 + b < nch ? r1[q4 + b] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < 8; ++b) {
+                if (q4 + (b & 3u) >= nch) continue;
+                flip2(v[b].x); flip2(v[b].y); flip2(v[b].z); flip2(v[b].w);
+            }
+        }
+        return;
+    }
+#endif
+#pragma unroll 1
+    for (uint32_t cc = 0; cc < 2; ++cc) {
+        if ((uint32_t)lane + 64u * cc >= ncols) break;
+        const uint4* rp = (const uint4*)(rows_fast + (size_t)(cc ? c1 : c0) * W);
+#ifdef PVAC_EXP_SIG_KB12
+        constexpr uint32_t kB = 12;
+#else
+        constexpr uint32_t kB = 8;
+#endif
+        for (uint32_t q8 = 0; q8 < nch; q8 += kB) {
+            uint4 v[kB];
+#pragma unroll
+            for (uint32_t b = 0; b < kB; ++b) {
+#ifdef PVAC_EXP_SIG_NOLOAD   // timing experiment: pseudo-random rows, no table reads (sigma wrong)
+                const uint32_t h = ((cc ? c1 : c0) * 0x9E3779B1u + (q8 + b) * 0x85EBCA77u) ^ (uint32_t)lane;
+                v[b] = make_uint4(h & 0x7F9F7F9Fu, (h * 0xC2B2AE3Du) & 0x7F9F7F9Fu, (h * 0x27D4EB2Fu) & 0x7F9F7F9Fu,
+                                  (h * 0x165667B1u) & 0x7F9F7F9Fu);
+#else
+                v[b] = q8 + b < nch ? rp[q8 + b] : make_uint4(0, 0, 0, 0);
+#endif
+            }
+#ifdef PVAC_EXP_SIG_NOFLIP   // timing experiment: rows read, one LDS op per batch (sigma wrong)
+            {
+                uint32_t z = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < kB; ++b) z ^= v[b].x ^ v[b].y ^ v[b].z ^ v[b].w;
+                lds_xor(img + __builtin_amdgcn_ubfe(z, 5, 10), 1u << (z & 31u));
+                continue;
+            }
+#endif
+#pragma unroll
+            for (uint32_t b = 0; b < kB; ++b) {
+                if (q8 + b >= nch) break;
+                flip2(v[b].x); flip2(v[b].y); flip2(v[b].z); flip2(v[b].w);
+            }
+        }
+    }
+}
+
+// Byte-delta column expansion (default Params): a row r is the key R = (r >> 5) | (r & 31) << 8,
+// i.e. its image word in byte 0 and its bit in byte 1. A column is its 192 keys in ascending order
+// as kDeltaBytes byte increments (R starts at 0; each byte advances R and flips R). A gap of 256 or
+// more is bridged by an increment of 255 followed by one of 0 (the same bit flipped twice), and the
+// column is padded with 0 increments (an even number: the last bit flipped twice more). Per flip:
+// one byte-select add, one byte-select shift for the LDS address, one for the bit. The table is
+// 3.4 MB (16384 x 208 B) against 6.3 MB of u16 rows, so it mostly stays in each XCD's 4 MB L2:
+// the u16 expansion was bound by these gathers (about 26 of 42 ms), not by the flips.
+constexpr uint32_t kDeltaBytes = 208;   // 13 chunks of 16 increments; <= 8 bridges per column
+template <int WV>
+__device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0, uint32_t c1) {
+    constexpr uint32_t img = WV * kFastWaveWords * 4u;   // byte address of wave WV's image
+    uint32_t two = 2u, one = 1u;
+    asm volatile("" : "+v"(two), "+v"(one));   // VGPR operands for the SDWA shifts
+    auto word4 = [&](uint32_t& R, uint32_t w) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            R += (w >> (8 * k)) & 255u;
+            // byte 0 of R << 2 (the word's LDS offset) and 1 << byte 1 of R, one SDWA shift each
+            uint32_t off, bit;
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+                : "=v"(off) : "v"(two), "v"(R));
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+                : "=v"(bit) : "v"(R), "v"(one));
+            __builtin_assume(off < 1024u);
+            lds_xor(img + off, bit);
+        }
+    };
+#pragma unroll 1
+    for (uint32_t cc = 0; cc < 2; ++cc) {
+        const uint4* rp = (const uint4*)(tab + (size_t)(cc ? c1 : c0) * kDeltaBytes);
+        uint32_t R = 0;
+        {
+            uint4 v[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) v[b] = rp[b];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) { word4(R, v[b].x); word4(R, v[b].y); word4(R, v[b].z); word4(R, v[b].w); }
+        }
+        {
+            uint4 v[5];
+#pragma unroll
+            for (int b = 0; b < 5; ++b) v[b] = rp[8 + b];
+#pragma unroll
+            for (int b = 0; b < 5; ++b) { word4(R, v[b].x); word4(R, v[b].y); word4(R, v[b].z); word4(R, v[b].w); }
+        }
+    }
 }
 
 // POW2: n_bits and m_bits are powers of two (default Params), so the rejection bound is
@@ -232,6 +365,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     uint32_t* bm = isX ? bmX : bmN;
     const uint64_t words_per_sigma = a.X.sigma_words;
     const uint32_t sub = blockIdx.y * 4 + wave, nsub = a.sub_blocks * 4;
+    const bool lds_at0 = (uint32_t)(size_t)(lds_u32*)slds == 0u;   // flip_cols_fast's absolute addresses
 
     // the salt-independent words of an edge (salt last: it is the only word in both blocks)
     auto edge_words = [&](uint64_t eo, uint64_t lo, uint64_t nl, uint64_t e, uint64_t (&words)[7]) {
@@ -353,6 +487,94 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // 256]; the skew puts the groups' equal word indices on different banks): lanes of
             // different groups never contend for a word. Copy 0 already holds the noise bits.
             const uint32_t W = a.width;
+            if (a.rows_delta && lds_at0) {   // host-checked: default Params, kFastWaveWords per wave
+                __builtin_amdgcn_s_setprio(2);   // LDS-atomic phase ahead of other waves' SHA-256
+                const uint32_t c0 = cols[lane], c1 = cols[lane + 64];   // x_col_wt == 128
+                for (uint32_t w4 = lane; w4 < (bx32 + bn32) / 4u; w4 += 64) ((uint4*)bmX)[w4] = make_uint4(0, 0, 0, 0);
+#ifdef PVAC_EXP_SIG_NOEXP   // timing experiment: no column expansion (sigma wrong)
+                if (a.width == 0x7FFFFFFFu)
+#endif
+                switch (__builtin_amdgcn_readfirstlane(wave)) {
+                    case 0: flip_cols_delta<0>(a.rows_delta, c0, c1); break;
+                    case 1: flip_cols_delta<1>(a.rows_delta, c0, c1); break;
+                    case 2: flip_cols_delta<2>(a.rows_delta, c0, c1); break;
+                    default: flip_cols_delta<3>(a.rows_delta, c0, c1); break;
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t* out = a.X.sigma + e * words_per_sigma;
+                {
+                    uint4* s4 = (uint4*)sig + lane;   // 256 words: one 16-byte store per lane
+                    const uint4 v = *s4;
+                    ((ulonglong2*)out)[lane] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
+                                                               (uint64_t)v.z | ((uint64_t)v.w << 32));
+                    *s4 = make_uint4(0, 0, 0, 0);
+                }
+                __builtin_amdgcn_s_setprio(0);
+                continue;
+            }
+            if (a.rows_fast && lds_at0) {   // host-checked: default Params, full columns, kFastWaveWords per wave
+                __builtin_amdgcn_s_setprio(2);   // LDS-atomic phase ahead of other waves' SHA-256
+#ifdef PVAC_EXP_SIG_NOMATCH   // A/B: columns in selection order
+                const uint32_t c0 = (uint32_t)lane < a.x_col_wt ? cols[lane] : 0u;
+                const uint32_t c1 = (uint32_t)lane + 64u < a.x_col_wt ? cols[lane + 64] : 0u;
+                for (uint32_t w4 = lane; w4 < (bx32 + bn32) / 4u; w4 += 64) ((uint4*)bmX)[w4] = make_uint4(0, 0, 0, 0);
+#else
+                // Bank matching (x_col_wt == 128): column c's rows start at bank c mod 32 and walk the
+                // banks upward, so 32 lanes whose columns have distinct c mod 32 hit distinct banks at
+                // every step. The 128 columns are counting-sorted by c mod 32 (the dead selection
+                // bitmaps hold the histogram and the sorted list) and round j = 2 k + g (group g =
+                // lane >> 5, slot k) takes sorted positions j, j + 4, ..., j + 124.
+                for (uint32_t w4 = lane; w4 < (bx32 + bn32) / 4u; w4 += 64) ((uint4*)bmX)[w4] = make_uint4(0, 0, 0, 0);
+                __builtin_amdgcn_wave_barrier();
+                uint32_t c0, c1;
+                {
+                    uint32_t* hist = bmX;
+                    uint16_t* srt = (uint16_t*)(bmX + 32);
+                    const uint32_t ca = cols[lane], cb = cols[lane + 64];
+                    const uint32_t pa = atomicAdd(&hist[ca & 31u], 1u);
+                    const uint32_t pb = atomicAdd(&hist[cb & 31u], 1u);
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t h = lane < 32 ? hist[lane] : 0u;
+                    const uint32_t ex = wave_incl_scan_u32(h) - h;
+                    const uint32_t ba = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ca & 31u) << 2), (int)ex);
+                    const uint32_t bb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((cb & 31u) << 2), (int)ex);
+                    srt[ba + pa] = (uint16_t)ca;
+                    srt[bb + pb] = (uint16_t)cb;
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t i4 = 4u * ((uint32_t)lane & 31u) + ((uint32_t)lane >> 5);
+                    c0 = srt[i4];
+                    c1 = srt[i4 + 2u];
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane < 24) ((uint4*)bmX)[lane] = make_uint4(0, 0, 0, 0);   // hist + srt: 96 words
+                }
+#endif
+#ifdef PVAC_EXP_SIG_NOEXP   // timing experiment: no column expansion (sigma wrong)
+                if (a.width == 0x7FFFFFFFu)
+#endif
+                switch (__builtin_amdgcn_readfirstlane(wave)) {
+                    case 0: flip_cols_fast<0>(a.rows_fast, W, c0, c1, a.x_col_wt, lane); break;
+                    case 1: flip_cols_fast<1>(a.rows_fast, W, c0, c1, a.x_col_wt, lane); break;
+                    case 2: flip_cols_fast<2>(a.rows_fast, W, c0, c1, a.x_col_wt, lane); break;
+                    default: flip_cols_fast<3>(a.rows_fast, W, c0, c1, a.x_col_wt, lane); break;
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t* out = a.X.sigma + e * words_per_sigma;
+                {
+                    uint4* s4 = (uint4*)sig + lane;   // 256 words: one 16-byte store per lane
+                    const uint4 v = *s4;
+#ifdef PVAC_EXP_SIG_NTSTORE
+                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                    u32x4 nv = {v.x, v.y, v.z, v.w};
+                    __builtin_nontemporal_store(nv, (u32x4*)out + lane);
+#else
+                    ((ulonglong2*)out)[lane] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
+                                                               (uint64_t)v.z | ((uint64_t)v.w << 32));
+#endif
+                    *s4 = make_uint4(0, 0, 0, 0);
+                }
+                __builtin_amdgcn_s_setprio(0);
+                continue;
+            }
             const bool split = sw32 == 256u && bx32 + bn32 >= 768u;   // default Params: 4 copies fit
             // Full row lists (every column exactly W rows, as gen_H makes them): no per-row guard,
             // the copies sit 272 words apart (bank offset 16 g without a modular wrap), and a flip
@@ -501,7 +723,94 @@ __global__ __launch_bounds__(256) void k_gen_H(uint16_t* rows, uint32_t* counts,
     }
 }
 
+// rows_fast from rows (one thread per column c): encode (r & 31) | (r >> 5) << 7 and order the
+// column's rows by LDS bank (r >> 5) mod 32 starting at bank c mod 32 (stable within a bank)
+__global__ __launch_bounds__(256) void k_encode_fast(const uint16_t* rows, uint16_t* out, uint32_t W, uint32_t n_cols) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c >= n_cols) return;
+    const uint16_t* r = rows + (size_t)c * W;
+    uint16_t* o = out + (size_t)c * W;
+    uint32_t k = 0;
+#ifdef PVAC_EXP_SIG_NOSORT   // A/B builds only (make exp-sig): draw order kept
+    for (uint32_t i = 0; i < W; ++i) o[k++] = (uint16_t)((r[i] & 31u) | ((r[i] >> 5) << 7));
+#else
+    for (uint32_t b = 0; b < 32; ++b)   // banks c mod 32, c mod 32 + 1, ... (see flip_cols_fast)
+        for (uint32_t i = 0; i < W; ++i) {
+            const uint32_t x = r[i];
+            if ((((x >> 5) - c) & 31u) == b) o[k++] = (uint16_t)((x & 31u) | ((x >> 5) << 7));
+        }
+#endif
+}
+
+// rows_delta from rows (one thread per column): keys R = (r >> 5) | (r & 31) << 8 in ascending
+// order as byte increments with bridges and even 0-padding (see flip_cols_delta); *ovf is set when
+// a column needs more than kDeltaBytes increments
+__global__ __launch_bounds__(256) void k_encode_delta(const uint16_t* rows, uint8_t* out, uint32_t W, uint32_t n_cols,
+                                                      uint32_t* ovf) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c >= n_cols) return;
+    const uint16_t* r = rows + (size_t)c * W;
+    uint8_t* o = out + (size_t)c * kDeltaBytes;
+    uint32_t k = 0, prev = 0;
+    auto put = [&](uint32_t d) {
+        if (k < kDeltaBytes) o[k] = (uint8_t)d;
+        ++k;
+    };
+    for (uint32_t b = 0; b < 32; ++b) {   // byte 1 of R: the bit
+        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // image words holding a row with this bit
+        for (uint32_t i = 0; i < W; ++i)
+            if ((r[i] & 31u) == b) m[r[i] >> 10] |= 1u << ((r[i] >> 5) & 31u);
+        for (uint32_t j = 0; j < 8; ++j)
+            while (m[j]) {
+                const uint32_t R = (j * 32u + (uint32_t)__builtin_ctz(m[j])) | (b << 8);
+                m[j] &= m[j] - 1u;
+                while (R - prev > 255u) { put(255u); put(0u); prev += 255u; }
+                put(R - prev);
+                prev = R;
+            }
+    }
+    if (k > kDeltaBytes || (k & 1u)) atomicOr(ovf, 1u);
+    while (k < kDeltaBytes) put(0u);
+}
+
 }  // namespace
+
+// rows_delta for the default geometry (see flip_cols_delta); synchronous; left null when a column
+// does not fit kDeltaBytes (the u16 expansion is used then)
+static hipError_t build_delta_rows(sigma_tables& T, const pvac_hip_params& prm, hipStream_t st) {
+    if (T.rows_delta) { hipFree(T.rows_delta); T.rows_delta = nullptr; }
+    if (!(prm.m_bits == 8192 && prm.x_col_wt == 128 && T.full && T.rows &&
+          sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords))
+        return hipSuccess;
+    uint32_t* ovf = nullptr;
+    hipError_t e = hipMalloc(&T.rows_delta, (size_t)T.n_cols * kDeltaBytes);
+    if (e == hipSuccess) e = hipMalloc(&ovf, 4);
+    if (e == hipSuccess) e = hipMemsetAsync(ovf, 0, 4, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_encode_delta, dim3((T.n_cols + 255) / 256), dim3(256), 0, st, T.rows, T.rows_delta, T.width,
+                           T.n_cols, ovf);
+        e = hipGetLastError();
+    }
+    uint32_t h = 1;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, ovf, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipFree(ovf);
+    if (e != hipSuccess || h) { hipFree(T.rows_delta); T.rows_delta = nullptr; }
+    return e;
+}
+
+// rows_fast for the default geometry (see flip_cols_fast); other geometries keep rows only
+static hipError_t build_fast_rows(sigma_tables& T, const pvac_hip_params& prm, hipStream_t st) {
+    if (T.rows_fast) { hipFree(T.rows_fast); T.rows_fast = nullptr; }
+    if (!(prm.m_bits == 8192 && prm.x_col_wt == 128 && T.full && T.width % 8 == 0 && T.width >= 8 &&
+          sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords))
+        return hipSuccess;
+    hipError_t e = hipMalloc(&T.rows_fast, (size_t)T.n_cols * T.width * 2);
+    if (e != hipSuccess) { T.rows_fast = nullptr; return e; }
+    hipLaunchKernelGGL(k_encode_fast, dim3((T.n_cols + 255) / 256), dim3(256), 0, st, T.rows, T.rows_fast, T.width,
+                       T.n_cols);
+    return hipGetLastError();
+}
 
 // host SHA-256 over a contiguous buffer
 void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]) {
@@ -532,6 +841,8 @@ void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]) {
 void sigma_tables_free(sigma_tables& T) {
     hipFree(T.rows);
     hipFree(T.counts);
+    hipFree(T.rows_fast);
+    hipFree(T.rows_delta);
     T = sigma_tables{};
 }
 
@@ -573,6 +884,8 @@ hipError_t sigma_tables_from_dense(sigma_tables& T, const pvac_hip_params& prm, 
     T.full = std::all_of(cnt.begin(), cnt.end(), [&](uint32_t k) { return k == width; });
     if (e == hipSuccess) e = hipMemcpyAsync(T.rows, rows.data(), rows.size() * 2, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(T.counts, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = build_fast_rows(T, prm, st);
+    if (e == hipSuccess) e = build_delta_rows(T, prm, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     T.ready = e == hipSuccess;
     return e;
@@ -589,6 +902,8 @@ hipError_t sigma_tables_generate(sigma_tables& T, const pvac_hip_params& prm, ui
     hipLaunchKernelGGL(k_gen_H, dim3(2048), dim3(256), lds, st, T.rows, T.counts, T.width, prm.m_bits, prm.n_bits,
                        prm.h_col_wt, prm.canon_tag);
     e = hipGetLastError();
+    if (e == hipSuccess) e = build_fast_rows(T, prm, st);
+    if (e == hipSuccess) e = build_delta_rows(T, prm, st);
     if (e != hipSuccess) return e;
     if (digest) {
         std::vector<uint16_t> rows((size_t)prm.n_bits * T.width);
@@ -627,6 +942,25 @@ hipError_t launch_sigma(const sigma_tables& T, const pvac_hip_params& prm, const
     a.salts = salts;
     a.salt_pos = salt_pos;
     a.rows = T.rows;
+    // PVAC_SIGMA_FAST=1 selects the previous (per-lane-group image copies) expansion, for A/B runs
+    static const bool old_fast = [] {
+        const char* v = std::getenv("PVAC_SIGMA_FAST");
+        return v && v[0] == '1';
+    }();
+#ifdef PVAC_EXP_SIG_OLD   // A/B builds only (make exp-sig)
+    const bool exp_old = true;
+#else
+    const bool exp_old = false;
+#endif
+    a.rows_fast = (T.rows_fast && !old_fast && !exp_old && prm.m_bits == 8192 && prm.x_col_wt == 128 && T.full &&
+                   sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords)
+                      ? T.rows_fast : nullptr;
+#ifdef PVAC_EXP_SIG_U16   // A/B builds only: the u16 row expansion
+    const bool exp_u16 = true;
+#else
+    const bool exp_u16 = false;
+#endif
+    a.rows_delta = (a.rows_fast && T.rows_delta && !exp_u16) ? T.rows_delta : nullptr;
     a.counts = T.counts;
     a.width = T.width;
     a.full = T.full ? 1u : 0u;
