@@ -20,6 +20,7 @@
 #include <vector>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "common.hpp"
 #include "sha256.hpp"
@@ -216,9 +217,8 @@ __host__ __device__ constexpr uint32_t sigma_wave_words(uint32_t m_bits, uint32_
 // columns). Wave WV's sigma image sits at a compile-time LDS address, and rows_fast encodes a row
 // r as (r & 31) | (r >> 5) << 7, so a flip is one bit-field extract (or shift) for the byte
 // offset, folded into the ds_xor's immediate base, and one shift for the bit: two VALU per flip.
-// Each column's rows are sorted by LDS bank, starting at bank c mod 32, and the caller deals the
-// columns to lanes so that the 32 lanes of one LDS cycle start at distinct banks: the lanes of one
-// ds_xor then spread over the banks instead of hitting them at random.
+// (The fallback when rows_delta is unavailable; bank-sorted row orders with bank-matched column
+// assignment, lane-rotated chunk orders and deeper load batches were measured and rejected.)
 constexpr uint32_t kFastWaveWords = sigma_wave_words(8192, 16384, 128);
 // LDS atomic XOR at an absolute LDS byte address (the dynamic LDS of k_sigma starts at 0: it has
 // no static __shared__ data; the kernel checks this before taking the fast path)
@@ -235,56 +235,17 @@ __device__ __forceinline__ void flip_cols_fast(const uint16_t* rows_fast, uint32
         lds_xor(img + __builtin_amdgcn_ubfe(x, 5, 10), 1u << (x & 31u));
         lds_xor(img + (x >> 21), 1u << ((x >> 16) & 31u));
     };
-#ifdef PVAC_EXP_SIG_PAIR   // A/B: both columns' chunks in one batch (4 + 4 loads in flight)
-    if (ncols == 128u) {
-        const uint4* r0 = (const uint4*)(rows_fast + (size_t)c0 * W);
-        const uint4* r1 = (const uint4*)(rows_fast + (size_t)c1 * W);
-        for (uint32_t q4 = 0; q4 < nch; q4 += 4) {
-            uint4 v[8];
-#pragma unroll
-            for (uint32_t b = 0; b < 4; ++b) {
-                v[b] = q4 + b < nch ? r0[q4 + b] : make_uint4(0, 0, 0, 0);
-                v[4 + b] = q4 + b < nch ? r1[q4 + b] : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (uint32_t b = 0; b < 8; ++b) {
-                if (q4 + (b & 3u) >= nch) continue;
-                flip2(v[b].x); flip2(v[b].y); flip2(v[b].z); flip2(v[b].w);
-            }
-        }
-        return;
-    }
-#endif
 #pragma unroll 1
     for (uint32_t cc = 0; cc < 2; ++cc) {
         if ((uint32_t)lane + 64u * cc >= ncols) break;
         const uint4* rp = (const uint4*)(rows_fast + (size_t)(cc ? c1 : c0) * W);
-#ifdef PVAC_EXP_SIG_KB12
-        constexpr uint32_t kB = 12;
-#else
         constexpr uint32_t kB = 8;
-#endif
         for (uint32_t q8 = 0; q8 < nch; q8 += kB) {
             uint4 v[kB];
 #pragma unroll
             for (uint32_t b = 0; b < kB; ++b) {
-#ifdef PVAC_EXP_SIG_NOLOAD   // timing experiment: pseudo-random rows, no table reads (sigma wrong)
-                const uint32_t h = ((cc ? c1 : c0) * 0x9E3779B1u + (q8 + b) * 0x85EBCA77u) ^ (uint32_t)lane;
-                v[b] = make_uint4(h & 0x7F9F7F9Fu, (h * 0xC2B2AE3Du) & 0x7F9F7F9Fu, (h * 0x27D4EB2Fu) & 0x7F9F7F9Fu,
-                                  (h * 0x165667B1u) & 0x7F9F7F9Fu);
-#else
                 v[b] = q8 + b < nch ? rp[q8 + b] : make_uint4(0, 0, 0, 0);
-#endif
             }
-#ifdef PVAC_EXP_SIG_NOFLIP   // timing experiment: rows read, one LDS op per batch (sigma wrong)
-            {
-                uint32_t z = 0;
-#pragma unroll
-                for (uint32_t b = 0; b < kB; ++b) z ^= v[b].x ^ v[b].y ^ v[b].z ^ v[b].w;
-                lds_xor(img + __builtin_amdgcn_ubfe(z, 5, 10), 1u << (z & 31u));
-                continue;
-            }
-#endif
 #pragma unroll
             for (uint32_t b = 0; b < kB; ++b) {
                 if (q8 + b >= nch) break;
@@ -328,15 +289,33 @@ __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0,
         uint32_t R = 0;
         {
             uint4 v[8];
+#ifdef PVAC_EXP_SIG_DNOLOAD   // timing experiment: synthetic increments, no table reads (sigma wrong)
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t h = ((cc ? c1 : c0) * 0x9E3779B1u + b * 0x85EBCA77u);
+                v[b] = make_uint4(h & 0x3F3F3F3Fu, (h * 0xC2B2AE3Du) & 0x3F3F3F3Fu, (h * 0x27D4EB2Fu) & 0x3F3F3F3Fu,
+                                  (h * 0x165667B1u) & 0x3F3F3F3Fu);
+            }
+#else
 #pragma unroll
             for (int b = 0; b < 8; ++b) v[b] = rp[b];
+#endif
 #pragma unroll
             for (int b = 0; b < 8; ++b) { word4(R, v[b].x); word4(R, v[b].y); word4(R, v[b].z); word4(R, v[b].w); }
         }
         {
             uint4 v[5];
+#ifdef PVAC_EXP_SIG_DNOLOAD
+#pragma unroll
+            for (int b = 0; b < 5; ++b) {
+                const uint32_t h = ((cc ? c1 : c0) * 0x9E3779B1u + (b + 8) * 0x85EBCA77u);
+                v[b] = make_uint4(h & 0x3F3F3F3Fu, (h * 0xC2B2AE3Du) & 0x3F3F3F3Fu, (h * 0x27D4EB2Fu) & 0x3F3F3F3Fu,
+                                  (h * 0x165667B1u) & 0x3F3F3F3Fu);
+            }
+#else
 #pragma unroll
             for (int b = 0; b < 5; ++b) v[b] = rp[8 + b];
+#endif
 #pragma unroll
             for (int b = 0; b < 5; ++b) { word4(R, v[b].x); word4(R, v[b].y); word4(R, v[b].z); word4(R, v[b].w); }
         }
@@ -488,7 +467,15 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             // different groups never contend for a word. Copy 0 already holds the noise bits.
             const uint32_t W = a.width;
             if (a.rows_delta && lds_at0) {   // host-checked: default Params, kFastWaveWords per wave
+#if defined(PVAC_EXP_SIG_PRIO0)
+                __builtin_amdgcn_s_setprio(0);
+#elif defined(PVAC_EXP_SIG_PRIO1)
+                __builtin_amdgcn_s_setprio(1);
+#elif defined(PVAC_EXP_SIG_PRIO3)
+                __builtin_amdgcn_s_setprio(3);
+#else
                 __builtin_amdgcn_s_setprio(2);   // LDS-atomic phase ahead of other waves' SHA-256
+#endif
                 const uint32_t c0 = cols[lane], c1 = cols[lane + 64];   // x_col_wt == 128
                 for (uint32_t w4 = lane; w4 < (bx32 + bn32) / 4u; w4 += 64) ((uint4*)bmX)[w4] = make_uint4(0, 0, 0, 0);
 #ifdef PVAC_EXP_SIG_NOEXP   // timing experiment: no column expansion (sigma wrong)
@@ -514,40 +501,9 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
             }
             if (a.rows_fast && lds_at0) {   // host-checked: default Params, full columns, kFastWaveWords per wave
                 __builtin_amdgcn_s_setprio(2);   // LDS-atomic phase ahead of other waves' SHA-256
-#ifdef PVAC_EXP_SIG_NOMATCH   // A/B: columns in selection order
                 const uint32_t c0 = (uint32_t)lane < a.x_col_wt ? cols[lane] : 0u;
                 const uint32_t c1 = (uint32_t)lane + 64u < a.x_col_wt ? cols[lane + 64] : 0u;
                 for (uint32_t w4 = lane; w4 < (bx32 + bn32) / 4u; w4 += 64) ((uint4*)bmX)[w4] = make_uint4(0, 0, 0, 0);
-#else
-                // Bank matching (x_col_wt == 128): column c's rows start at bank c mod 32 and walk the
-                // banks upward, so 32 lanes whose columns have distinct c mod 32 hit distinct banks at
-                // every step. The 128 columns are counting-sorted by c mod 32 (the dead selection
-                // bitmaps hold the histogram and the sorted list) and round j = 2 k + g (group g =
-                // lane >> 5, slot k) takes sorted positions j, j + 4, ..., j + 124.
-                for (uint32_t w4 = lane; w4 < (bx32 + bn32) / 4u; w4 += 64) ((uint4*)bmX)[w4] = make_uint4(0, 0, 0, 0);
-                __builtin_amdgcn_wave_barrier();
-                uint32_t c0, c1;
-                {
-                    uint32_t* hist = bmX;
-                    uint16_t* srt = (uint16_t*)(bmX + 32);
-                    const uint32_t ca = cols[lane], cb = cols[lane + 64];
-                    const uint32_t pa = atomicAdd(&hist[ca & 31u], 1u);
-                    const uint32_t pb = atomicAdd(&hist[cb & 31u], 1u);
-                    __builtin_amdgcn_wave_barrier();
-                    const uint32_t h = lane < 32 ? hist[lane] : 0u;
-                    const uint32_t ex = wave_incl_scan_u32(h) - h;
-                    const uint32_t ba = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ca & 31u) << 2), (int)ex);
-                    const uint32_t bb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((cb & 31u) << 2), (int)ex);
-                    srt[ba + pa] = (uint16_t)ca;
-                    srt[bb + pb] = (uint16_t)cb;
-                    __builtin_amdgcn_wave_barrier();
-                    const uint32_t i4 = 4u * ((uint32_t)lane & 31u) + ((uint32_t)lane >> 5);
-                    c0 = srt[i4];
-                    c1 = srt[i4 + 2u];
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane < 24) ((uint4*)bmX)[lane] = make_uint4(0, 0, 0, 0);   // hist + srt: 96 words
-                }
-#endif
 #ifdef PVAC_EXP_SIG_NOEXP   // timing experiment: no column expansion (sigma wrong)
                 if (a.width == 0x7FFFFFFFu)
 #endif
@@ -562,14 +518,8 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                 {
                     uint4* s4 = (uint4*)sig + lane;   // 256 words: one 16-byte store per lane
                     const uint4 v = *s4;
-#ifdef PVAC_EXP_SIG_NTSTORE
-                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                    u32x4 nv = {v.x, v.y, v.z, v.w};
-                    __builtin_nontemporal_store(nv, (u32x4*)out + lane);
-#else
                     ((ulonglong2*)out)[lane] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
                                                                (uint64_t)v.z | ((uint64_t)v.w << 32));
-#endif
                     *s4 = make_uint4(0, 0, 0, 0);
                 }
                 __builtin_amdgcn_s_setprio(0);
@@ -723,23 +673,13 @@ __global__ __launch_bounds__(256) void k_gen_H(uint16_t* rows, uint32_t* counts,
     }
 }
 
-// rows_fast from rows (one thread per column c): encode (r & 31) | (r >> 5) << 7 and order the
-// column's rows by LDS bank (r >> 5) mod 32 starting at bank c mod 32 (stable within a bank)
+// rows_fast from rows (one thread per column): encode (r & 31) | (r >> 5) << 7, draw order kept
 __global__ __launch_bounds__(256) void k_encode_fast(const uint16_t* rows, uint16_t* out, uint32_t W, uint32_t n_cols) {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
     if (c >= n_cols) return;
     const uint16_t* r = rows + (size_t)c * W;
     uint16_t* o = out + (size_t)c * W;
-    uint32_t k = 0;
-#ifdef PVAC_EXP_SIG_NOSORT   // A/B builds only (make exp-sig): draw order kept
-    for (uint32_t i = 0; i < W; ++i) o[k++] = (uint16_t)((r[i] & 31u) | ((r[i] >> 5) << 7));
-#else
-    for (uint32_t b = 0; b < 32; ++b)   // banks c mod 32, c mod 32 + 1, ... (see flip_cols_fast)
-        for (uint32_t i = 0; i < W; ++i) {
-            const uint32_t x = r[i];
-            if ((((x >> 5) - c) & 31u) == b) o[k++] = (uint16_t)((x & 31u) | ((x >> 5) << 7));
-        }
-#endif
+    for (uint32_t i = 0; i < W; ++i) o[i] = (uint16_t)((r[i] & 31u) | ((r[i] >> 5) << 7));
 }
 
 // rows_delta from rows (one thread per column): keys R = (r >> 5) | (r & 31) << 8 in ascending
@@ -942,28 +882,26 @@ hipError_t launch_sigma(const sigma_tables& T, const pvac_hip_params& prm, const
     a.salts = salts;
     a.salt_pos = salt_pos;
     a.rows = T.rows;
-    // PVAC_SIGMA_FAST=1 selects the previous (per-lane-group image copies) expansion, for A/B runs
-    static const bool old_fast = [] {
-        const char* v = std::getenv("PVAC_SIGMA_FAST");
-        return v && v[0] == '1';
-    }();
-#ifdef PVAC_EXP_SIG_OLD   // A/B builds only (make exp-sig)
-    const bool exp_old = true;
-#else
-    const bool exp_old = false;
+    // Column expansion: byte-delta tables (default), else u16 rows with per-wave images, else the
+    // per-lane-group image copies, else the generic guarded loop. PVAC_SIGMA_PATH = delta | u16 |
+    // copies | generic caps the choice (read per launch: A/B runs and the tests of every path).
+    int path = 0;
+    if (const char* v = std::getenv("PVAC_SIGMA_PATH")) {
+        const std::string pv(v);
+        path = pv == "u16" ? 1 : pv == "copies" ? 2 : pv == "generic" ? 3 : 0;
+    }
+#if defined(PVAC_EXP_SIG_OLD)   // A/B builds only (make exp-sig)
+    path = 2;
+#elif defined(PVAC_EXP_SIG_U16)
+    path = 1;
 #endif
-    a.rows_fast = (T.rows_fast && !old_fast && !exp_old && prm.m_bits == 8192 && prm.x_col_wt == 128 && T.full &&
-                   sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords)
-                      ? T.rows_fast : nullptr;
-#ifdef PVAC_EXP_SIG_U16   // A/B builds only: the u16 row expansion
-    const bool exp_u16 = true;
-#else
-    const bool exp_u16 = false;
-#endif
-    a.rows_delta = (a.rows_fast && T.rows_delta && !exp_u16) ? T.rows_delta : nullptr;
+    const bool fast_ok = prm.m_bits == 8192 && prm.x_col_wt == 128 && T.full &&
+                         sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords;
+    a.rows_fast = (fast_ok && path <= 1) ? T.rows_fast : nullptr;
+    a.rows_delta = (a.rows_fast && path == 0) ? T.rows_delta : nullptr;
     a.counts = T.counts;
     a.width = T.width;
-    a.full = T.full ? 1u : 0u;
+    a.full = (T.full && path <= 2) ? 1u : 0u;
     a.canon = prm.canon_tag;
     a.n_bits = prm.n_bits;
     a.m_bits = prm.m_bits;

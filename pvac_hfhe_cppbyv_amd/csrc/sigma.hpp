@@ -11,9 +11,8 @@ namespace pvhip {
 struct sigma_tables {
     uint16_t* rows = nullptr;
     uint32_t* counts = nullptr;
-    // m_bits == 8192 and full columns only: the same rows re-encoded for k_sigma's fast column
-    // expansion, (r & 31) | (r >> 5) << 7 (so bits 5..14 are the image byte offset), each column's
-    // rows sorted by LDS bank (word mod 32)
+    // m_bits == 8192, x_col_wt == 128 and full columns only: the same rows re-encoded for k_sigma's
+    // fast column expansion, (r & 31) | (r >> 5) << 7 (bits 5..14 are the image byte offset)
     uint16_t* rows_fast = nullptr;
     // the same default-geometry columns as 208 byte increments of R = (r >> 5) | (r & 31) << 8
     // (see k_sigma.hip flip_cols_delta); null when unavailable

@@ -428,6 +428,40 @@ def test_sigma_batch_matches_oracle(engine, oracle):
             k += 1
 
 
+@pytest.mark.parametrize("path", ["delta", "u16", "copies", "generic"])
+def test_sigma_expansion_paths(engine, oracle, monkeypatch, path):
+    """Every column-expansion path of k_sigma (PVAC_SIGMA_PATH: byte-delta tables, u16 rows with
+    per-wave images, per-lane-group copies, the generic guarded loop) gives the oracle's
+    sigma_from_H on a sample, and the same bytes as the default path on 2,600 edges."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=77)
+    H, _ = oracle.gen_H(77)
+    eng.set_H(H)
+    X = eng.gen_fresh(65, 41, 20)
+    ne = X.meta.numel()
+    salts = eng.torch.empty(ne, dtype=eng.torch.int64, device=eng.device)
+    eng.fill_random(salts, 12)
+    X.sigma = eng.torch.zeros((ne, 128), dtype=eng.torch.int64, device=eng.device)
+    monkeypatch.delenv("PVAC_SIGMA_PATH", raising=False)
+    eng.sigma(X, salts)
+    ref_all = X.sigma.clone()
+    X.sigma.fill_(-1)
+    monkeypatch.setenv("PVAC_SIGMA_PATH", path)
+    eng.sigma(X, salts)
+    eng.torch.cuda.synchronize()
+    assert eng.torch.equal(X.sigma, ref_all)
+    hs = X.to_host()
+    sl = salts.cpu().numpy().view(np.uint64)
+    k = 0
+    for c in hs[:3]:
+        for e in range(c.nE):
+            L = c.layers[int(c.meta[e]) & 0xFFFFFFFF]
+            ref = oracle.sigma(77, H, int(L["ztag"]), int(L["nonce_lo"]), int(L["nonce_hi"]),
+                               (int(c.meta[e]) >> 32) & 0xFFFF, (int(c.meta[e]) >> 48) & 0xFF, int(sl[k]))
+            assert np.array_equal(c.sigma[e], ref), (path, k)
+            k += 1
+
+
 def _pair_host(X, p):
     """Cipher p of a device batch, copied alone (no full-batch transfer)."""
     from helpers import LAYER_DT
