@@ -522,6 +522,26 @@ def sigma_bench(eng, args, with_cpu):
     full = {"pairs": ns, "ct_mul_per_s": ns / el, "ms_per_batch": el * 1000,
             "sigma_kernel_ms": sig_avg, "sigma_GBs": sig_bytes / (sig_avg / 1000.0) / 1e9,
             "edges": edges}
+    # self-check (untimed): the same batch through two other column expansions of k_sigma (u16 rows,
+    # the generic guarded loop: different tables and decoders, same selection) gives the same bytes
+    # for every sigma of the batch (PVAC_SIGMA_PATH, read per launch)
+    if os.environ.get("PVAC_SIGMA_PATH") is None:
+        agree = {}
+        cnt = Cs.e_cnt[:ns].long()
+        start = torch.repeat_interleave(Cs.e_off[:ns].long() - (torch.cumsum(cnt, 0) - cnt), cnt)
+        rows = start + torch.arange(int(cnt.sum().item()), device=dev)   # the written edge slots
+        ref = Cs.sigma[rows].clone()
+        for path in ("u16", "generic"):
+            os.environ["PVAC_SIGMA_PATH"] = path
+            try:
+                Cb2, plan2 = eng.ct_mul_plan(A, B)
+                C2 = eng.ct_mul(A, B, nonces=nonces, salts=salts, flags=MUL_WITH_SIGMA, C_=Cb2, plan=plan2)
+                torch.cuda.synchronize(dev)
+                agree[path] = bool(torch.equal(C2.sigma[rows], ref))
+            finally:
+                del os.environ["PVAC_SIGMA_PATH"]
+            del C2, Cb2
+        full["checks"] = {"sigma_paths_agree": all(agree.values()), "paths": ["delta"] + list(agree)}
     if with_cpu:
         full["cpu_baseline"] = _ref_full_baseline()
     return full
