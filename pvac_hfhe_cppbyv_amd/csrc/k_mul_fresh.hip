@@ -1541,9 +1541,10 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 const uint32_t lp = __umulhi(s, bdiv);
                 const uint32_t r = s - lp * Bm;
                 const uint32_t lid = ident ? base + lp : remap[base + lp];
-                cm[p] = make_meta(lid, r, cell & 1u);
-                cl[p] = w.lo;
-                chh[p] = w.hi;
+                // streaming stores: the output is not read again by this kernel (-1%, A/B)
+                __builtin_nontemporal_store((unsigned long long)make_meta(lid, r, cell & 1u), (unsigned long long*)cm + p);
+                __builtin_nontemporal_store((unsigned long long)w.lo, (unsigned long long*)cl + p);
+                __builtin_nontemporal_store((unsigned long long)w.hi, (unsigned long long*)chh + p);
                 if (sp) sp[p] = p;   // hash order == emit order here
             }
             if (zero) misc[F3_ZERO] = 1u;
