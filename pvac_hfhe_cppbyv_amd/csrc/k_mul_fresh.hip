@@ -980,6 +980,10 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
     return x;
 }
 
+#ifndef PVAC_F3_BS   // A/B builds only: workgroup size of k_ct_mul_fresh3
+#define PVAC_F3_BS 512
+#endif
+constexpr uint32_t kF3Threads = PVAC_F3_BS;
 template <int BS>
 __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* __restrict__ gp, fresh3_layout Ls) {
     constexpr int KI = (kFreshKeysMax + BS - 1) / BS;    // key slots per thread (rebuild)
@@ -990,7 +994,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
     constexpr int U = 4;                                 // product rounds per pass
     constexpr uint32_t kT16 = 0xFFFFu;                   // no first-insert time
     constexpr uint32_t kBig = 7u;                        // slot record: more than 3 bucket mates
-    static_assert(BS == (int)kFreshThreads && BS >= (int)kFreshEdgesMax && NW <= 16, "fresh geometry");
+    static_assert(BS % 64 == 0 && BS >= (int)kFreshEdgesMax && NW <= 16, "fresh geometry");
     static_assert(kFreshProdMax <= 16u * 256u, "16 scan segments of 256 product times");
     argp gq = launder((uint64_t)gp);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1619,7 +1623,7 @@ hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* ar
         static int occ_cache[2] = {-1, 0};   // {LDS bytes, blocks per CU}
         if (occ_cache[0] != (int)L.total) {
             int nb = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ct_mul_fresh3<kFreshThreads>, kFreshThreads,
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ct_mul_fresh3<kF3Threads>, kF3Threads,
                                                               L.total) != hipSuccess || nb < 1)
                 nb = 1;
             occ_cache[0] = (int)L.total;
@@ -1634,7 +1638,7 @@ hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* ar
         if (const char* e = std::getenv("PVAC_FRESH_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
         uint64_t blocks = (uint64_t)num_cus * per_cu;
         if (blocks > a.A.n) blocks = a.A.n;
-        hipLaunchKernelGGL((k_ct_mul_fresh3<kFreshThreads>), dim3((unsigned)blocks), dim3(kFreshThreads), L.total, st,
+        hipLaunchKernelGGL((k_ct_mul_fresh3<kF3Threads>), dim3((unsigned)blocks), dim3(kF3Threads), L.total, st,
                            args_dev, L);
         return hipGetLastError();
     }
