@@ -24,6 +24,30 @@ PVH_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 #endif
 }
 
+// majority(a, b, c) in one VALU instruction (v_bitop3_b32, truth table 0xE8); the compiler emits
+// three (xor, and, bitop3) for the expression
+PVH_HD uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
+
+// x + y + k with the round constant k in an SGPR: one v_add3_u32 (gfx950 VOP3 takes no literal, so
+// the compiler otherwise spends a VOP2 add on the literal and a second add)
+PVH_HD uint32_t add3k(uint32_t x, uint32_t y, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "s"(k));
+    return r;
+#else
+    return x + y + k;
+#endif
+}
+
 struct sha_state { uint32_t h[8]; };
 
 PVH_HD void sha_init(sha_state& s) {
@@ -61,9 +85,9 @@ PVH_HD void sha_compress(sha_state& s, const uint32_t blk[16]) {
         }
         const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
         const uint32_t ch = (e & f) ^ (~e & g);
-        const uint32_t t1 = h + S1 + ch + kSHA_K[i] + wi;
+        const uint32_t t1 = add3k(h, wi, kSHA_K[i]) + S1 + ch;
         const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
-        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        const uint32_t mj = maj3(a, b, c);
         const uint32_t t2 = S0 + mj;
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
