@@ -542,9 +542,9 @@ def sigma_bench(eng, args, with_cpu):
                 del os.environ["PVAC_SIGMA_PATH"]
             del C2, Cb2
         full["checks"] = {"sigma_paths_agree": all(agree.values()), "paths": ["delta"] + list(agree)}
-    # k_sigma is not HBM-bound (1 KiB written per edge): its roofline is integer-VALU issue (PMC
-    # VALU count per launch of this batch, profiles/r02/pmc_sigma, over the kernel time, against
-    # the ceiling measured now) with the LDS pipe beside it
+    # k_sigma is not HBM-bound (1 KiB written per edge): it is bound by the LDS pipe (its atomic-XOR
+    # flips, bank conflicts in most of the LDS cycles; PMC, profiles/r02/pmc_sigma) with integer VALU
+    # beside it (PMC VALU count per launch over this kernel time, against the ceiling measured now)
     try:
         with open(os.path.join(ROOT, "profiles", "r02", "pmc_sigma", "summary.json")) as f:
             ks = json.load(f).get("k_sigma", {})
@@ -553,11 +553,14 @@ def sigma_bench(eng, args, with_cpu):
         ceil_w = eng.alu_ceiling(0)
         if ks and notes.get("edges_per_launch") == int(edges) and sig_avg > 0 and ceil_w:
             ach = ks["SQ_INSTS_VALU"] / (sig_avg / 1000.0)
-            full["roofline"] = {"bound": "valu", "achieved": ach, "peak": ceil_w, "unit": "wave64 VALU inst/s",
-                                "frac": ach / ceil_w, "valu_per_edge": ks["SQ_INSTS_VALU"] / edges,
-                                "lds_bank_conflict_frac": ks.get("lds_bank_conflict_frac"),
-                                "source": "SQ_INSTS_VALU per launch (profiles/r02/pmc_sigma) / kernel time; "
-                                          "peak: pvac_hip_alu_ceiling(0) on this GPU"}
+            full["roofline"] = {
+                "bound": "lds",
+                "lds_busy_frac": notes.get("lds_busy_frac"),
+                "lds_bank_conflict_frac": ks.get("lds_bank_conflict_frac"),
+                "valu": {"achieved": ach, "peak": ceil_w, "unit": "wave64 VALU inst/s", "frac": ach / ceil_w,
+                         "per_edge": ks["SQ_INSTS_VALU"] / edges},
+                "source": "PMC of this batch (profiles/r02/pmc_sigma: SQ_LDS_IDX_ACTIVE / CU cycles, "
+                          "SQ_LDS_BANK_CONFLICT, SQ_INSTS_VALU); VALU peak: pvac_hip_alu_ceiling(0) on this GPU"}
     except Exception:
         pass
     if with_cpu:
