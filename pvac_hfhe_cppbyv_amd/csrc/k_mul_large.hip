@@ -232,19 +232,23 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                         const uint32_t dd = r >= sidx ? r - sidx : r + Bm - sidx;
                         const ulonglong2 sw = swv[q];
                         const uint32_t se = sidv[q];
-#pragma unroll
-                        for (uint32_t c = 0; c < 2; ++c) {
-                            const uint32_t e = di[2 * dd + c];
+                        // the dense slot of channel sch meets sparse channel sch (P), the other one
+                        // gives M: reading the slots in that order keeps each sum in fixed registers
+                        // (a select between the P and M accumulators made the compiler copy one of
+                        // them back, 5 moves per product)
+                        auto probe = [&](uint32_t slot, acc128c& acc) {
+                            const uint32_t e = di[slot];
                             if (e != kInf) {
-                                const ulonglong2 dv = dw[2 * dd + c];
+                                const ulonglong2 dv = dw[slot];
                                 uint64_t x0, x1;
                                 fp_mul_fold1(fp{dv.x, dv.y}, fp{sw.x, sw.y}, x0, x1);
-                                if (c == sch) acc_add(P[u], x0, x1);
-                                else acc_add(M[u], x0, x1);
+                                acc_add(acc, x0, x1);
                                 const uint32_t t = e + se;
                                 tmin[u] = t < tmin[u] ? t : tmin[u];
                             }
-                        }
+                        };
+                        probe(2 * dd + sch, P[u]);
+                        probe(2 * dd + (sch ^ 1u), M[u]);
                     }
                 }
             }
