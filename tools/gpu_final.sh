@@ -12,6 +12,11 @@ tail -1 gpurun_out/final/bench.log | cut -c1-600
 (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/final/prof" -o run --output-format csv \
     -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/final/prof.log" 2>&1) || exit $?
 echo prof ok
+# the headline command alone (no side legs): rocprof's average for k_ct_mul_fresh3 is then the
+# bench line's avg_kernel_ms
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/final/prof_headline" -o run --output-format csv \
+    -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu --no-extras > "$GRAFT_REPO_ROOT/gpurun_out/final/prof_headline.log" 2>&1) || exit $?
+echo prof headline ok
 # N>1 rehearsal (2 gloo ranks on cuda:0) and one rank at the N>1 shard size (2^21 pairs)
 PVAC_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --pairs 262144 \
