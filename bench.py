@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--cpu-share-threads", type=int, default=16, help="second CPU baseline: the box's CPU share")
     ap.add_argument("--sigma-pairs", type=int, default=1 << 12)
     ap.add_argument("--chain-inputs", type=int, default=1 << 16, help="cfg 4 chain inputs (enc_value outputs)")
-    ap.add_argument("--chain-chunk", type=int, default=1 << 10)
+    ap.add_argument("--chain-chunk", type=int, default=1 << 12)
     ap.add_argument("--chain-depth", type=int, default=8)
     ap.add_argument("--chain-streams", type=int, default=1,
                     help="host threads / HIP streams running chunks (2 measured no faster: the products kernel is VALU-bound)")
@@ -645,6 +645,7 @@ def chain_bench(eng, args):
     dev = eng.device
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
     S = max(1, args.chain_streams)
+    torch.cuda.reset_peak_memory_stats(dev)
     _enc_keys(eng)
     vals = torch.empty(n, dtype=torch.int64, device=dev)
     rnd = torch.empty(n * ENC_STRIDE, dtype=torch.int64, device=dev)
@@ -751,7 +752,8 @@ def chain_bench(eng, args):
            "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
            "edges_per_input_by_step": [e / n for e in step_edges],
-           "stream_ms_by_step": step_ms, "last_step_ms_by_chunk": [r["last_ms"] for r in results]}
+           "stream_ms_by_step": step_ms, "last_step_ms_by_chunk": [r["last_ms"] for r in results],
+           "peak_hbm_reserved_gb": torch.cuda.max_memory_reserved(dev) / 1e9}
     gf, gp = sum(r["gsum_failed"] for r in results), sum(r["gsum_pairs"] for r in results)
     out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
                                  "step, on the device (untimed)", "pair_steps": gp, "failed": gf,
