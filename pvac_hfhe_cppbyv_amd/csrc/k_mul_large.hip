@@ -44,6 +44,18 @@ __device__ __forceinline__ uint64_t* w64(uint32_t* s, uint64_t o) { return (uint
 
 __device__ __forceinline__ uint32_t mod_small(uint32_t x, uint32_t B) { return x >= B ? x - B : x; }
 
+// a bucket leader with first-insert time t and E > 0 edges: its 2-bit edge code lands in the u64
+// of its 16-time block (times are unique, so the add is an OR) and E in the block's count
+__device__ __forceinline__ void leader_mark(unsigned long long* bpack, uint32_t t, uint32_t E) {
+    const uint64_t code = E < 3u ? E : 3u;
+    atomicAdd(&bpack[t >> 4], ((unsigned long long)E << 32) | (code << (2u * (t & 15u))));
+}
+
+// static bucket groups (large_desc::g_head): 0 = the key is alone in its libstdc++ bucket
+__device__ __forceinline__ const uint32_t* group_heads(const mul_large_args& g, const large_desc& d) {
+    return d.g_head != kNoGrp ? g.grp + d.g_head : nullptr;
+}
+
 // workgroup exclusive scan for any multiple-of-64 block size
 template <int BS>
 __device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* part, uint32_t& total) {
@@ -170,6 +182,10 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
     uint32_t* tkey = S + d.o_tkey;
     uint32_t* info = S + d.o_info;
     ulonglong2* sums = (ulonglong2*)(S + d.o_sums);
+    // keys alone in their bucket are their own bucket leaders: mark them here, where the atomic
+    // overlaps the multiply-bound loop of other waves, and `rank` skips them
+    const uint32_t* ghead = group_heads(g, d);
+    unsigned long long* bpack = (unsigned long long*)w64(S, d.o_bmask);
     bool any = false;
 
     bool dense = nd >= kLargeDenseMin;
@@ -265,6 +281,7 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                     sums[2 * s] = make_ulonglong2(ps.lo, ps.hi);
                     sums[2 * s + 1] = make_ulonglong2(ms.lo, ms.hi);
                     any |= eb != 0;
+                    if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tmin[u], __popc(eb));
                 }
             }
         }
@@ -306,6 +323,7 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                 sums[2 * s] = make_ulonglong2(p.lo, p.hi);
                 sums[2 * s + 1] = make_ulonglong2(m.lo, m.hi);
                 any |= eb != 0;
+                if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tkr, __popc(eb));
             }
         }
     }
@@ -444,14 +462,17 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     const uint32_t* ghead = g.grp + (stat ? d.g_head : 0);
     const uint32_t* gnext = g.grp + (stat ? d.g_next : 0);
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
+        // static groups: a key alone in its bucket (the common case) was marked by `products`
+        // and `order` takes t_b = its own time, within = 0
+        const uint32_t q0 = stat ? ghead[s] : 1u;
+        if (!q0) continue;
         const uint32_t t = tkey[s];
         if (t == kInf) continue;
         uint32_t tmin = t, w = 0, E = 0;
         if (stat) {
             // the bucket's slots are a static property of (bucket count, B): walk them, keep the
-            // ones present in this pair (a lone slot, the common case, reads nothing more)
-            uint32_t q = ghead[s];
-            if (!q) E = __popc(info[s] & 3u);
+            // ones present in this pair
+            uint32_t q = q0;
             while (q) {
                 const uint32_t s2 = q - 1;
                 q = gnext[s2];
@@ -479,12 +500,7 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
         within[s] = w;
         if (tmin == t) {
             etot[s] = E;
-            // one atomic per leader: its edge code lands in 2 free bits (first-insert times are
-            // unique, so the add is an OR) and its edges in the block count
-            if (E) {
-                const uint64_t code = E < 3u ? E : 3u;
-                atomicAdd(&bpack[t >> 4], ((unsigned long long)E << 32) | (code << (2u * (t & 15u))));
-            }
+            if (E) leader_mark(bpack, t, E);   // one atomic per leader
         }
     }
 }
@@ -563,18 +579,21 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     const uint32_t* cpos = S + d.o_cpos;
     uint32_t* order = S + d.o_order;
     uint32_t* hpos = S + d.o_hpos;
+    const uint32_t* ghead = group_heads(g, d);
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
-        if (tkey[s] == kInf) continue;
+        const uint32_t ts = tkey[s];
+        if (ts == kInf) continue;
         const uint32_t eb = info[s] & 3u;
         if (!eb) continue;
-        const uint32_t t = tb[s], blk = t >> 4, bit = t & 15u;
+        const bool lone = ghead && ghead[s] == 0u;   // its own bucket leader, nothing before it
+        const uint32_t t = lone ? ts : tb[s], blk = t >> 4, bit = t & 15u;
         const unsigned long long v = bpack[blk];
         // edge codes of the leaders later in this block (2 bits per time): 1 and 2 are their edge
         // counts; 3 (buckets of 3+ edges) is resolved from the leader's slot, found from its
         // (i, j) = (t / |B.E|, t % |B.E|)
         const uint64_t codes = (v & 0xFFFFFFFFull) >> (2u * bit + 2u);
         const uint64_t esc = codes & (codes >> 1) & 0x5555555555555555ull;
-        uint32_t hp = (uint32_t)(v >> 32) + within[s] + (uint32_t)__popcll(codes & 0x5555555555555555ull) +
+        uint32_t hp = (uint32_t)(v >> 32) + (lone ? 0u : within[s]) + (uint32_t)__popcll(codes & 0x5555555555555555ull) +
                       2u * (uint32_t)__popcll(codes & 0xAAAAAAAAAAAAAAAAull) - 3u * (uint32_t)__popcll(esc);
         uint64_t m = esc;
         while (m) {
