@@ -770,7 +770,8 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     int rc = ensure_pairs(c, A->n);
     if (rc) return rc;
     c->merge_host.clear();
-    plan->reserved[0] = ++c->plan_stamp;
+    // as in ct_mul_plan: earlier plans go stale now, this one is stamped only once it has succeeded
+    const uint32_t stamp = ++c->plan_stamp;
     hipError_t e = hipMemsetAsync(c->stats, 0, sizeof(plan_stats), c->stream);
     if (e == hipSuccess)
         e = launch_plan_add(*A, *B, *C, c->stats, c->pair_class, c->large_ids, c->prm.edge_budget, c->stream);
@@ -814,6 +815,7 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
         std::sort(c->merge_host.begin(), c->merge_host.end(),
                   [](const merge_pair_info& x, const merge_pair_info& y) { return x.pair < y.pair; });
     }
+    plan->reserved[0] = stamp;
     return PVAC_OK;
 }
 
