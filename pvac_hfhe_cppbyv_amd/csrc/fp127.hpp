@@ -341,4 +341,54 @@ __device__ __forceinline__ fp fp_fold3(uint64_t l0, uint64_t l1, uint64_t l2) {
     return fp_from_words(lo, hi);
 }
 
+// ---- column accumulators over 26-bit limbs ------------------------------------------------
+// Sum of many products a*b of canonical operands without a carry chain per product: a and b
+// split into five limbs of 26/26/26/26/23 bits (< 2^26), and column k of the running sum is a
+// u64 that takes a_i b_j (< 2^52) for every i + j = k, one v_mad_u64_u32 each (25 per product,
+// nothing else). A column takes at most 5 terms per product, so from a normalised start (< 2^26)
+// col26_norm must run within every 2^11 products (5 * 2^11 * 2^52 + 2^26 < 2^64). col26_fold
+// gives the canonical residue of the sum, the same value as the reference's fp_add chain of
+// canonical fp_mul results (field.hpp:50-56, 209-213: that chain computes the exact sum mod p).
+constexpr uint32_t kM26 = (1u << 26) - 1u;
+__device__ __forceinline__ void fp_split26(const fp& v, uint32_t* l) {   // v canonical (< 2^127)
+    l[0] = (uint32_t)v.lo & kM26;
+    l[1] = (uint32_t)(v.lo >> 26) & kM26;
+    l[2] = (uint32_t)((v.lo >> 52) | (v.hi << 12)) & kM26;
+    l[3] = (uint32_t)(v.hi >> 14) & kM26;
+    l[4] = (uint32_t)(v.hi >> 40);
+}
+__device__ __forceinline__ void col26_zero(uint64_t* c) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = 0;
+}
+// c += a * b (limb vectors): 25 v_mad_u64_u32
+__device__ __forceinline__ void col26_mac(uint64_t* c, const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) c[i + j] += (uint64_t)a[i] * b[j];
+}
+// carries up: columns 0..7 < 2^26 afterwards, the value unchanged
+__device__ __forceinline__ void col26_norm(uint64_t* c) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c[k + 1] += c[k] >> 26;
+        c[k] &= kM26;
+    }
+}
+// canonical residue of sum_k c_k 2^(26k) for normalised columns (c_8 < 2^64)
+__device__ __forceinline__ fp col26_fold(const uint64_t* c) {
+    typedef unsigned __int128 u128;
+    const u128 m127 = ((u128)1 << 127) - 1;
+    // 2^130 == 2^3, 2^156 == 2^29, 2^182 == 2^55, 2^208 == 2^81 (mod p); bits >= 127 of c_4 2^104
+    // and c_8 2^81 wrap to bit 0
+    const u128 x = (u128)c[0] + ((u128)c[1] << 26) + ((u128)c[2] << 52) + ((u128)c[3] << 78) +
+                   ((u128)(c[4] & ((1u << 23) - 1u)) << 104);                               // < 2^127
+    const u128 y = ((u128)c[5] << 3) + ((u128)c[6] << 29) + ((u128)c[7] << 55) +
+                   ((u128)(c[8] & ((1ull << 46) - 1ull)) << 81);                            // < 2^128
+    const u128 t = x + (y & m127);                                                          // < 2^128
+    const u128 f = (t & m127) + (t >> 127) + (y >> 127) + (c[4] >> 23) + (c[8] >> 46);      // < 2^127 + 2^19
+    return fp_from_words((uint64_t)f, (uint64_t)(f >> 64));
+}
+
 }  // namespace pvhip

@@ -149,10 +149,17 @@ constexpr uint32_t kBmax = kLP * kLPRows;
 constexpr uint32_t kChunk = 384;         // sparse-side edges staged per round
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
+#ifdef PVAC_PROD_FOLD1   // A/B builds only: the round-1 dense loop (fp_mul_fold1 + 128-bit sums)
 // dense mode: dw[2B] (16 B) | di[2B] | sw[kChunk] (16 B) | sinf[kChunk] | sid[kChunk] | dup
+constexpr uint32_t kDenseFixed = 40u, kDenseChunk = 24u;
+#else
+// dense mode: dl4[2][B] (limbs 0-3, 16 B) | dl1[2][B] (limb 4) | di[2][B] | sl4[kChunk] (16 B) |
+//             sl1[kChunk] | sinf[kChunk] | sid[kChunk] | dup; [ch][idx] so lanes r read adjacent words
+constexpr uint32_t kDenseFixed = 48u, kDenseChunk = 28u;
+#endif
 // scatter   : acc[2B x 3] (u64) | tk[B]
 __host__ __device__ inline uint32_t prod_lds_bytes(uint32_t Bm) {
-    const uint32_t dense = al16(40u * Bm) + 24u * kChunk + 16u;
+    const uint32_t dense = al16(kDenseFixed * Bm) + kDenseChunk * kChunk + 16u;
     const uint32_t scat = 48u * Bm + 4u * Bm;
     return dense > scat ? dense : scat;
 }
@@ -189,6 +196,112 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
     bool any = false;
 
     bool dense = nd >= kLargeDenseMin;
+#ifndef PVAC_PROD_FOLD1
+    if (dense) {
+        // Dense-owner mode with column accumulators (fp127.hpp col26_*): both sides are staged as
+        // 26-bit limbs, each probe is 25 v_mad_u64_u32 into the lane's P or M columns and a
+        // saturating add + min for the first-insert time. Empty dense slots hold zero limbs and
+        // time kInf, so the loop has no branch: a miss adds 0 and leaves the time alone.
+        uint4* dl4 = (uint4*)plds;
+        uint32_t* dl1 = (uint32_t*)(plds + 32u * Bm);
+        uint32_t* di = dl1 + 2u * Bm;
+        uint4* sl4 = (uint4*)(plds + al16(kDenseFixed * Bm));
+        uint32_t* sl1 = (uint32_t*)(sl4 + kChunk);
+        uint32_t* sinf = sl1 + kChunk;
+        uint32_t* sidv = sinf + kChunk;
+        uint32_t* dup = sidv + kChunk;
+        for (uint32_t k = tid; k < 2 * Bm; k += kLP) {
+            di[k] = kInf;
+            dl4[k] = make_uint4(0, 0, 0, 0);
+            dl1[k] = 0;
+        }
+        if (tid == 0) *dup = 0;
+        __syncthreads();
+        const uint32_t* dids = denseA ? idsA : idsB;
+        const pvac_ct_batch& D = denseA ? g.A : g.B;
+        const uint64_t deo = denseA ? aeo : beo;
+        for (uint32_t k = tid; k < nd; k += kLP) {
+            const uint32_t e = dids[k];
+            const uint64_t m = D.meta[deo + e];
+            const uint32_t sl = meta_ch(m) * Bm + meta_idx(m);
+            // di holds the dense side's share of the first-insert time t = i |B.E| + j
+            if (atomicCAS(&di[sl], kInf, denseA ? e * nB : e) != kInf) {
+                *dup = 1;
+            } else {   // canonical operands: the limb split needs a, b < 2^127
+                uint32_t l[5];
+                fp_split26(fp_canon(D.w_lo[deo + e], D.w_hi[deo + e]), l);
+                dl4[sl] = make_uint4(l[0], l[1], l[2], l[3]);
+                dl1[sl] = l[4];
+            }
+        }
+        __syncthreads();
+        dense = *dup == 0;   // duplicate (layer, idx, ch) edges: use the scatter mode instead
+        if (dense) {
+            const uint32_t* sids = denseA ? idsB : idsA;
+            const pvac_ct_batch& Sp = denseA ? g.B : g.A;
+            const uint64_t seo = denseA ? beo : aeo;
+            const uint32_t rows = (Bm + kLP - 1) / kLP;   // workgroup-uniform (1 for B <= 384)
+            for (uint32_t u = 0; u < rows; ++u) {
+                const uint32_t r = tid + u * kLP;
+                const bool live = r < Bm;
+                uint64_t P[9], M[9];
+                col26_zero(P);
+                col26_zero(M);
+                uint32_t tmin = kInf;
+                for (uint32_t c0 = 0; c0 < ns; c0 += kChunk) {
+                    const uint32_t cn = min(kChunk, ns - c0);
+                    __syncthreads();
+                    for (uint32_t k = tid; k < cn; k += kLP) {
+                        const uint32_t e = sids[c0 + k];
+                        const uint64_t m = Sp.meta[seo + e];
+                        uint32_t l[5];
+                        fp_split26(fp_canon(Sp.w_lo[seo + e], Sp.w_hi[seo + e]), l);
+                        sl4[k] = make_uint4(l[0], l[1], l[2], l[3]);
+                        sl1[k] = l[4];
+                        sinf[k] = meta_idx(m) | (meta_ch(m) << 16);
+                        sidv[k] = denseA ? e : e * nB;   // the sparse side's share of t
+                    }
+                    __syncthreads();
+                    if (live) {
+                        for (uint32_t q = 0; q < cn; ++q) {
+                            const uint32_t si = sinf[q];
+                            const uint32_t sidx = si & 0xFFFFu, sch = si >> 16;
+                            const uint32_t dd = r >= sidx ? r - sidx : r + Bm - sidx;
+                            const uint4 b4 = sl4[q];
+                            const uint32_t b[5] = {b4.x, b4.y, b4.z, b4.w, sl1[q]};
+                            const uint32_t se = sidv[q];
+                            // dense channel sch meets sparse channel sch in P, the other one in M
+                            const uint32_t sp = sch * Bm + dd, sm = (sch ^ 1u) * Bm + dd;
+                            const uint4 p4 = dl4[sp], m4 = dl4[sm];
+                            const uint32_t ap[5] = {p4.x, p4.y, p4.z, p4.w, dl1[sp]};
+                            const uint32_t am[5] = {m4.x, m4.y, m4.z, m4.w, dl1[sm]};
+                            col26_mac(P, ap, b);
+                            col26_mac(M, am, b);
+                            tmin = min(tmin, min(__builtin_elementwise_add_sat(di[sp], se),
+                                                 __builtin_elementwise_add_sat(di[sm], se)));
+                        }
+                        col26_norm(P);
+                        col26_norm(M);
+                    }
+                }
+                if (live) {
+                    const uint64_t s = slot0 + r;
+                    tkey[s] = tmin;
+                    if (tmin != kInf) {
+                        const fp ps = col26_fold(P), ms = col26_fold(M);
+                        const uint32_t eb = (fp_nonzero(ps) ? 1u : 0u) | (fp_nonzero(ms) ? 2u : 0u);
+                        info[s] = eb;
+                        sums[2 * s] = make_ulonglong2(ps.lo, ps.hi);
+                        sums[2 * s + 1] = make_ulonglong2(ms.lo, ms.hi);
+                        any |= eb != 0;
+                        if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tmin, __popc(eb));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+#else
     if (dense) {
         ulonglong2* dw = (ulonglong2*)plds;
         uint32_t* di = (uint32_t*)(plds + 32u * Bm);
@@ -287,6 +400,7 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         }
         __syncthreads();
     }
+#endif
     if (!dense) {
         unsigned long long* acc = (unsigned long long*)plds;
         uint32_t* tk = (uint32_t*)(plds + 48u * Bm);
