@@ -758,13 +758,16 @@ def chain_bench(eng, args):
     out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
                                  "step, on the device (untimed)", "pair_steps": gp, "failed": gf,
                         "invariant_ok": gf == 0 and gp == n * depth, "check_seconds": check_s}
-    # ALU roofline: lazy products per second against the fp_mul_fold1 ceiling measured on this GPU
-    # (register-resident probe, k_ubench.hip); per product the general path also adds the sum
+    # ALU roofline: products per second against the column-accumulated product ceiling measured on
+    # this GPU (register-resident col26_mac probe, k_ubench.hip: the dense loop's own multiply, 25
+    # v_mad_u64_u32 per product); the fp_mul_fold1 ceiling of round 1 is reported beside it
     try:
-        ceil = eng.alu_ceiling(1)
-        out["roofline"] = {"bound": "valu", "achieved": products / chain_s, "peak": ceil, "unit": "fp_mul_fold1/s",
+        ceil = eng.alu_ceiling(3)
+        out["roofline"] = {"bound": "valu", "achieved": products / chain_s, "peak": ceil, "unit": "products/s",
                            "frac": products / chain_s / ceil,
-                           "peak_source": "pvac_hip_alu_ceiling(1): register-resident fp_mul_fold1, 8 waves/SIMD"}
+                           "peak_source": "pvac_hip_alu_ceiling(3): register-resident col26_mac (two column "
+                                          "accumulators per lane), 8 waves/SIMD",
+                           "fold1_ceiling": eng.alu_ceiling(1)}
     except Exception as ex:
         out["roofline"] = {"error": repr(ex)}
     if errors:

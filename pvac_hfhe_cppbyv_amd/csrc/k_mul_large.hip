@@ -146,16 +146,22 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
 constexpr int kLP = 384;                 // products workgroup: one lane per output index r (B = 337)
 constexpr int kLPRows = 3;               // B <= kLP * kLPRows
 constexpr uint32_t kBmax = kLP * kLPRows;
+#ifdef PVAC_PROD_FOLD1
 constexpr uint32_t kChunk = 384;         // sparse-side edges staged per round
+#else
+constexpr uint32_t kChunk = 128;         // sparse-side edges staged per round (chain steps: ~20)
+#endif
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
 #ifdef PVAC_PROD_FOLD1   // A/B builds only: the round-1 dense loop (fp_mul_fold1 + 128-bit sums)
 // dense mode: dw[2B] (16 B) | di[2B] | sw[kChunk] (16 B) | sinf[kChunk] | sid[kChunk] | dup
 constexpr uint32_t kDenseFixed = 40u, kDenseChunk = 24u;
 #else
-// dense mode: dl4[2][B] (limbs 0-3, 16 B) | dl1[2][B] (limb 4) | di[2][B] | sl4[kChunk] (16 B) |
-//             sl1[kChunk] | sinf[kChunk] | sid[kChunk] | dup; [ch][idx] so lanes r read adjacent words
-constexpr uint32_t kDenseFixed = 48u, kDenseChunk = 28u;
+// dense mode: dl4[2][2B] (limbs 0-3, 16 B) | dx[2][2B] (limb 4, first-insert share) | sl4[kChunk]
+//             (16 B) | sl1[kChunk] | sinf[kChunk] | sid[kChunk] | dup. Per channel the B dense slots
+//             are stored twice (x and x + B), so lane r finds slot (r - sidx) mod B at r + B - sidx:
+//             no wrap test, and the sparse edge's part of the address is wave-uniform (SALU)
+constexpr uint32_t kDenseFixed = 96u, kDenseChunk = 28u;
 #endif
 // scatter   : acc[2B x 3] (u64) | tk[B]
 __host__ __device__ inline uint32_t prod_lds_bytes(uint32_t Bm) {
@@ -203,17 +209,15 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         // saturating add + min for the first-insert time. Empty dense slots hold zero limbs and
         // time kInf, so the loop has no branch: a miss adds 0 and leaves the time alone.
         uint4* dl4 = (uint4*)plds;
-        uint32_t* dl1 = (uint32_t*)(plds + 32u * Bm);
-        uint32_t* di = dl1 + 2u * Bm;
+        uint2* dx = (uint2*)(plds + 64u * Bm);
         uint4* sl4 = (uint4*)(plds + al16(kDenseFixed * Bm));
         uint32_t* sl1 = (uint32_t*)(sl4 + kChunk);
         uint32_t* sinf = sl1 + kChunk;
         uint32_t* sidv = sinf + kChunk;
         uint32_t* dup = sidv + kChunk;
-        for (uint32_t k = tid; k < 2 * Bm; k += kLP) {
-            di[k] = kInf;
+        for (uint32_t k = tid; k < 4 * Bm; k += kLP) {
             dl4[k] = make_uint4(0, 0, 0, 0);
-            dl1[k] = 0;
+            dx[k] = make_uint2(0, kInf);
         }
         if (tid == 0) *dup = 0;
         __syncthreads();
@@ -223,15 +227,17 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         for (uint32_t k = tid; k < nd; k += kLP) {
             const uint32_t e = dids[k];
             const uint64_t m = D.meta[deo + e];
-            const uint32_t sl = meta_ch(m) * Bm + meta_idx(m);
-            // di holds the dense side's share of the first-insert time t = i |B.E| + j
-            if (atomicCAS(&di[sl], kInf, denseA ? e * nB : e) != kInf) {
+            const uint32_t sl = meta_ch(m) * 2u * Bm + meta_idx(m);
+            // dx.y holds the dense side's share of the first-insert time t = i |B.E| + j
+            const uint32_t te = denseA ? e * nB : e;
+            if (atomicCAS(&dx[sl].y, kInf, te) != kInf) {
                 *dup = 1;
             } else {   // canonical operands: the limb split needs a, b < 2^127
                 uint32_t l[5];
                 fp_split26(fp_canon(D.w_lo[deo + e], D.w_hi[deo + e]), l);
-                dl4[sl] = make_uint4(l[0], l[1], l[2], l[3]);
-                dl1[sl] = l[4];
+                dl4[sl] = dl4[sl + Bm] = make_uint4(l[0], l[1], l[2], l[3]);
+                dx[sl].x = l[4];
+                dx[sl + Bm] = make_uint2(l[4], te);
             }
         }
         __syncthreads();
@@ -244,6 +250,8 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
             for (uint32_t u = 0; u < rows; ++u) {
                 const uint32_t r = tid + u * kLP;
                 const bool live = r < Bm;
+                const uint4* dl4r = dl4 + (live ? r : 0u);
+                const uint2* dxr = dx + (live ? r : 0u);
                 uint64_t P[9], M[9];
                 col26_zero(P);
                 col26_zero(M);
@@ -258,27 +266,28 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                         fp_split26(fp_canon(Sp.w_lo[seo + e], Sp.w_hi[seo + e]), l);
                         sl4[k] = make_uint4(l[0], l[1], l[2], l[3]);
                         sl1[k] = l[4];
-                        sinf[k] = meta_idx(m) | (meta_ch(m) << 16);
+                        // wave-uniform offsets of the P and M slots relative to lane r: the dense
+                        // channel equal to the sparse one gives P, the other M
+                        const uint32_t sidx = meta_idx(m), sch = meta_ch(m);
+                        sinf[k] = (sch * 2u * Bm + Bm - sidx) | (((sch ^ 1u) * 2u * Bm + Bm - sidx) << 16);
                         sidv[k] = denseA ? e : e * nB;   // the sparse side's share of t
                     }
                     __syncthreads();
                     if (live) {
                         for (uint32_t q = 0; q < cn; ++q) {
-                            const uint32_t si = sinf[q];
-                            const uint32_t sidx = si & 0xFFFFu, sch = si >> 16;
-                            const uint32_t dd = r >= sidx ? r - sidx : r + Bm - sidx;
+                            const uint32_t so = __builtin_amdgcn_readfirstlane(sinf[q]);
+                            const uint32_t oP = so & 0xFFFFu, oM = so >> 16;
                             const uint4 b4 = sl4[q];
                             const uint32_t b[5] = {b4.x, b4.y, b4.z, b4.w, sl1[q]};
                             const uint32_t se = sidv[q];
-                            // dense channel sch meets sparse channel sch in P, the other one in M
-                            const uint32_t sp = sch * Bm + dd, sm = (sch ^ 1u) * Bm + dd;
-                            const uint4 p4 = dl4[sp], m4 = dl4[sm];
-                            const uint32_t ap[5] = {p4.x, p4.y, p4.z, p4.w, dl1[sp]};
-                            const uint32_t am[5] = {m4.x, m4.y, m4.z, m4.w, dl1[sm]};
+                            const uint4 p4 = dl4r[oP], m4 = dl4r[oM];
+                            const uint2 px = dxr[oP], mx = dxr[oM];
+                            const uint32_t ap[5] = {p4.x, p4.y, p4.z, p4.w, px.x};
+                            const uint32_t am[5] = {m4.x, m4.y, m4.z, m4.w, mx.x};
                             col26_mac(P, ap, b);
                             col26_mac(M, am, b);
-                            tmin = min(tmin, min(__builtin_elementwise_add_sat(di[sp], se),
-                                                 __builtin_elementwise_add_sat(di[sm], se)));
+                            tmin = min(tmin, min(__builtin_elementwise_add_sat(px.y, se),
+                                                 __builtin_elementwise_add_sat(mx.y, se)));
                         }
                         col26_norm(P);
                         col26_norm(M);

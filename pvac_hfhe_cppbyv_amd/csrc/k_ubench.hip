@@ -9,6 +9,8 @@
 //   kind 1: lazy products fp_mul_fold1 (the general path's per-product multiply) per second,
 //           register resident, 4 independent chains per lane
 //   kind 2: full fp_mul (two folds + canonical form) per second, as kind 1
+//   kind 3: column-accumulated products (col26_mac: 25 v_mad_u64_u32 into nine u64 columns, the
+//           general path's dense loop since round 2) per second, two accumulators per lane
 // Grids fill every CU at 8 waves per SIMD. Used by measurement only, never by the ct_* ops.
 #include "common.hpp"
 
@@ -88,6 +90,31 @@ __global__ __launch_bounds__(kUB) void k_probe_mul(uint64_t* out, uint32_t iters
     out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
 }
 
+// two column accumulators (P and M of the products kernel) fed from limb vectors that change every
+// iteration (one VALU op each), so nothing is loop-invariant
+__global__ __launch_bounds__(kUB) void k_probe_col26(uint64_t* out, uint32_t iters, uint32_t seed) {
+    const uint32_t s = (threadIdx.x ^ seed) * 2654435761u + blockIdx.x;
+    uint32_t a[5], b[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        a[k] = (s >> k) & kM26;
+        b[k] = (s * (k + 7)) & kM26;
+    }
+    uint64_t P[9], M[9];
+    col26_zero(P);
+    col26_zero(M);
+    for (uint32_t i = 0; i < iters; ++i) {
+        col26_mac(P, a, b);
+        col26_mac(M, b, a);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[k]) : "v"(i));
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r ^= P[k] ^ M[k];
+    out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
+}
+
 }  // namespace
 
 // ops per second of probe `kind` (see above), timed with HIP events on `st` (synchronises)
@@ -110,6 +137,9 @@ hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s) {
         } else if (kind == 1) {
             hipLaunchKernelGGL(k_probe_mul<false>, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
             ops = (double)blocks * kUB * iters * 4.0;           // lane products
+        } else if (kind == 3) {
+            hipLaunchKernelGGL(k_probe_col26, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
+            ops = (double)blocks * kUB * iters * 2.0;           // lane products
         } else {
             hipLaunchKernelGGL(k_probe_mul<true>, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
             ops = (double)blocks * kUB * iters * 4.0;
