@@ -6,10 +6,12 @@
 // space is cut along its natural independence: every product of an A edge in layer la and a
 // B edge in layer lb lands in product layer lp = la*LB + lb, a cyclic convolution of length B
 // over Fp with +/- channels. One workgroup owns one (la, lb) TASK:
-//   dense-owner mode : the side with more edges becomes a dense [B][2] table in LDS; one lane
-//                      per output index r loops over the other side's edges, multiplies, and
-//                      accumulates P/M sums and the key's first-insert time in REGISTERS (no
-//                      atomics). For saturated chain layers (674 edges) every probe is useful.
+//   dense-owner mode : the side with more edges becomes a dense [2][B] table of 26-bit limbs in
+//                      LDS; one lane per output index r loops over the other side's edges and
+//                      accumulates P/M sums as nine u64 columns each (25 v_mad_u64_u32 per
+//                      product, no carry chain; fp127.hpp col26_*) and the key's first-insert time
+//                      in REGISTERS (no atomics). For saturated chain layers (674 edges) every
+//                      probe is useful.
 //   scatter mode     : sparse x sparse tasks (and inputs with duplicate (layer, idx, ch) edges)
 //                      accumulate 43/42/42-bit limbs with LDS atomics, as the fresh kernel.
 // Results go to a dense per-pair key-slot array [|A.L||B.L|][B] in global scratch.
@@ -146,23 +148,14 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
 constexpr int kLP = 384;                 // products workgroup: one lane per output index r (B = 337)
 constexpr int kLPRows = 3;               // B <= kLP * kLPRows
 constexpr uint32_t kBmax = kLP * kLPRows;
-#ifdef PVAC_PROD_FOLD1
-constexpr uint32_t kChunk = 384;         // sparse-side edges staged per round
-#else
 constexpr uint32_t kChunk = 128;         // sparse-side edges staged per round (chain steps: ~20)
-#endif
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
-#ifdef PVAC_PROD_FOLD1   // A/B builds only: the round-1 dense loop (fp_mul_fold1 + 128-bit sums)
-// dense mode: dw[2B] (16 B) | di[2B] | sw[kChunk] (16 B) | sinf[kChunk] | sid[kChunk] | dup
-constexpr uint32_t kDenseFixed = 40u, kDenseChunk = 24u;
-#else
 // dense mode: dl4[2][2B] (limbs 0-3, 16 B) | dx[2][2B] (limb 4, first-insert share) | sl4[kChunk]
 //             (16 B) | sl1[kChunk] | sinf[kChunk] | sid[kChunk] | dup. Per channel the B dense slots
 //             are stored twice (x and x + B), so lane r finds slot (r - sidx) mod B at r + B - sidx:
 //             no wrap test, and the sparse edge's part of the address is wave-uniform (SALU)
 constexpr uint32_t kDenseFixed = 96u, kDenseChunk = 28u;
-#endif
 // scatter   : acc[2B x 3] (u64) | tk[B]
 __host__ __device__ inline uint32_t prod_lds_bytes(uint32_t Bm) {
     const uint32_t dense = al16(kDenseFixed * Bm) + kDenseChunk * kChunk + 16u;
@@ -202,7 +195,6 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
     bool any = false;
 
     bool dense = nd >= kLargeDenseMin;
-#ifndef PVAC_PROD_FOLD1
     if (dense) {
         // Dense-owner mode with column accumulators (fp127.hpp col26_*): both sides are staged as
         // 26-bit limbs, each probe is 25 v_mad_u64_u32 into the lane's P or M columns and a
@@ -310,106 +302,6 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         }
         __syncthreads();
     }
-#else
-    if (dense) {
-        ulonglong2* dw = (ulonglong2*)plds;
-        uint32_t* di = (uint32_t*)(plds + 32u * Bm);
-        ulonglong2* swv = (ulonglong2*)(plds + al16(40u * Bm));
-        uint32_t* sinf = (uint32_t*)(swv + kChunk);
-        uint32_t* sidv = sinf + kChunk;
-        uint32_t* dup = sidv + kChunk;
-        for (uint32_t k = tid; k < 2 * Bm; k += kLP) di[k] = kInf;
-        if (tid == 0) *dup = 0;
-        __syncthreads();
-        const uint32_t* dids = denseA ? idsA : idsB;
-        const pvac_ct_batch& D = denseA ? g.A : g.B;
-        const uint64_t deo = denseA ? aeo : beo;
-        for (uint32_t k = tid; k < nd; k += kLP) {
-            const uint32_t e = dids[k];
-            const uint64_t m = D.meta[deo + e];
-            const uint32_t sl = meta_idx(m) * 2 + meta_ch(m);
-            // di holds the dense side's share of the first-insert time t = i |B.E| + j
-            if (atomicCAS(&di[sl], kInf, denseA ? e * nB : e) != kInf) {
-                *dup = 1;
-            } else {   // canonical operands: the lazy product below needs a, b < 2^127
-                const fp w = fp_canon(D.w_lo[deo + e], D.w_hi[deo + e]);
-                dw[sl] = make_ulonglong2(w.lo, w.hi);
-            }
-        }
-        __syncthreads();
-        dense = *dup == 0;   // duplicate (layer, idx, ch) edges: use the scatter mode instead
-        if (dense) {
-            const uint32_t* sids = denseA ? idsB : idsA;
-            const pvac_ct_batch& Sp = denseA ? g.B : g.A;
-            const uint64_t seo = denseA ? beo : aeo;
-            // lanes own output indices r (at most kLPRows per lane); P/M sums are lazy 128-bit
-            // register accumulators (acc128c), reduced once at the end
-            acc128c P[kLPRows], M[kLPRows];
-            uint32_t tmin[kLPRows];
-#pragma unroll
-            for (int u = 0; u < kLPRows; ++u) { acc_zero(P[u]); acc_zero(M[u]); tmin[u] = kInf; }
-            for (uint32_t c0 = 0; c0 < ns; c0 += kChunk) {
-                const uint32_t cn = min(kChunk, ns - c0);
-                __syncthreads();
-                for (uint32_t k = tid; k < cn; k += kLP) {
-                    const uint32_t e = sids[c0 + k];
-                    const uint64_t m = Sp.meta[seo + e];
-                    const fp w = fp_canon(Sp.w_lo[seo + e], Sp.w_hi[seo + e]);
-                    swv[k] = make_ulonglong2(w.lo, w.hi);
-                    sinf[k] = meta_idx(m) | (meta_ch(m) << 16);
-                    sidv[k] = denseA ? e : e * nB;   // the sparse side's share of t
-                }
-                __syncthreads();
-#pragma unroll
-                for (int u = 0; u < kLPRows; ++u) {
-                    const uint32_t r = tid + u * kLP;
-                    if (r >= Bm) break;
-                    for (uint32_t q = 0; q < cn; ++q) {
-                        const uint32_t si = sinf[q];
-                        const uint32_t sidx = si & 0xFFFFu, sch = si >> 16;
-                        const uint32_t dd = r >= sidx ? r - sidx : r + Bm - sidx;
-                        const ulonglong2 sw = swv[q];
-                        const uint32_t se = sidv[q];
-                        // the dense slot of channel sch meets sparse channel sch (P), the other one
-                        // gives M: reading the slots in that order keeps each sum in fixed registers
-                        // (a select between the P and M accumulators made the compiler copy one of
-                        // them back, 5 moves per product)
-                        auto probe = [&](uint32_t slot, acc128c& acc) {
-                            const uint32_t e = di[slot];
-                            if (e != kInf) {
-                                const ulonglong2 dv = dw[slot];
-                                uint64_t x0, x1;
-                                fp_mul_fold1(fp{dv.x, dv.y}, fp{sw.x, sw.y}, x0, x1);
-                                acc_add(acc, x0, x1);
-                                const uint32_t t = e + se;
-                                tmin[u] = t < tmin[u] ? t : tmin[u];
-                            }
-                        };
-                        probe(2 * dd + sch, P[u]);
-                        probe(2 * dd + (sch ^ 1u), M[u]);
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kLPRows; ++u) {
-                const uint32_t r = tid + u * kLP;
-                if (r >= Bm) break;
-                const uint64_t s = slot0 + r;
-                tkey[s] = tmin[u];
-                if (tmin[u] != kInf) {
-                    const fp ps = acc_fold(P[u]), ms = acc_fold(M[u]);
-                    const uint32_t eb = (fp_nonzero(ps) ? 1u : 0u) | (fp_nonzero(ms) ? 2u : 0u);
-                    info[s] = eb;
-                    sums[2 * s] = make_ulonglong2(ps.lo, ps.hi);
-                    sums[2 * s + 1] = make_ulonglong2(ms.lo, ms.hi);
-                    any |= eb != 0;
-                    if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tmin[u], __popc(eb));
-                }
-            }
-        }
-        __syncthreads();
-    }
-#endif
     if (!dense) {
         unsigned long long* acc = (unsigned long long*)plds;
         uint32_t* tk = (uint32_t*)(plds + 48u * Bm);
