@@ -171,6 +171,43 @@ def test_large_dense_chain_like_vs_oracle(oracle):
     assert plan.n_large == len(xs)
 
 
+def test_large_column_bounds_vs_oracle(oracle):
+    """Column accumulators of the dense loop (fp127.hpp col26_*) at their limits: both sides
+    saturated (every (idx, ch) cell of a layer, so the sparse side is 674 edges = 6 chunks of 128),
+    weights at and near the top of the canonical range (p - 1 = all 26-bit limbs full, values that
+    canonicalise to it, 2^127 - 2^k) mixed with random full-range words; squares and a 2-layer x
+    1-layer shape, vs the oracle bit-exact."""
+    rng = np.random.default_rng(0xC0126)
+    B = 337
+    p = (1 << 127) - 1
+    top = [p - 1, p - 2, (1 << 127) - (1 << 26) - 1, (1 << 126), p + (p - 1), (1 << 128) - 2]
+
+    def sat(nl, top_frac):
+        n = nl * 2 * B
+        pick = rng.permutation(n).astype(np.uint64)   # every (layer, idx, ch) once, shuffled
+        lay, rest = pick // np.uint64(2 * B), pick % np.uint64(2 * B)
+        meta = lay | ((rest >> np.uint64(1)) << np.uint64(32)) | ((rest & np.uint64(1)) << np.uint64(48))
+        lo = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+        hi = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+        sel = rng.random(n) < top_frac
+        for k in np.nonzero(sel)[0]:
+            v = top[int(rng.integers(0, len(top)))]
+            lo[k], hi[k] = v & (2**64 - 1), v >> 64
+        L = np.zeros(nl, LAYER_DT)
+        L["ztag"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+        L["nonce_lo"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+        return Cipher(L, meta, lo, hi)
+
+    xs, ys = [], []
+    for k in range(6):
+        x = sat(1 + k % 2, 1.0 if k < 2 else 0.5)
+        y = x if k % 3 == 0 else sat(1, 1.0 if k < 2 else 0.5)
+        xs.append(x)
+        ys.append(y)
+    plan = _check_vs_oracle(oracle, {"canon_tag": 0xC0}, xs, ys, 0xC1)
+    assert plan.n_large == len(xs)
+
+
 def test_large_scatter_and_duplicates_vs_oracle(oracle):
     """Scatter mode (sparse x sparse tasks) and duplicate (layer, idx, ch) edges in the dense side,
     empty layers, empty ciphers, single edges."""
