@@ -207,6 +207,19 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         uint32_t* sinf = sl1 + kChunk;
         uint32_t* sidv = sinf + kChunk;
         uint32_t* dup = sidv + kChunk;
+        const uint32_t* sids = denseA ? idsB : idsA;
+        const pvac_ct_batch& Sp = denseA ? g.B : g.A;
+        const uint64_t seo = denseA ? beo : aeo;
+        // the first sparse chunk's loads go out before the dense staging, so the two sides' global
+        // round trips overlap (thread k < kChunk < kLP stages sparse edge k)
+        uint32_t pe = 0;
+        uint64_t pmeta = 0, plo = 0, phi = 0;
+        if (tid < min(ns, kChunk)) {
+            pe = sids[tid];
+            pmeta = Sp.meta[seo + pe];
+            plo = Sp.w_lo[seo + pe];
+            phi = Sp.w_hi[seo + pe];
+        }
         for (uint32_t k = tid; k < 4 * Bm; k += kLP) {
             dl4[k] = make_uint4(0, 0, 0, 0);
             dx[k] = make_uint2(0, kInf);
@@ -216,28 +229,37 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         const uint32_t* dids = denseA ? idsA : idsB;
         const pvac_ct_batch& D = denseA ? g.A : g.B;
         const uint64_t deo = denseA ? aeo : beo;
-        for (uint32_t k = tid; k < nd; k += kLP) {
-            const uint32_t e = dids[k];
-            const uint64_t m = D.meta[deo + e];
-            const uint32_t sl = meta_ch(m) * 2u * Bm + meta_idx(m);
-            // dx.y holds the dense side's share of the first-insert time t = i |B.E| + j
-            const uint32_t te = denseA ? e * nB : e;
-            if (atomicCAS(&dx[sl].y, kInf, te) != kInf) {
-                *dup = 1;
-            } else {   // canonical operands: the limb split needs a, b < 2^127
-                uint32_t l[5];
-                fp_split26(fp_canon(D.w_lo[deo + e], D.w_hi[deo + e]), l);
-                dl4[sl] = dl4[sl + Bm] = make_uint4(l[0], l[1], l[2], l[3]);
-                dx[sl].x = l[4];
-                dx[sl + Bm] = make_uint2(l[4], te);
+        for (uint32_t k0 = tid; k0 < nd; k0 += 2u * kLP) {   // two edges per round, loads first
+            uint32_t e[2];
+            uint64_t m[2], wl[2], wh[2];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const uint32_t k = k0 + (uint32_t)v * kLP;
+                e[v] = k < nd ? dids[k] : 0u;
+                m[v] = k < nd ? D.meta[deo + e[v]] : 0ull;
+                wl[v] = k < nd ? D.w_lo[deo + e[v]] : 0ull;
+                wh[v] = k < nd ? D.w_hi[deo + e[v]] : 0ull;
+            }
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                if (k0 + (uint32_t)v * kLP >= nd) break;
+                const uint32_t sl = meta_ch(m[v]) * 2u * Bm + meta_idx(m[v]);
+                // dx.y holds the dense side's share of the first-insert time t = i |B.E| + j
+                const uint32_t te = denseA ? e[v] * nB : e[v];
+                if (atomicCAS(&dx[sl].y, kInf, te) != kInf) {
+                    *dup = 1;
+                } else {   // canonical operands: the limb split needs a, b < 2^127
+                    uint32_t l[5];
+                    fp_split26(fp_canon(wl[v], wh[v]), l);
+                    dl4[sl] = dl4[sl + Bm] = make_uint4(l[0], l[1], l[2], l[3]);
+                    dx[sl].x = l[4];
+                    dx[sl + Bm] = make_uint2(l[4], te);
+                }
             }
         }
         __syncthreads();
         dense = *dup == 0;   // duplicate (layer, idx, ch) edges: use the scatter mode instead
         if (dense) {
-            const uint32_t* sids = denseA ? idsB : idsA;
-            const pvac_ct_batch& Sp = denseA ? g.B : g.A;
-            const uint64_t seo = denseA ? beo : aeo;
             const uint32_t rows = (Bm + kLP - 1) / kLP;   // workgroup-uniform (1 for B <= 384)
             for (uint32_t u = 0; u < rows; ++u) {
                 const uint32_t r = tid + u * kLP;
@@ -251,11 +273,13 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                 for (uint32_t c0 = 0; c0 < ns; c0 += kChunk) {
                     const uint32_t cn = min(kChunk, ns - c0);
                     __syncthreads();
-                    for (uint32_t k = tid; k < cn; k += kLP) {
-                        const uint32_t e = sids[c0 + k];
-                        const uint64_t m = Sp.meta[seo + e];
+                    if ((uint32_t)tid < cn) {
+                        const uint32_t k = (uint32_t)tid;
+                        const bool first = u == 0 && c0 == 0;   // prefetched above
+                        const uint32_t e = first ? pe : sids[c0 + k];
+                        const uint64_t m = first ? pmeta : Sp.meta[seo + e];
                         uint32_t l[5];
-                        fp_split26(fp_canon(Sp.w_lo[seo + e], Sp.w_hi[seo + e]), l);
+                        fp_split26(fp_canon(first ? plo : Sp.w_lo[seo + e], first ? phi : Sp.w_hi[seo + e]), l);
                         sl4[k] = make_uint4(l[0], l[1], l[2], l[3]);
                         sl1[k] = l[4];
                         // wave-uniform offsets of the P and M slots relative to lane r: the dense
