@@ -66,7 +66,10 @@ def main():
     # ranks sharing the visible GPUs (local rank modulo the device count)
     backend = os.environ.get("PVAC_BENCH_BACKEND", "nccl")
     gpu = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    # PVAC_BENCH_DIST=1 runs the distributed flow (process group, gathers, self-checks) at world 1
+    # too: under torch.distributed.run with one rank it puts the collectives on RCCL on a 1-GPU box
+    dist_on = world > 1 or os.environ.get("PVAC_BENCH_DIST") == "1"
+    if dist_on:
         torch.cuda.set_device(gpu)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -115,19 +118,19 @@ def main():
         out = plan = None   # release the previous output first: its cached block is reused
         out, plan = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     eng.timing_reset()
     eng.timing(True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = plan = None   # (at 2^21 pairs two outputs do not fit in HBM together)
         out, plan = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.timing(False)
@@ -230,6 +233,7 @@ def main():
                                       "note": "no PMC summary for this kernel / batch in profiles/"}
 
     result["checks"] = self_checks(eng, args, A, B, out, nonces, n, first, seed, world, rank)
+    result["checks"]["collective_backend"] = dist.get_backend() if dist_on else None
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(eng, A, B, out, n, args)
     # the cfg-3 batch (~35 GB of inputs, outputs and nonces) is done with: release it so the side
@@ -245,7 +249,7 @@ def main():
             result["extras"] = {"error": repr(ex)}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -35,10 +35,11 @@ def exclusive_offsets(counts):
 
 def global_edge_offsets(local_total: int, device=None):
     """All ranks' output-edge totals (one all_gather of 8 bytes per rank) -> (this rank's offset in
-    the global edge CSR, grand total, per-rank totals). Single process: (0, local_total, [local])."""
+    the global edge CSR, grand total, per-rank totals). No process group: (0, local_total, [local]).
+    A one-rank group still issues the collective (bench.py PVAC_BENCH_DIST=1: RCCL on one GPU)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return 0, int(local_total), [int(local_total)]
     world, rank = dist.get_world_size(), dist.get_rank()
     if dist.get_backend() == "gloo":
@@ -55,7 +56,7 @@ def max_over_ranks(value: float, device=None) -> float:
     """Timing reduction of the driver contract (max over ranks)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     if dist.get_backend() == "gloo":
         device = "cpu"
@@ -87,12 +88,12 @@ def combine_digests(ds) -> int:
 
 def all_gather_u64(values, device=None):
     """all_gather of an equal-length u64 vector from every rank -> list (per rank) of numpy u64.
-    Single process: [values]."""
+    No process group: [values]."""
     import numpy as np
     import torch
     import torch.distributed as dist
     v = np.ascontiguousarray(values, dtype=np.uint64)
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [v.copy()]
     world = dist.get_world_size()
     if dist.get_backend() == "gloo":

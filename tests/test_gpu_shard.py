@@ -28,14 +28,16 @@ def test_two_shards_equal_one_batch():
     assert l0 + l1 == l_all
 
 
-def _bench_json(args, world, port=None):
+def _bench_json(args, world, port=None, backend="gloo", launcher=False):
     import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, PVAC_BENCH_BACKEND="gloo")
-    if world == 1:
+    env = dict(os.environ, PVAC_BENCH_BACKEND=backend)
+    if launcher:   # torch.distributed.run even for one rank: the process group and its collectives run
+        env["PVAC_BENCH_DIST"] = "1"
+    if world == 1 and not launcher:
         cmd = [sys.executable, os.path.join(root, "bench.py")] + args
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
@@ -60,3 +62,21 @@ def test_bench_world2_shard_digests_equal_one_gpu():
     assert c1["shard_digests_ok"] and c1["gsum_invariant"]["pairs"] == 8192
     assert c2["global_digest"] == c1["global_digest"]
     assert c2["global_output_edges"] == c1["global_output_edges"]
+
+
+def test_bench_rccl_one_rank_collectives():
+    """bench.py's distributed flow over RCCL ("nccl" backend on ROCm) with one rank on cuda:0
+    (torch.distributed.run, PVAC_BENCH_DIST=1): the process group, the device-tensor all_gathers of
+    edge totals / shard digests / pair windows and the all_reduce of the step time go through RCCL,
+    and the result equals a run without any process group. (The 1-GPU pool cannot host two RCCL
+    ranks on one device; the world-2 flow is covered over gloo above.)"""
+    from test_shard_dist import _free_port
+    common = ["--gpus", "1", "--pairs", "4096", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-extras",
+              "--check-window", "512"]
+    rccl = _bench_json(common, 1, _free_port(), backend="nccl", launcher=True)
+    plain = _bench_json(common, 1)
+    c, c0 = rccl["checks"], plain["checks"]
+    assert c["collective_backend"] == "nccl" and c0["collective_backend"] is None
+    assert c["shard_digests_ok"] and c["gsum_invariant"]["ok"] and c["gsum_invariant"]["pairs"] == 4096
+    assert c["global_digest"] == c0["global_digest"]
+    assert c["global_output_edges"] == c0["global_output_edges"]
