@@ -317,8 +317,8 @@ class Oracle:
         assert rc == 0
         return self._trim(oc, ov)
 
-    def ct_mul(self, A, B, nonces, salts=None, H=None, canon_tag=0, edge_budget=1200000):
-        prm = default_params(canon_tag, edge_budget)
+    def ct_mul(self, A, B, nonces, salts=None, H=None, canon_tag=0, edge_budget=1200000, Bm=337):
+        prm = default_params(canon_tag, edge_budget, B=Bm)
         va, vb = self._view(A), self._view(B)
         capL, capE = C.c_uint64(), C.c_uint64()
         self.lib.orc_ct_mul_caps(C.byref(prm), C.byref(va), C.byref(vb), C.byref(capL), C.byref(capE))

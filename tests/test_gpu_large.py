@@ -208,6 +208,32 @@ def test_large_column_bounds_vs_oracle(oracle):
     assert plan.n_large == len(xs)
 
 
+@pytest.mark.parametrize("Bm", [97, 1031])
+def test_ct_mul_other_B_vs_oracle(oracle, Bm):
+    """Params.B other than 337 (the reference takes B from Params, core/types.hpp): a small B
+    (dense tables of 194 cells) and B = 1031 (three output rows per products lane, 97 KB of LDS per
+    workgroup), fresh-shaped and dense chain-like pairs, vs the oracle with the same B."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    rng = np.random.default_rng(Bm)
+    xs, ys = [], []
+    for k in range(6):
+        xs.append(_mk(rng, 2, 20 + k, dup_ok=False, B=Bm))
+        ys.append(_mk(rng, 2, 20, dup_ok=False, B=Bm))
+    for k in range(6):
+        nl = 2 + k % 3
+        x = _mk(rng, nl, int(nl * rng.integers(Bm // 2, 2 * Bm)), dup_ok=False, B=Bm)
+        y = _mk(rng, 2, 40, dup_ok=False, B=Bm)
+        xs.append(x); ys.append(y)
+        xs.append(y); ys.append(x)
+    xs.append(_mk(rng, 3, 60, dup_ok=True, B=Bm))   # duplicates: scatter mode
+    ys.append(_mk(rng, 2, 50, dup_ok=True, B=Bm))
+    eng = Engine(device=0, B=Bm, canon_tag=0xB0)
+    out, plan, per = _run_mul(eng, xs, ys, seed=Bm)
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        ref = oracle.ct_mul(x, y, per[p], canon_tag=0xB0, Bm=Bm)
+        _same(out[p], ref, view=False)
+
+
 def test_large_scatter_and_duplicates_vs_oracle(oracle):
     """Scatter mode (sparse x sparse tasks) and duplicate (layer, idx, ch) edges in the dense side,
     empty layers, empty ciphers, single edges."""
