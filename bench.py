@@ -6,7 +6,10 @@ Workload (BASELINE.json cfg 3): batched weights-only ct_mul over fresh-shaped Ci
 one GPU, inputs resident in HBM. One step = plan (sizing) + exec over the whole batch.
 Multi-GPU (cfg 5): one process per GPU, 2^21 pairs per rank (2^24 at N=8); each rank owns an
 independent shard (weak scaling); the only collective is the gather of per-rank output totals
-(global CSR offsets), over RCCL.
+(global CSR offsets), over RCCL. `python bench.py --gpus N` (N > 1, no launcher environment) starts
+N ranks itself through torch.distributed.run before this process touches the GPU; under a launcher
+(WORLD_SIZE set) each rank takes its own GPU (LOCAL_RANK) and the ranks check that their devices
+are distinct. The line reports the devices and the world size / backend torch.distributed saw.
 
 Also reported (side fields, rank 0): cfg 2 element-wise Fp127 add/mul at 2^24, full ct_mul WITH
 sigma (the reference's complete ct_mul) on a smaller batch, cfg 4 (GPU enc_value + depth-8
@@ -28,7 +31,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each). N > 1 without a launcher: bench.py starts N ranks itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=None,
@@ -41,6 +45,10 @@ def parse():
     ap.add_argument("--chain-inputs", type=int, default=1 << 16, help="cfg 4 chain inputs (enc_value outputs)")
     ap.add_argument("--chain-chunk", type=int, default=1 << 12)
     ap.add_argument("--chain-depth", type=int, default=8)
+    ap.add_argument("--chain-check", type=int, default=16,
+                    help="cfg 4: chains (first inputs of the first chunk) whose final outputs are digest-compared "
+                         "with the pinned CPU port, which is also timed on them (cpu_baseline)")
+    ap.add_argument("--chain-ref", type=int, default=2, help="cfg 4: reference chains (oracle/_ref) timed, depth 4")
     ap.add_argument("--chain-streams", type=int, default=1,
                     help="host threads / HIP streams running chunks (2 measured no faster: the products kernel is VALU-bound)")
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
@@ -48,13 +56,96 @@ def parse():
                     help="run one side measurement alone (profiling) and print its JSON")
     ap.add_argument("--check-window", type=int, default=4096,
                     help="pairs per rank whose digests rank 0 recomputes from global indices (shard check)")
+    ap.add_argument("--topology-only", action="store_true",
+                    help="launcher check: every rank reports its device and the process group, no GPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     return ap.parse_args()
 
 
+def _shared_ok():
+    """PVAC_BENCH_ALLOW_SHARED=1: ranks may share a GPU (the one-GPU rehearsal of the N > 1 flow;
+    gloo collectives). Never set by the driver: there every rank must own a distinct GPU."""
+    return os.environ.get("PVAC_BENCH_ALLOW_SHARED") == "1"
+
+
+def spawn(args):
+    """`--gpus N` (N > 1) with no launcher: start N ranks (torch.distributed.run, one process per
+    GPU, 127.0.0.1 rendezvous) and forward rank 0's JSON line. This process never initialises the
+    GPU (torch.cuda.device_count() does not on this ROCm image), so nothing is re-executed after a
+    HIP call. Returns the children's exit status."""
+    import socket
+    import subprocess
+    import torch
+    n = args.gpus
+    vis = torch.cuda.device_count()
+    if n > vis and not _shared_ok():
+        print(f"bench.py: --gpus {n} needs {n} distinct visible GPUs (one rank each); this host shows {vis}",
+              file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = []
+    for line in proc.stdout:   # progress is forwarded as it comes (to stderr); the JSON line last
+        if line.startswith("{"):
+            lines.append(line.strip())
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: ranks exited with status {rc}", file=sys.stderr, flush=True)
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr, flush=True)
+        return 3
+    print(lines[0], flush=True)
+    return 0
+
+
+def _device_id(torch, gpu):
+    """Identity of a rank's GPU: the device uuid (distinct per physical GPU, whatever each rank's
+    visible-device numbering), else host + ordinal; "cpu" for a device-less launcher check."""
+    import socket
+    if gpu is None:
+        return f"{socket.gethostname()}:cpu"
+    try:
+        pr = torch.cuda.get_device_properties(gpu)
+        return f"{pr.uuid}" if str(pr.uuid) else f"{socket.gethostname()}:{pr.pci_domain_id}:{pr.pci_bus_id}"
+    except Exception:
+        return f"{socket.gethostname()}:cuda:{gpu}"
+
+
+def topology(torch, dist, dist_on, world, rank, gpu):
+    """Every rank's device and what torch.distributed saw; raises unless the ranks own distinct
+    devices (or sharing was asked for)."""
+    me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": gpu,
+          "id": _device_id(torch, gpu)}
+    if dist_on:
+        allv = [None] * dist.get_world_size()
+        dist.all_gather_object(allv, me)
+        seen = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend())}
+    else:
+        allv = [me]
+        seen = {"world_size": 1, "backend": None}
+    distinct = len({d["id"] for d in allv})
+    if distinct < len(allv) and not _shared_ok():
+        raise RuntimeError(f"bench.py: {len(allv)} ranks on {distinct} distinct devices ({allv}); one rank per "
+                           "GPU is required (PVAC_BENCH_ALLOW_SHARED=1 only for the one-GPU rehearsal)")
+    if seen["world_size"] != world:
+        raise RuntimeError(f"bench.py: WORLD_SIZE {world} but the process group has {seen['world_size']} ranks")
+    return {"n_gpus": distinct, "ranks": len(allv), "devices": allv, "dist": seen,
+            "shared_devices": distinct < len(allv)}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(spawn(args))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -62,19 +153,40 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU over RCCL; PVAC_BENCH_BACKEND=gloo rehearses the multi-rank flow with
-    # ranks sharing the visible GPUs (local rank modulo the device count)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    # one process per GPU over RCCL; PVAC_BENCH_BACKEND=gloo + PVAC_BENCH_ALLOW_SHARED=1 rehearse
+    # the multi-rank flow with ranks sharing the visible GPUs (local rank modulo the device count)
     backend = os.environ.get("PVAC_BENCH_BACKEND", "nccl")
-    gpu = local % max(torch.cuda.device_count(), 1)
+    ndev = torch.cuda.device_count()
+    if args.topology_only:
+        gpu = None if ndev == 0 else local % ndev
+    elif local < ndev:
+        gpu = local
+    elif _shared_ok() and ndev:
+        gpu = local % ndev
+    else:
+        raise SystemExit(f"bench.py: rank {rank} (local {local}) has no GPU of its own ({ndev} visible)")
     # PVAC_BENCH_DIST=1 runs the distributed flow (process group, gathers, self-checks) at world 1
     # too: under torch.distributed.run with one rank it puts the collectives on RCCL on a 1-GPU box
     dist_on = world > 1 or os.environ.get("PVAC_BENCH_DIST") == "1"
     if dist_on:
-        torch.cuda.set_device(gpu)
-        if backend == "nccl":
+        if gpu is not None:
+            torch.cuda.set_device(gpu)
+        if backend == "nccl" and gpu is not None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group("gloo")
+    topo = topology(torch, dist, dist_on, world, rank, gpu)
+    if args.topology_only:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "ct_mul/s", "topology_only": True,
+                              "n_gpus": topo["n_gpus"], "ranks": topo["ranks"], "devices": topo["devices"],
+                              "dist": topo["dist"]}), flush=True)
+        if dist_on:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     from pvac_hfhe_cppbyv_amd import Engine
 
     eng = Engine(device=gpu, canon_tag=0x5EED0003)
@@ -122,6 +234,7 @@ def main():
         dist.barrier()
     eng.timing_reset()
     eng.timing(True)
+    redo0 = eng.ct_mul_redo_count()
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
@@ -160,7 +273,10 @@ def main():
         "metric": METRIC,
         "value": value,
         "unit": "ct_mul/s",
-        "n_gpus": world,
+        "n_gpus": topo["n_gpus"],
+        "ranks": topo["ranks"],
+        "devices": [d["id"] for d in topo["devices"]],
+        "dist": topo["dist"],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -177,7 +293,8 @@ def main():
             "edges_per_layer": args.epl,
             "global_pairs": world * n,
             "output_edges_per_pair": out_edges / n,
-            "parallelism": f"dp{world} (independent pair shards, gather of totals over RCCL)",
+            "parallelism": f"dp{world} (independent pair shards, gather of totals over "
+                           f"{topo['dist']['backend'] or 'no process group'})",
             "shard": {"first_pair": first, "edge_slot_offset": placement.get("offset"),
                       "global_edge_slots": placement.get("total_edge_slots")},
         },
@@ -232,7 +349,11 @@ def main():
         result["roofline"]["valu"] = {"peak": ceil_w, "unit": "wave64 VALU inst/s", "achieved": None,
                                       "note": "no PMC summary for this kernel / batch in profiles/"}
 
+    # fresh-kernel pairs re-run on the general path during the timed steps (a key sum of 0 mod p:
+    # never for these uniform nonzero weights, so any redo here is a kernel defect costing time)
+    redo = eng.ct_mul_redo_count() - redo0
     result["checks"] = self_checks(eng, args, A, B, out, nonces, n, first, seed, world, rank)
+    result["checks"]["fresh_redo"] = {"pairs_per_step": redo / args.steps, "ok": redo == 0}
     result["checks"]["collective_backend"] = dist.get_backend() if dist_on else None
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(eng, A, B, out, n, args)
@@ -308,26 +429,12 @@ def cpu_baseline(eng, A, B, out, n, args):
     ct_mul minus sigma, std::unordered_map aggregation) on a bounded sample of the SAME
     device-resident inputs; digests are cross-checked against the GPU output."""
     import numpy as np
-    import torch
     from helpers import Oracle, default_params
     orc = Oracle.load()
     k = min(args.cpu_pairs, n)
     u = lambda t: t.cpu().numpy().view(np.uint64)
-    a_loff, a_eoff = u(A.l_off[:k]), u(A.e_off[:k])
-    b_loff, b_eoff = u(B.l_off[:k]), u(B.e_off[:k])
-    a_lend = int(a_loff[-1] + u(A.l_cnt[k - 1:k])[0])
-    a_eend = int(a_eoff[-1] + u(A.e_cnt[k - 1:k])[0])
-    b_lend = int(b_loff[-1] + u(B.l_cnt[k - 1:k])[0])
-    b_eend = int(b_eoff[-1] + u(B.e_cnt[k - 1:k])[0])
-    cs = lambda x: np.ascontiguousarray(x)
-    # keep u64 (np.append with a Python int would promote uint64 + int64 -> float64)
-    app = lambda a, v: cs(np.concatenate([a, np.array([v], np.uint64)]))
-    al, ae = app(a_loff, a_lend), app(a_eoff, a_eend)
-    bl, be = app(b_loff, b_lend), app(b_eoff, b_eend)
-    assert al.dtype == np.uint64 and be.dtype == np.uint64
-    a_lay = cs(A.layers[:a_lend].cpu().numpy()); b_lay = cs(B.layers[:b_lend].cpu().numpy())
-    am, awl, awh = u(A.meta[:a_eend]), u(A.w_lo[:a_eend]), u(A.w_hi[:a_eend])
-    bm, bwl, bwh = u(B.meta[:b_eend]), u(B.w_lo[:b_eend]), u(B.w_hi[:b_eend])
+    al, a_lay, ae, am, awl, awh = _pack_host(A, k)
+    bl, b_lay, be, bm, bwl, bwh = _pack_host(B, k)
     counts = np.zeros(k, np.uint64)
     digests = np.zeros(k, np.uint64)
     prm = default_params(0x5EED0003)
@@ -354,6 +461,28 @@ def cpu_baseline(eng, A, B, out, n, args):
         "cpu_model": _cpu_model(),
         "gpu_output_matches": bool(np.array_equal(gpu_dig, digests) and np.array_equal(gpu_cnt, counts)),
     }
+
+
+def _pack_host(X, k):
+    """The first k ciphers of a device batch (capacity-padded CSR allowed) as host arrays in the
+    oracle's packed layout: offsets with k + 1 entries (u64), layer records, meta, w_lo, w_hi."""
+    import numpy as np
+    import torch
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+
+    def rows(off, cnt):   # the used slots of every cipher, in order
+        cnt = cnt.to(torch.int64)
+        excl = torch.cumsum(cnt, 0) - cnt
+        idx = torch.repeat_interleave(off.to(torch.int64) - excl, cnt)
+        packed = torch.zeros(k + 1, dtype=torch.int64, device=cnt.device)
+        packed[1:] = torch.cumsum(cnt, 0)
+        return idx + torch.arange(idx.numel(), device=idx.device), packed
+
+    li, lo = rows(X.l_off[:k], X.l_cnt[:k])
+    ei, eo = rows(X.e_off[:k], X.e_cnt[:k])
+    cs = np.ascontiguousarray
+    return (cs(u(lo)), cs(X.layers[li].cpu().numpy()), cs(u(eo)), cs(u(X.meta[ei])), cs(u(X.w_lo[ei])),
+            cs(u(X.w_hi[ei])))
 
 
 def _cpu_model():
@@ -410,7 +539,7 @@ def extras(eng, args, with_cpu):
             fp[name]["gpu_output_matches"] = bool(np.array_equal(glo, olo))
     res["fp127_cfg2"] = fp
     del bufs
-    res["ct_add_sub_cfg3"] = add_bench(eng, args)
+    res["ct_add_sub_cfg3"] = add_bench(eng, args, with_cpu)
     res["ct_mul_with_sigma"] = sigma_bench(eng, args, with_cpu)
     res["cfg4_chain"] = chain_bench(eng, args)
     res["enc_value"] = enc_bench(eng, args, with_cpu)
@@ -435,7 +564,37 @@ def _host_roundtrip(pairs=1 << 15):
         return {"error": repr(ex)}
 
 
-def add_bench(eng, args):
+def _add_cpu_prep(A, B, k):
+    return k, _pack_host(A, k), _pack_host(B, k)
+
+
+def _add_cpu(eng, cpu, C_, neg, args):
+    """The pinned port's ct_add / ct_sub on the first k pairs of the same batch (1 thread and the
+    box's CPU share), edge digests compared with the GPU output."""
+    import ctypes as C
+    import numpy as np
+    from helpers import Oracle, default_params
+    orc = Oracle.load()
+    prm = default_params(0x5EED0003)
+    k, a, b = cpu
+    P = lambda x: x.ctypes.data_as(C.c_void_p)
+    out = {}
+    for th in (1, max(1, args.cpu_share_threads)):
+        cnt, dig = np.zeros(k, np.uint64), np.zeros(k, np.uint64)
+        secs = orc.lib.orc_ct_add_batch_timed(C.byref(prm), k, *(P(x) for x in a), *(P(x) for x in b), int(neg), th,
+                                              P(cnt), P(dig))
+        out[th] = (secs, cnt, dig)
+    secs, cnt, dig = out[1]
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    mt = max(1, args.cpu_share_threads)
+    return {"value": k / secs, "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": f"the first {k} pairs of the batch, weights-only, {secs:.2f} s",
+            "multi_thread": {"value": k / out[mt][0], "cores": mt, "seconds": out[mt][0]},
+            "gpu_output_matches": bool(np.array_equal(u(eng.digest(_head(C_, k))), dig) and
+                                       np.array_equal(u(C_.e_cnt[:k]), cnt))}
+
+
+def add_bench(eng, args, with_cpu=False):
     """Batched ct_add / ct_sub / ct_scale (A13 / A6) on the cfg-3 batch shape (2^20 fresh-shaped pairs,
     weights only): the k_ct_add stream kernel against the HBM roofline. Algorithmic bytes per
     pair: every input edge read and written once (2 x 24 B x (|A.E| + |B.E|)), every layer record
@@ -446,8 +605,11 @@ def add_bench(eng, args):
     A = eng.gen_fresh(n, 0x5EED0A01, args.epl)
     B = eng.gen_fresh(n, 0x5EED0A02, args.epl)
     res = {"pairs": n}
+    cpu = _add_cpu_prep(A, B, min(args.cpu_pairs, n)) if with_cpu else None
     for name, neg in (("add", False), ("sub", True)):
         C_ = eng.ct_add(A, B, negate=neg)   # warm-up
+        if cpu is not None:
+            res.setdefault("cpu_baseline", {})[name] = _add_cpu(eng, cpu, C_, neg, args)
         del C_
         torch.cuda.synchronize(dev)
         eng.timing_reset()
@@ -644,10 +806,12 @@ def chain_bench(eng, args):
     host threads, each with its own engine context on its own HIP stream, so one chunk's
     VALU-bound products overlap another chunk's atomic / memory-bound ordering kernels."""
     import threading
+    import numpy as np
     import torch
     from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine, powg_table
     dev = eng.device
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
+    n_chk = max(0, min(args.chain_check, chunk))
     S = max(1, args.chain_streams)
     torch.cuda.reset_peak_memory_stats(dev)
     _enc_keys(eng)
@@ -714,6 +878,9 @@ def chain_bench(eng, args):
                         tc = time.perf_counter()
                         r["gsum_failed"] += e2.check_mul_gsum(cur, X, out, nonces)
                         r["gsum_pairs"] += k
+                        if c0 == 0 and d == depth - 1 and n_chk:   # the oracle sample's GPU side
+                            r["chk_digests"] = e2.digest(_head(out, n_chk)).cpu().numpy().view(np.uint64).copy()
+                            r["chk_counts"] = out.e_cnt[:n_chk].cpu().numpy().view(np.uint64).copy()
                         r["check_s"] += time.perf_counter() - tc
                         r["products"] += float((cur.e_cnt[:k].to(torch.float64) *
                                                 X.e_cnt[:k].to(torch.float64)).sum().item())
@@ -744,6 +911,7 @@ def chain_bench(eng, args):
     # minus the untimed invariant checks (workers run them in turn on their own stream)
     check_s = max(r["check_s"] for r in results)
     chain_s = time.perf_counter() - t1 - check_s
+    x_host = _pack_host(X_all, n_chk) if n_chk else None   # the sampled chains' inputs
     del X_all, vals
     errors = [r["error"] for r in results if "error" in r]
     step_ms = [sum(r["step_ms"][d] for r in results) for d in range(depth)]
@@ -776,7 +944,74 @@ def chain_bench(eng, args):
         out["roofline"] = {"error": repr(ex)}
     if errors:
         out["errors"] = errors
+    if n_chk and x_host is not None:
+        out.update(_chain_cpu(args, x_host, n_chk, depth, results[0].get("chk_digests"),
+                              results[0].get("chk_counts"), n * depth / chain_s))
     return out
+
+
+def _head(X, k):
+    """View of the first k ciphers of a batch (absolute offsets: no copy)."""
+    from pvac_hfhe_cppbyv_amd import DeviceBatch
+    return DeviceBatch(k, X.l_off[:k], X.l_cnt[:k], X.layers, X.e_off[:k], X.e_cnt[:k], X.meta, X.w_lo, X.w_hi)
+
+
+def _chain_cpu(args, x_host, k, depth, gpu_dig, gpu_cnt, gpu_rate):
+    """cfg 4's CPU side on the bench's own first k chains (same enc_value inputs): the pinned port
+    (oracle/pvac_oracle.cpp, the reference's unordered_map aggregation) runs c_j = ct_mul(c_{j-1}, x)
+    to the same depth on 1 thread and on the box's CPU share, and its final edge digests must equal
+    the GPU's; the unmodified reference (oracle/_ref, full ct_mul with sigma) is timed on a short chain."""
+    import ctypes as C
+    import numpy as np
+    from helpers import Oracle, default_params
+    orc = Oracle.load()
+    prm = default_params(0x5EED0003)
+    lo, lay, eo, meta, wl, wh = x_host
+    P = lambda x: x.ctypes.data_as(C.c_void_p)
+    res = {}
+    runs = {}
+    for th in (1, max(1, args.cpu_share_threads)):
+        cnt, dig, se = np.zeros(k, np.uint64), np.zeros(k, np.uint64), np.zeros(depth, np.uint64)
+        secs = orc.lib.orc_ct_mul_chain_timed(C.byref(prm), k, P(lo), P(lay), P(eo), P(meta), P(wl), P(wh), depth, th,
+                                              P(cnt), P(dig), P(se))
+        runs[th] = (secs, cnt, dig, se)
+    secs, cnt, dig, se = runs[1]
+    ok = gpu_dig is not None and bool(np.array_equal(dig, gpu_dig) and np.array_equal(cnt, gpu_cnt))
+    res["oracle_sample_ok"] = ok
+    res["oracle_sample"] = {"chains": k, "depth": depth, "check": "final c_depth edge digests (meta, w) and edge "
+                            "counts of the bench's first chains vs the pinned CPU port on the same enc_value inputs",
+                            "edges_per_input_by_step": [float(x) / k for x in se]}
+    mt = max(1, args.cpu_share_threads)
+    res["cpu_baseline"] = {
+        "value": k * depth / secs, "unit": "ct_mul/s", "cores": 1, "kind": "port",
+        "sample": f"{k} chains to depth {depth} (the bench's first {k} enc_value inputs), weights-only, {secs:.2f} s",
+        "multi_thread": {"value": k * depth / runs[mt][0], "cores": mt, "seconds": runs[mt][0]},
+        "impl": "oracle/pvac_oracle.cpp orc_ct_mul_chain_timed (pinned to the reference by tests/test_oracle.py)",
+        "gpu_over_cpu_1core": gpu_rate / (k * depth / secs)}
+    ref = _ref_chain_baseline(args.chain_ref)
+    if ref:
+        res["cpu_baseline"]["reference"] = ref
+    return res
+
+
+def _ref_chain_baseline(ninputs, depth=4):
+    """The UNMODIFIED reference's chain (full ct_mul WITH sigma, tests/test_main.cpp:289-295 shape):
+    depth 4 on a few inputs, since its sigma stage costs ~104 us per output edge (depth 8 would take
+    ~80 s per chain)."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe) or ninputs <= 0:
+        return None
+    try:
+        outp = subprocess.run([exe, "time_chain", str(ninputs), str(depth)], capture_output=True, text=True,
+                              timeout=240)
+        r = json.loads([l for l in outp.stdout.splitlines() if l.startswith("{")][-1])
+        return {"value": r["ct_mul_per_s"], "unit": "ct_mul/s", "cores": 1, "kind": "reference",
+                "sample": f"{r['inputs']} chains to depth {r['depth']} (reference pvac-hfhe 0.1.0, enc_value inputs, "
+                          f"full ct_mul with sigma), {r['seconds']:.2f} s",
+                "edges_by_step": r["edges_by_step"]}
+    except Exception as ex:
+        return {"error": repr(ex)}
 
 
 def _ref_full_baseline():

@@ -2,8 +2,10 @@
  *
  * Drop-in boundary for the pvac-hfhe 0.1.0 hot path (reference: include/pvac/...). The
  * reference exposes a header-only, by-value C++ API and no FFI; every entry point below
- * names the reference function it replaces. The C++ shim headers under include/pvac/ keep
- * the reference's type names and signatures and route through these entry points.
+ * names the reference function it replaces. The C++ adapter include/pvac_hip.hpp is
+ * templated on the reference's own pvac::Cipher / PubKey types (it does not restate them) and
+ * routes batched calls through these entry points; INTEGRATION.md §2 is the patch a
+ * maintainer adds to the reference's ops/arithmetic.hpp to dispatch ct_mul & co. through it.
  *
  * Conventions
  *  - All functions are noexcept, never throw, and return int status: 0 = ok, <0 = error
@@ -15,7 +17,7 @@
  *  - Fp values are p = 2^127-1 field elements as two u64 limbs (lo, hi) in SoA arrays.
  *  - Randomness is an explicit input: the reference draws nonces/salts from getrandom(2)
  *    inside ct_mul (core/random.hpp:40-110); here the caller passes those words, which
- *    makes outputs reproducible and testable. The C++ shim fills them from getrandom.
+ *    makes outputs reproducible and testable. The C++ adapter fills them from getrandom.
  */
 #ifndef PVAC_HIP_H
 #define PVAC_HIP_H

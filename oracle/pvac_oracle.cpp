@@ -959,4 +959,98 @@ double orc_ct_mul_batch_timed(const orc_params* prm, uint64_t npairs, const uint
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+/* batched weights-only ct_add / ct_sub (A13 / A6) over packed pairs, for bench.py's cpu_baseline of
+ * the cfg-3 add/sub leg: per-pair output edge counts and FNV-1a edge digests. Returns seconds. */
+double orc_ct_add_batch_timed(const orc_params* prm, uint64_t npairs, const uint64_t* a_loff, const orc_layer* a_layers,
+                              const uint64_t* a_eoff, const uint64_t* a_meta, const uint64_t* a_wlo,
+                              const uint64_t* a_whi, const uint64_t* b_loff, const orc_layer* b_layers,
+                              const uint64_t* b_eoff, const uint64_t* b_meta, const uint64_t* b_wlo,
+                              const uint64_t* b_whi, int negate_b, int threads, uint64_t* out_counts,
+                              uint64_t* out_digests) {
+    if (threads < 1) threads = 1;
+    auto view = [](const uint64_t* loff, const orc_layer* layers, const uint64_t* eoff, const uint64_t* meta,
+                   const uint64_t* wlo, const uint64_t* whi, uint64_t i) {
+        orc_cipher c{};
+        c.nL = loff[i + 1] - loff[i]; c.nE = eoff[i + 1] - eoff[i];
+        c.layers = const_cast<orc_layer*>(layers + loff[i]);
+        c.meta = const_cast<uint64_t*>(meta + eoff[i]);
+        c.w_lo = const_cast<uint64_t*>(wlo + eoff[i]);
+        c.w_hi = const_cast<uint64_t*>(whi + eoff[i]);
+        return c;
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            for (uint64_t i = (uint64_t)t; i < npairs; i += (uint64_t)threads) {
+                orc_cipher A = view(a_loff, a_layers, a_eoff, a_meta, a_wlo, a_whi, i);
+                orc_cipher B = view(b_loff, b_layers, b_eoff, b_meta, b_wlo, b_whi, i);
+                Ct a = load(&A), b = load(&B), c;
+                ct_add_impl(prm, a, b, negate_b != 0, (prm->m_bits + 63) / 64, false, c);
+                u64 h = 0xcbf29ce484222325ULL;
+                for (auto& e : c.E) {
+                    h = fnv_step(h, (u64)e.layer | ((u64)e.idx << 32) | ((u64)e.ch << 48));
+                    h = fnv_step(h, e.w.lo);
+                    h = fnv_step(h, e.w.hi);
+                }
+                if (out_counts) out_counts[i] = c.E.size();
+                if (out_digests) out_digests[i] = h;
+            }
+        });
+    for (auto& x : th) x.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+/* cfg 4 on the CPU port (SURVEY 8(d) restatement of tests/test_main.cpp:289-295): per input i,
+ * c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) for k = 1..depth, weights only. Nonces do not reach the
+ * edges (only layer records), so they are synthetic here; the FNV-1a edge digest of c_depth is
+ * comparable with the engine's. step_edges[d] accumulates |c_{d+1}.E| over the inputs. */
+double orc_ct_mul_chain_timed(const orc_params* prm, uint64_t ninputs, const uint64_t* loff, const orc_layer* layers,
+                              const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
+                              int depth, int threads, uint64_t* out_counts, uint64_t* out_digests,
+                              uint64_t* step_edges) {
+    if (threads < 1) threads = 1;
+    std::vector<std::vector<u64>> per((size_t)threads, std::vector<u64>((size_t)(depth > 0 ? depth : 1), 0));
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            std::vector<u64> nonces;
+            for (uint64_t i = (uint64_t)t; i < ninputs; i += (uint64_t)threads) {
+                orc_cipher X{};
+                X.nL = loff[i + 1] - loff[i]; X.nE = eoff[i + 1] - eoff[i];
+                X.layers = const_cast<orc_layer*>(layers + loff[i]);
+                X.meta = const_cast<uint64_t*>(meta + eoff[i]);
+                X.w_lo = const_cast<uint64_t*>(wlo + eoff[i]);
+                X.w_hi = const_cast<uint64_t*>(whi + eoff[i]);
+                const Ct x = load(&X);
+                Ct c = x;
+                for (int d = 0; d < depth; ++d) {
+                    Ct nxt;
+                    nonces.assign(2 * c.L.size() * x.L.size(), 0);
+                    for (size_t k = 0; k < nonces.size(); ++k) nonces[k] = i * 0x100000001b3ULL + 977u * (u64)d + k;
+                    ct_mul_impl(prm, nullptr, c, x, nonces.data(), nullptr, nxt);
+                    c = std::move(nxt);
+                    per[(size_t)t][(size_t)d] += c.E.size();
+                }
+                u64 h = 0xcbf29ce484222325ULL;
+                for (auto& e : c.E) {
+                    h = fnv_step(h, (u64)e.layer | ((u64)e.idx << 32) | ((u64)e.ch << 48));
+                    h = fnv_step(h, e.w.lo);
+                    h = fnv_step(h, e.w.hi);
+                }
+                if (out_counts) out_counts[i] = c.E.size();
+                if (out_digests) out_digests[i] = h;
+            }
+        });
+    for (auto& x : th) x.join();
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (step_edges)
+        for (int d = 0; d < depth; ++d) {
+            step_edges[d] = 0;
+            for (int t = 0; t < threads; ++t) step_edges[d] += per[(size_t)t][(size_t)d];
+        }
+    return secs;
+}
+
 }  // extern "C"

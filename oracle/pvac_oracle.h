@@ -121,6 +121,20 @@ double orc_ct_mul_batch_timed(const orc_params* prm, uint64_t npairs,
                               const uint64_t* b_loff, const orc_layer* b_layers, const uint64_t* b_eoff,
                               const uint64_t* b_meta, const uint64_t* b_wlo, const uint64_t* b_whi,
                               int threads, uint64_t* out_counts, uint64_t* out_digests);
+/* batched weights-only ct_add (negate_b = 0) / ct_sub (1) over packed pairs; per-pair edge counts
+ * and FNV-1a edge digests. Returns seconds. */
+double orc_ct_add_batch_timed(const orc_params* prm, uint64_t npairs, const uint64_t* a_loff, const orc_layer* a_layers,
+                              const uint64_t* a_eoff, const uint64_t* a_meta, const uint64_t* a_wlo,
+                              const uint64_t* a_whi, const uint64_t* b_loff, const orc_layer* b_layers,
+                              const uint64_t* b_eoff, const uint64_t* b_meta, const uint64_t* b_wlo,
+                              const uint64_t* b_whi, int negate_b, int threads, uint64_t* out_counts,
+                              uint64_t* out_digests);
+/* cfg 4: depth-`depth` chains c_k = ct_mul(c_{k-1}, x_i) per input of a packed batch (weights
+ * only); final edge counts / FNV-1a edge digests per input, per-step edge totals. Returns seconds. */
+double orc_ct_mul_chain_timed(const orc_params* prm, uint64_t ninputs, const uint64_t* loff, const orc_layer* layers,
+                              const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
+                              int depth, int threads, uint64_t* out_counts, uint64_t* out_digests,
+                              uint64_t* step_edges);
 
 #ifdef __cplusplus
 }

@@ -538,6 +538,33 @@ static void cmd_time_mul(int npairs, int threads) {
                 npairs, threads, s, npairs / s, et);
 }
 
+// cfg 4's workload on the unmodified reference (SURVEY 8(d) restatement of tests/test_main.cpp:289-295):
+// x = enc_value(v), c_0 = x, c_k = ct_mul(c_{k-1}, x) for k = 1..depth (full ct_mul, sigma included).
+// Only the ct_mul steps are timed; one line of JSON with the per-step edge counts.
+static void cmd_time_chain(int ninputs, int depth) {
+    reseed(0x5EED0D40ULL);
+    g_logging = false;
+    Params prm; PubKey pk; SecKey sk;
+    keygen(prm, pk, sk);
+    std::vector<Cipher> X;
+    for (int i = 0; i < ninputs; ++i) X.push_back(enc_value(pk, sk, (uint64_t)i * 31u + 7u));
+    std::vector<size_t> edges((size_t)depth, 0);
+    double s = 0.0;
+    for (int i = 0; i < ninputs; ++i) {
+        Cipher c = X[(size_t)i];
+        for (int d = 0; d < depth; ++d) {
+            auto t0 = std::chrono::steady_clock::now();
+            c = ct_mul(pk, c, X[(size_t)i]);
+            s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            edges[(size_t)d] += c.E.size();
+        }
+    }
+    std::printf("{\"inputs\": %d, \"depth\": %d, \"seconds\": %.6f, \"ct_mul_per_s\": %.6f, \"edges_by_step\": [",
+                ninputs, depth, s, ninputs * depth / s);
+    for (int d = 0; d < depth; ++d) std::printf("%s%zu", d ? ", " : "", edges[(size_t)d]);
+    std::printf("]}\n");
+}
+
 static void cmd_time_enc(int ncalls) {
     reseed(0x5EED0D00ULL);
     g_logging = false;
@@ -644,6 +671,10 @@ int main(int argc, char** argv) {
     }
     if (cmd == "time_enc") {
         cmd_time_enc(argc > 2 ? std::atoi(argv[2]) : 16);
+        return 0;
+    }
+    if (cmd == "time_chain") {
+        cmd_time_chain(argc > 2 ? std::atoi(argv[2]) : 1, argc > 3 ? std::atoi(argv[3]) : 3);
         return 0;
     }
     if (cmd == "time_mul") {

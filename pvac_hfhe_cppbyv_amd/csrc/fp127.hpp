@@ -345,11 +345,14 @@ __device__ __forceinline__ fp fp_fold3(uint64_t l0, uint64_t l1, uint64_t l2) {
 // Sum of many products a*b of canonical operands without a carry chain per product: a and b
 // split into five limbs of 26/26/26/26/23 bits (< 2^26), and column k of the running sum is a
 // u64 that takes a_i b_j (< 2^52) for every i + j = k, one v_mad_u64_u32 each (25 per product,
-// nothing else). A column takes at most 5 terms per product, so from a normalised start (< 2^26)
-// col26_norm must run within every 2^11 products (5 * 2^11 * 2^52 + 2^26 < 2^64). col26_fold
+// nothing else). Limb 4 is < 2^23, so per product column 3 takes 4 terms < 2^52 and column 4 three
+// terms < 2^52 plus two < 2^49: at most 4 * 2^52 = 2^54 per product and column. From a normalised
+// start (< 2^26) col26_norm must therefore run within every 1023 products
+// (1023 * 2^54 + 2^26 < 2^64; kCol26MaxProducts, checked where the loops size their chunks). col26_fold
 // gives the canonical residue of the sum, the same value as the reference's fp_add chain of
 // canonical fp_mul results (field.hpp:50-56, 209-213: that chain computes the exact sum mod p).
 constexpr uint32_t kM26 = (1u << 26) - 1u;
+constexpr uint32_t kCol26MaxProducts = 1023u;   // products per column set between col26_norm calls
 __device__ __forceinline__ void fp_split26(const fp& v, uint32_t* l) {   // v canonical (< 2^127)
     l[0] = (uint32_t)v.lo & kM26;
     l[1] = (uint32_t)(v.lo >> 26) & kM26;

@@ -23,6 +23,7 @@
 //                        independent, no overflow below 2^21 addends). compact_layers is a
 //                        wave-wide bitmask closure over LDS-resident parent masks; edges are
 //                        staged in LDS at their emit positions and written out coalesced.
+#include <atomic>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -1421,7 +1422,12 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                     emit(rec0[k] >> 16, (ordB[k] >> 27) & 3u, o1 + ((ordB[k] >> 19) & 7u));
                     emit(rec1[k] & 0xFFFFu, (ordB[k] >> 29) & 3u, o2 + ((ordB[k] >> 22) & 7u));
                 } else if (tb0 != kT16) {   // big bucket: each slot's rank from the others' times (O(z^2), rare)
+                    // Two passes: every member's rank is computed from the UNMODIFIED first-insert
+                    // times while only the positions' limb words record the cell; the cell words
+                    // get their positions afterwards (an emit inside the rank loop would overwrite
+                    // times that later members still compare against)
                     const uint32_t q0 = rec0[k] & 0xFFFFu, g = rec0[k] >> 16;
+                    uint32_t cnt = 0;
                     for (uint32_t q = q0; q < q0 + g; ++q) {
                         const uint32_t m = members[q];
                         const uint64_t x = tk64[m];
@@ -1436,8 +1442,12 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                             const uint32_t t2 = min(y0, y1);
                             within += t2 != kT16 && t2 > t ? (y0 != kT16 ? 1u : 0u) + (y1 != kT16 ? 1u : 0u) : 0u;
                         }
-                        emit(m, e, o0 + within);
+                        uint32_t p = o0 + within;
+                        if (e & 1u) lim[3u * p++ + 2u] = (unsigned long long)(2u * m) << 52;
+                        if (e & 2u) lim[3u * p + 2u] = (unsigned long long)(2u * m + 1u) << 52;
+                        cnt += __popc(e);
                     }
+                    for (uint32_t p = o0; p < o0 + cnt; ++p) tk16[2u * (uint32_t)(lim[3u * p + 2u] >> 52)] = (uint16_t)p;
                 }
             }
         }
@@ -1620,21 +1630,25 @@ hipError_t launch_ct_mul_fresh(const mul_fresh_args& a, const mul_fresh_args* ar
         if (L.total > 160u * 1024u) return hipErrorInvalidValue;
         // resident workgroups per CU as the runtime counts them (LDS granules, registers): the
         // grid is persistent, so a workgroup that is not resident would run after the others
-        static int occ_cache[2] = {-1, 0};   // {LDS bytes, blocks per CU}
-        if (occ_cache[0] != (int)L.total) {
+        // (cache keyed by the LDS size, shared by every context and thread: one atomic word
+        // {LDS bytes << 8 | blocks}, so a reader never sees half an update)
+        static std::atomic<uint64_t> occ_cache{0};
+        uint64_t oc = occ_cache.load(std::memory_order_relaxed);
+        if ((oc >> 8) != (uint64_t)L.total + 1u) {
             int nb = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ct_mul_fresh3<kF3Threads>, kF3Threads,
                                                               L.total) != hipSuccess || nb < 1)
                 nb = 1;
-            occ_cache[0] = (int)L.total;
-            occ_cache[1] = nb;
+            oc = (((uint64_t)L.total + 1u) << 8) | (uint64_t)std::min(nb, 255);
+            occ_cache.store(oc, std::memory_order_relaxed);
             if (std::getenv("PVAC_DEBUG_OCC"))
                 std::fprintf(stderr, "[pvac] k_ct_mul_fresh3: %u B LDS per workgroup, %d resident per CU\n", L.total, nb);
         }
+        const int occ_blocks = (int)(oc & 0xFFu);
         // the API counts LDS in 128-byte steps; measured residency (tools/res_probe.hip) follows
         // 2 KiB granules: 53,248 B gives 3 workgroups per CU, 53,888 B only 2
         const int lds_fit = (int)((160u * 1024u) / ((L.total + 2047u) & ~2047u));
-        int per_cu = std::min(std::min(occ_cache[1], lds_fit), 3);
+        int per_cu = std::min(std::min(occ_blocks, lds_fit), 3);
         if (const char* e = std::getenv("PVAC_FRESH_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
         uint64_t blocks = (uint64_t)num_cus * per_cu;
         if (blocks > a.A.n) blocks = a.A.n;

@@ -149,6 +149,8 @@ constexpr int kLP = 384;                 // products workgroup: one lane per out
 constexpr int kLPRows = 3;               // B <= kLP * kLPRows
 constexpr uint32_t kBmax = kLP * kLPRows;
 constexpr uint32_t kChunk = 128;         // sparse-side edges staged per round (chain steps: ~20)
+// one product per sparse edge goes into each lane's P and M column sets between col26_norm calls
+static_assert(kChunk <= kCol26MaxProducts, "col26 columns overflow: normalise more often");
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
 // dense mode: dl4[2][2B] (limbs 0-3, 16 B) | dx[2][2B] (limb 4, first-insert share) | sl4[kChunk]

@@ -80,6 +80,7 @@ struct pvac_hip_ctx {
     std::vector<large_desc> large_host;
     std::vector<large_desc> large_exec;
     uint32_t plan_stamp = 0;
+    uint64_t last_mul_pairs = 0;       // pairs of the last ct_mul_exec (pair_status is valid for these)
     uint64_t redo_total = 0;           // pairs re-run by redo_fresh_pairs since the context was created
     large_desc* desc_dev = nullptr;
     size_t desc_cap = 0;
@@ -401,7 +402,7 @@ int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* c, uint64_t* out) {
 int pvac_hip_ct_mul_status(pvac_hip_ctx* c, uint32_t* out, size_t n) {
     if (!c || (!out && n)) return fail(c, PVAC_EINVAL, "ct_mul_status: bad arguments");
     if (!n) return PVAC_OK;
-    if (n > c->pair_cap) return fail(c, PVAC_EINVAL, "ct_mul_status: more pairs than the last plan held");
+    if (n > c->last_mul_pairs) return fail(c, PVAC_EINVAL, "ct_mul_status: more pairs than the last ct_mul_exec held");
     const hipError_t e = hipMemcpyAsync(out, c->pair_status, n * 4, hipMemcpyDeviceToDevice, c->stream);
     return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "ct_mul_status");
 }
@@ -673,9 +674,14 @@ int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batc
     if (!rc) rc = run_large(c, A, B, nonces, C, flags, salt_pos);
     if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = hip_fail(c, hipErrorUnknown, "ct_mul_exec (redo)");
     c->large_host.swap(plan_set);
-    if (rc) return rc;
-    c->redo_total += cnt;
-    return c->large_host.empty() ? PVAC_OK : plan_static_groups(c);
+    if (!rc) {
+        c->redo_total += cnt;
+        // the plan's own static group tables were replaced by the redo set's: rebuild them
+        if (!c->large_host.empty()) rc = plan_static_groups(c);
+    }
+    // on failure the group tables may still belong to the redo set: no exec may reuse this plan
+    if (rc) ++c->plan_stamp;
+    return rc;
 }
 
 }  // namespace
@@ -690,6 +696,7 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         return fail(c, PVAC_EINVAL, "ct_mul_exec: plan is not this context's latest ct_mul plan");
     if (!nonces) return fail(c, PVAC_EINVAL, "ct_mul_exec: nonces required");
     if (!C->layers || !C->meta || !C->w_lo || !C->w_hi) return fail(c, PVAC_EINVAL, "ct_mul_exec: output arrays");
+    c->last_mul_pairs = 0;   // pair_status is valid again only once this exec has launched its kernels
     const bool with_sigma = (flags & PVAC_MUL_WITH_SIGMA) != 0;
     if (with_sigma && (!salts || !C->sigma || !c->H.ready))
         return fail(c, PVAC_EINVAL, "ct_mul_exec: WITH_SIGMA needs salts, C->sigma and H");
@@ -748,6 +755,7 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         int rc = redo_fresh_pairs(c, A, B, nonces, C, flags, salt_pos);
         if (rc) return rc;
     }
+    c->last_mul_pairs = A->n;
     if (with_sigma) {
         scoped_timer t(c, "sigma");
         hipError_t e = launch_sigma(c->H, c->prm, *C, salts, salt_pos, c->num_cus, c->stream);

@@ -236,6 +236,12 @@ class Oracle:
         lib.orc_ct_mul_batch_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 12 + \
             [C.c_int, u64p, u64p]
         lib.orc_ct_mul_batch_timed.restype = C.c_double
+        lib.orc_ct_mul_chain_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 6 + \
+            [C.c_int, C.c_int, u64p, u64p, u64p]
+        lib.orc_ct_mul_chain_timed.restype = C.c_double
+        lib.orc_ct_add_batch_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 12 + \
+            [C.c_int, C.c_int, u64p, u64p]
+        lib.orc_ct_add_batch_timed.restype = C.c_double
         lib.orc_prf_core.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_int, C.c_int, u64p]
         lib.orc_prf_R.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_int, u64p]
         lib.orc_prf_noise_delta.argtypes = [C.POINTER(OrcSecret)] + [C.c_uint64] * 4 + [C.c_uint32, C.c_uint32, u64p]

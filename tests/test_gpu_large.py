@@ -338,3 +338,93 @@ def test_engine_chain_depth8_vs_oracle(oracle):
             _same(out[p], ref, view=False)
         cur = [Cipher(o.layers, o.meta, o.w_lo, o.w_hi) for o in out]
     assert min(c.nE for c in cur) == 345088
+
+
+def test_enc_value_chain_depth8_vs_oracle(oracle):
+    """cfg 4 with its real producer: x_i = GPU enc_value(v_i) (38-40 edges, compact_edges-merged and
+    Fisher-Yates shuffled within each layer, ops/encrypt.hpp:162-291), then c_k = ct_mul(c_{k-1}, x_i)
+    to depth 8 with every step's input the engine's own DEVICE output (no host round trip, as in
+    bench.py), each step bit-exact vs the oracle (tests/test_main.cpp:289-295 restated)."""
+    import torch
+    from helpers import fixture_secret
+    from pvac_hfhe_cppbyv_amd import Engine
+    sk, man, em = fixture_secret()
+    eng = Engine(device=0, canon_tag=man["canon_tag"])
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    eng.set_powg(read_u64("powg_B.u64"))
+    rng = np.random.default_rng(0xC4A1)
+    n = 3
+    vals = rng.integers(0, 2**64, n, dtype=np.uint64)
+    X, st = eng.enc_value(vals, rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    xh = [Cipher(c.layers, c.meta, c.w_lo, c.w_hi) for c in X.to_host()]
+    assert all(38 <= c.nE <= 40 for c in xh)
+    cur_d, cur_h = X, xh
+    for k in range(1, 9):
+        Cb, plan = eng.ct_mul_plan(cur_d, X)
+        nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=eng.device)
+        eng.fill_random(nonces, 0xC4A0 + k)
+        out = eng.ct_mul(cur_d, X, nonces=nonces, C_=Cb, plan=plan)
+        assert eng.check_mul_gsum(cur_d, X, out, nonces) == 0
+        oh = out.to_host()
+        nz = nonces.cpu().numpy().view(np.uint64)
+        loff = Cb.l_off.cpu().numpy().view(np.uint64)
+        for p in range(n):
+            base = int(loff[p]) + cur_h[p].nL + xh[p].nL
+            per = nz[2 * base:2 * base + 2 * cur_h[p].nL * xh[p].nL]
+            ref = oracle.ct_mul(cur_h[p], xh[p], per, canon_tag=man["canon_tag"])
+            _same(oh[p], ref, view=False)
+        cur_d, cur_h = out, [Cipher(o.layers, o.meta, o.w_lo, o.w_hi) for o in oh]
+    assert min(c.nE for c in cur_h) > 300000
+
+
+def _bucket_census(x, y, nbk, B=337):
+    """Per libstdc++ bucket of ct_mul(x, y)'s key slots: (slots of the key space in the bucket, keys
+    with products). Returns the largest number of emitting keys among buckets of 4+ slots."""
+    G = 0x9E3779B97F4A7C15
+    LA, LB = len(x.layers), len(y.layers)
+    slots = np.arange(LA * LB * B, dtype=np.uint64)
+    keys = ((slots // np.uint64(B)) << np.uint64(32)) | (slots % np.uint64(B))
+    bk = (keys * np.uint64(G)) % np.uint64(nbk)   # u64 wrap-around multiply, as size_t
+    size = np.bincount(bk.astype(np.int64), minlength=nbk)
+    la = (x.meta & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    ia = ((x.meta >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64)
+    lb = (y.meta & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    ib = ((y.meta >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64)
+    present = np.unique(((la[:, None] * LB + lb[None, :]) * B + (ia[:, None] + ib[None, :]) % B).ravel())
+    pk = np.bincount(bk[present].astype(np.int64), minlength=nbk)
+    big = size >= 4
+    return int(pk[big].max()) if big.any() else 0
+
+
+def test_fresh_big_buckets_no_redo_vs_oracle(oracle):
+    """Buckets of 4+ key slots (the fresh kernel's member list, k_mul_fresh.hip P4) with several
+    emitting keys: every rank comes from unmodified first-insert times, so the fresh kernel emits
+    the reference order itself (no pair falls back to the general path) and matches the oracle.
+    The default fresh shape (20 edges per layer: 1,613 buckets) has no bucket of more than 3 slots;
+    23 edges per layer gives 2,116 products, 2,179 buckets and 156 key slots in buckets of 4-5."""
+    import torch
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0xB16)
+    n = 2048
+    A, B = eng.gen_fresh(n, 0xB160, 23), eng.gen_fresh(n, 0xB161, 23)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    assert plan.n_large == 0
+    nonces = torch.empty(2 * plan.total_layer_slots, dtype=torch.int64, device=eng.device)
+    eng.fill_random(nonces, 0xB162)
+    r0 = eng.ct_mul_redo_count()
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+    assert eng.ct_mul_redo_count() == r0
+    ha, hb = A.to_host(), B.to_host()
+    nz = nonces.cpu().numpy().view(np.uint64)
+    loff = Cb.l_off.cpu().numpy().view(np.uint64)
+    hit = 0
+    for p in range(0, n, 16):
+        x = Cipher(ha[p].layers, ha[p].meta, ha[p].w_lo, ha[p].w_hi)
+        y = Cipher(hb[p].layers, hb[p].meta, hb[p].w_lo, hb[p].w_hi)
+        hit += _bucket_census(x, y, oracle.bucket_count(x.nE * y.nE)) >= 2
+        base = int(loff[p]) + x.nL + y.nL
+        ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0xB16)
+        _same(out[p], ref, view=False)
+    assert hit >= 8   # the sampled pairs do exercise big buckets with several emitting keys

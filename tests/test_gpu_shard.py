@@ -28,36 +28,47 @@ def test_two_shards_equal_one_batch():
     assert l0 + l1 == l_all
 
 
-def _bench_json(args, world, port=None, backend="gloo", launcher=False):
-    import json
+def _bench_run(args, world, port=None, backend="gloo", launcher=False, shared=False):
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PVAC_BENCH_BACKEND=backend)
+    env.pop("PVAC_BENCH_ALLOW_SHARED", None)
+    if shared:   # the one-GPU rehearsal: ranks share cuda:0
+        env["PVAC_BENCH_ALLOW_SHARED"] = "1"
     if launcher:   # torch.distributed.run even for one rank: the process group and its collectives run
         env["PVAC_BENCH_DIST"] = "1"
-    if world == 1 and not launcher:
+    if not launcher:   # bench.py itself (at --gpus N > 1 it starts the N ranks)
         cmd = [sys.executable, os.path.join(root, "bench.py")] + args
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py")] + args
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+
+
+def _bench_json(args, world, port=None, backend="gloo", launcher=False, shared=False):
+    import json
+    p = _bench_run(args, world, port, backend, launcher, shared)
     assert p.returncode == 0, p.stderr[-3000:]
-    return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    js = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(js) == 1, p.stdout[-3000:]
+    return json.loads(js[0])
 
 
 def test_bench_world2_shard_digests_equal_one_gpu():
-    """bench.py's N>1 path on one GPU: two ranks (gloo for the gathers, both on cuda:0) each run
-    their shard of the global batch; rank 0 recomputes both ranks' pair windows from the global
-    indices, the gsum invariant holds on every pair, and the gathered digest equals a one-rank run
-    of the same 2 x 4096 pairs."""
-    from test_shard_dist import _free_port
+    """bench.py's N>1 path on one GPU: `bench.py --gpus 2` starts the two ranks itself (gloo for the
+    gathers, both on cuda:0 in the shared-device rehearsal); each runs its shard of the global
+    batch, rank 0 recomputes both ranks' pair windows from the global indices, the gsum invariant
+    holds on every pair, and the gathered digest equals a one-rank run of the same 2 x 4096 pairs.
+    The line counts ONE GPU for the two ranks."""
     common = ["--steps", "1", "--warmup", "0", "--no-cpu", "--no-extras", "--check-window", "512"]
-    two = _bench_json(["--gpus", "2", "--pairs", "4096"] + common, 2, _free_port())
+    two = _bench_json(["--gpus", "2", "--pairs", "4096"] + common, 2, shared=True)
     one = _bench_json(["--gpus", "1", "--pairs", "8192"] + common, 1)
     c2, c1 = two["checks"], one["checks"]
-    assert two["n_gpus"] == 2 and c2["shard_digests_ok"] and c2["shard_windows"]["ranks"] == 2
+    assert two["n_gpus"] == 1 and two["ranks"] == 2 and two["dist"] == {"world_size": 2, "backend": "gloo"}
+    assert one["n_gpus"] == 1 and one["ranks"] == 1
+    assert c2["shard_digests_ok"] and c2["shard_windows"]["ranks"] == 2
     assert c2["gsum_invariant"]["ok"] and c2["gsum_invariant"]["pairs"] == 8192
     assert c1["shard_digests_ok"] and c1["gsum_invariant"]["pairs"] == 8192
     assert c2["global_digest"] == c1["global_digest"]
@@ -80,3 +91,15 @@ def test_bench_rccl_one_rank_collectives():
     assert c["shard_digests_ok"] and c["gsum_invariant"]["ok"] and c["gsum_invariant"]["pairs"] == 4096
     assert c["global_digest"] == c0["global_digest"]
     assert c["global_output_edges"] == c0["global_output_edges"]
+
+
+def test_bench_gpus2_on_one_gpu_fails_loudly():
+    """Without the rehearsal switch, `bench.py --gpus N` with fewer than N GPUs stops before any
+    GPU work with a clear message instead of reporting N GPUs."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    p = _bench_run(["--gpus", "2", "--pairs", "4096", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-extras"], 2)
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "distinct visible GPUs" in p.stderr
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]

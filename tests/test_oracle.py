@@ -227,3 +227,65 @@ def test_ct_reader_roundtrip_seed3():
     assert len(cts) == 9
     with open(path, "rb") as f:
         assert write_ct(cts) == f.read()
+
+
+def _pack(cs):
+    lc = np.array([c.nL for c in cs], np.uint64)
+    ec = np.array([c.nE for c in cs], np.uint64)
+    lo = np.concatenate([[0], np.cumsum(lc)]).astype(np.uint64)
+    eo = np.concatenate([[0], np.cumsum(ec)]).astype(np.uint64)
+    cat = lambda f: np.ascontiguousarray(np.concatenate([getattr(c, f) for c in cs]).astype(np.uint64))
+    return lo, np.ascontiguousarray(np.concatenate([c.layers for c in cs])), eo, cat("meta"), cat("w_lo"), cat("w_hi")
+
+
+def _fnv(c):
+    h = 0xcbf29ce484222325
+    for m, lo, hi in zip(c.meta, c.w_lo, c.w_hi):
+        for x in (int(m), int(lo), int(hi)):
+            for i in range(8):
+                h = ((h ^ ((x >> (8 * i)) & 0xFF)) * 0x100000001b3) & (2**64 - 1)
+    return h
+
+
+def test_chain_timed_equals_stepwise_ct_mul(oracle):
+    """The cfg-4 CPU baseline (orc_ct_mul_chain_timed, bench.py extras.cfg4_chain.cpu_baseline) is
+    the same chain as ct_mul step by step on the reference's own enc_value outputs, on 1 and 3
+    threads: final edge digests and per-step edge totals."""
+    import ctypes as C
+    from helpers import default_params
+    xs = [read_ct(os.path.join(REF, f"enc{i}.ct"))[0] for i in range(3)]
+    depth = 3
+    ref_d, ref_steps = [], np.zeros(depth, np.uint64)
+    for x in xs:
+        c = x
+        for d in range(depth):
+            c = oracle.ct_mul(c, x, np.zeros(2 * c.nL * x.nL, np.uint64), canon_tag=0x5EED0003)
+            ref_steps[d] += c.nE
+        ref_d.append(_fnv(c))
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    packed = _pack(xs)
+    prm = default_params(0x5EED0003)
+    for th in (1, 3):
+        cnt, dig, se = np.zeros(3, np.uint64), np.zeros(3, np.uint64), np.zeros(depth, np.uint64)
+        oracle.lib.orc_ct_mul_chain_timed(C.byref(prm), 3, *(P_(a) for a in packed), depth, th, P_(cnt), P_(dig), P_(se))
+        assert [int(v) for v in dig] == ref_d
+        assert np.array_equal(se, ref_steps)
+
+
+def test_add_batch_timed_equals_ct_add(oracle):
+    """bench.py's ct_add / ct_sub CPU baseline (orc_ct_add_batch_timed) reproduces the reference's
+    own ct_add / ct_sub outputs of the eight fixture pairs (edge digests and counts)."""
+    import ctypes as C
+    from helpers import default_params
+    xs = [read_ct(os.path.join(REF, f"pair{p}_x.ct"))[0] for p in range(8)]
+    ys = [read_ct(os.path.join(REF, f"pair{p}_y.ct"))[0] for p in range(8)]
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    a, b = _pack(xs), _pack(ys)
+    prm = default_params(0)
+    for neg, name in ((0, "add"), (1, "sub")):
+        refs = [read_ct(os.path.join(REF, f"pair{p}_{name}.ct"))[0] for p in range(8)]
+        cnt, dig = np.zeros(8, np.uint64), np.zeros(8, np.uint64)
+        oracle.lib.orc_ct_add_batch_timed(C.byref(prm), 8, *(P_(x) for x in a), *(P_(x) for x in b), neg, 2,
+                                          P_(cnt), P_(dig))
+        assert [int(v) for v in cnt] == [r.nE for r in refs]
+        assert [int(v) for v in dig] == [_fnv(r) for r in refs]
