@@ -350,6 +350,7 @@ def test_enc_value_chain_depth8_vs_oracle(oracle):
     from pvac_hfhe_cppbyv_amd import Engine
     sk, man, em = fixture_secret()
     eng = Engine(device=0, canon_tag=man["canon_tag"])
+    assert eng.gen_H().hex() == man["H_digest"]
     eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
                    em["lpn_tau_den"])
     eng.set_powg(read_u64("powg_B.u64"))
