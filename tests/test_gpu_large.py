@@ -404,12 +404,13 @@ def test_fresh_big_buckets_no_redo_vs_oracle(oracle):
     emitting keys: every rank comes from unmodified first-insert times, so the fresh kernel emits
     the reference order itself (no pair falls back to the general path) and matches the oracle.
     The default fresh shape (20 edges per layer: 1,613 buckets) has no bucket of more than 3 slots;
-    23 edges per layer gives 2,116 products, 2,179 buckets and 156 key slots in buckets of 4-5."""
+    16 x 20 edges per layer (32 x 40 edges) gives 1,280 products, 1,289 buckets and 92 key slots
+    in buckets of 4 (all held in the kernel's member list)."""
     import torch
     from pvac_hfhe_cppbyv_amd import Engine
     eng = Engine(device=0, canon_tag=0xB16)
     n = 2048
-    A, B = eng.gen_fresh(n, 0xB160, 23), eng.gen_fresh(n, 0xB161, 23)
+    A, B = eng.gen_fresh(n, 0xB160, 16), eng.gen_fresh(n, 0xB161, 20)
     Cb, plan = eng.ct_mul_plan(A, B)
     assert plan.n_large == 0
     nonces = torch.empty(2 * plan.total_layer_slots, dtype=torch.int64, device=eng.device)
