@@ -7,7 +7,13 @@ so the read side is doubled (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is ta
 No cycles-per-instruction constant: the VALU roofline divides SQ_INSTS_VALU per launch by the kernel
 time and by the ceiling measured on the device (pvac_hip_alu_ceiling, bench.py roofline.valu).
 lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / (256 CUs x kernel cycles), wait_frac =
-SQ_WAIT_ANY / SQ_WAVE_CYCLES."""
+SQ_WAIT_ANY / SQ_WAVE_CYCLES.
+
+Full-size dispatches only: a bench run launches the headline kernel on the whole batch (warm-up +
+timed steps) and once more on the self-check window (4,096 pairs) with the SAME persistent grid, so
+the grid size cannot tell them apart. Each pass keeps the dispatches whose duration is at least half
+of that pass's longest one (the round-2 summaries averaged all four dispatches equally, which
+scaled every per-launch figure by ~3/4). `dispatches` records how many were kept and dropped."""
 import csv
 import glob
 import json
@@ -18,6 +24,7 @@ from collections import defaultdict
 
 def main(root):
     acc = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(dict)   # (kernel, pass file) -> {dispatch: ns}
     for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
@@ -26,16 +33,32 @@ def main(root):
                 name = row.get("Counter_Name")
                 try:
                     v = float(row.get("Counter_Value", "nan"))
+                    ns = float(row.get("End_Timestamp", 0)) - float(row.get("Start_Timestamp", 0))
                 except ValueError:
                     continue
-                acc[short][(name, row.get("Dispatch_Id"))].append(v)
+                disp = (path, row.get("Dispatch_Id"))
+                acc[short][(name, disp)].append(v)
+                dur[(short, path)][disp] = ns
     out = {}
     for kern, d in acc.items():
+        keep, dropped = set(), 0
+        for (k2, _path), dd in dur.items():
+            if k2 != kern or not dd:
+                continue
+            top = max(dd.values())
+            for disp, ns in dd.items():
+                if ns >= 0.5 * top:
+                    keep.add(disp)
+                else:
+                    dropped += 1
         per = defaultdict(list)
-        for (name, _disp), vals in d.items():
-            per[name].append(sum(vals))   # sum over XCD/SE dimensions of one dispatch
+        for (name, disp), vals in d.items():
+            if disp in keep:
+                per[name].append(sum(vals))   # sum over XCD/SE dimensions of one dispatch
         out[kern] = {n: sum(v) / len(v) for n, v in per.items()}
         m = out[kern]
+        m["dispatches"] = {"kept_per_pass": max((len(v) for v in per.values()), default=0),
+                           "dropped_short": dropped}
         if "FETCH_SIZE" in m:
             m["hbm_read_bytes_corrected"] = 2 * m["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in m:

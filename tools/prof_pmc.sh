@@ -9,7 +9,7 @@ cd "$ROOT"
 export TMPDIR=/tmp
 KRE="${1:-k_ct_mul}"
 shift || true
-OUT="$ROOT/gpurun_out/pmc"
+OUT="${PMC_OUT:-$ROOT/gpurun_out/pmc}"
 mkdir -p "$OUT"
 BENCH=(python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu --no-extras "$@")
 if [ "${PMC_SET:-}" = "cache" ]; then
@@ -68,5 +68,6 @@ if k and "hbm_bytes_per_launch" in k:
                "lds_bank_conflict_frac": k.get("lds_bank_conflict_frac"), "wait_frac": k.get("wait_frac"),
                "kernel_cycles": k.get("kernel_cycles"),
                "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) / WRITE_SIZE, "
-                         "mean per dispatch; tools/prof_pmc.sh"}, open(sys.argv[2], "w"), indent=1)
+                         "mean per full-batch dispatch (the self-check window launch excluded); tools/prof_pmc.sh",
+               "dispatches": k.get("dispatches")}, open(sys.argv[2], "w"), indent=1)
 PY
