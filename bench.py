@@ -333,18 +333,20 @@ def main():
     # the integer-ALU roofline of the same kernel: VALU wave-instructions per second (PMC count per
     # launch / HIP-event kernel time) against the ceiling measured now on this GPU (k_ubench.hip)
     try:
-        ceil_w = eng.alu_ceiling(0)
+        ceil_w = eng.alu_ceiling(4)
+        ceil_mix = eng.alu_ceiling(0)
     except Exception:
-        ceil_w = None
+        ceil_w = ceil_mix = None
     vi = pm.get("valu_insts_per_launch")
     if ceil_w and vi and avg_kernel_ms > 0:
         ach = vi / (avg_kernel_ms / 1000.0)
         result["roofline"]["valu"] = {
             "achieved": ach, "peak": ceil_w, "unit": "wave64 VALU inst/s", "frac": ach / ceil_w,
             "insts_per_pair": vi / n, "lds_bank_conflict_frac": pm.get("lds_bank_conflict_frac"),
-            "source": "SQ_INSTS_VALU per launch (profiles/pmc_ct_mul_fresh.json) / kernel time; peak: "
-                      "pvac_hip_alu_ceiling(0), a v_mad_u64_u32 / v_add_co_u32 / v_alignbit_b32 probe "
-                      "at 8 waves per SIMD on this GPU"}
+            "mad_mix_ceiling": ceil_mix,
+            "source": "SQ_INSTS_VALU per full-batch launch (profiles/pmc_ct_mul_fresh.json) / kernel time; peak: "
+                      "pvac_hip_alu_ceiling(4), independent 32-bit v_add_u32 / v_xor_b32 / v_alignbit_b32 "
+                      "at 8 waves per SIMD on this GPU (the kind-0 v_mad_u64_u32 mix beside it)"}
     elif ceil_w:
         result["roofline"]["valu"] = {"peak": ceil_w, "unit": "wave64 VALU inst/s", "achieved": None,
                                       "note": "no PMC summary for this kernel / batch in profiles/"}

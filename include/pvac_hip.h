@@ -127,7 +127,9 @@ int pvac_hip_ctx_gen_H(pvac_hip_ctx* ctx, uint8_t digest_out[32]);
 /* Measured integer-ALU ceilings of this device for the roofline report (k_ubench.hip), per second:
  * kind 0 = wave64 integer VALU instructions (v_mad_u64_u32 / v_add_co_u32 / v_alignbit_b32 mix),
  * 1 = lazy fp_mul_fold1 products, 2 = full fp_mul products, 3 = column-accumulated products
- * (col26_mac, the general path's dense loop). Synchronous. */
+ * (col26_mac, the general path's dense loop), 4 = wave64 single-pass 32-bit VALU instructions
+ * (v_add_u32 / v_xor_b32 / v_alignbit_b32: the issue ceiling of a mostly 32-bit VALU stream).
+ * Synchronous. */
 int pvac_hip_alu_ceiling(pvac_hip_ctx* ctx, int kind, double* per_s);
 /* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */
 int pvac_hip_timing_enable(pvac_hip_ctx* ctx, int on);

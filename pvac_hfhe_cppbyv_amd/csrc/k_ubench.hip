@@ -65,6 +65,53 @@ __global__ __launch_bounds__(kUB) void k_probe_valu(uint64_t* out, uint32_t iter
     out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
 }
 
+// single-pass 32-bit VALU issue: 24 independent v_add_u32 / v_xor_b32 / v_alignbit_b32 per iteration
+// (kind 4). The bound for a kernel whose VALU stream is mostly 32-bit (the fresh ct_mul kernel):
+// the kind-0 mix above carries v_mad_u64_u32, which issues slower than a 32-bit op.
+__global__ __launch_bounds__(kUB) void k_probe_valu32(uint64_t* out, uint32_t iters, uint32_t seed) {
+    const uint32_t a = threadIdx.x ^ seed, b = a * 2654435761u + 1u;
+    uint32_t y[8], z[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        y[k] = a * (k + 3);
+        z[k] = b ^ (k * 0x9E3779B9u);
+    }
+    for (uint32_t i = 0; i < iters; ++i) {
+        asm volatile(
+            "v_add_u32 %0, %0, %16\n\t"
+            "v_add_u32 %1, %1, %16\n\t"
+            "v_add_u32 %2, %2, %16\n\t"
+            "v_add_u32 %3, %3, %16\n\t"
+            "v_add_u32 %4, %4, %17\n\t"
+            "v_add_u32 %5, %5, %17\n\t"
+            "v_add_u32 %6, %6, %17\n\t"
+            "v_add_u32 %7, %7, %17\n\t"
+            "v_xor_b32 %8, %8, %0\n\t"
+            "v_xor_b32 %9, %9, %1\n\t"
+            "v_xor_b32 %10, %10, %2\n\t"
+            "v_xor_b32 %11, %11, %3\n\t"
+            "v_xor_b32 %12, %12, %4\n\t"
+            "v_xor_b32 %13, %13, %5\n\t"
+            "v_xor_b32 %14, %14, %6\n\t"
+            "v_xor_b32 %15, %15, %7\n\t"
+            "v_alignbit_b32 %0, %8, %0, 7\n\t"
+            "v_alignbit_b32 %1, %9, %1, 7\n\t"
+            "v_alignbit_b32 %2, %10, %2, 7\n\t"
+            "v_alignbit_b32 %3, %11, %3, 7\n\t"
+            "v_alignbit_b32 %4, %12, %4, 7\n\t"
+            "v_alignbit_b32 %5, %13, %5, 7\n\t"
+            "v_alignbit_b32 %6, %14, %6, 7\n\t"
+            "v_alignbit_b32 %7, %15, %7, 7"
+            : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7]),
+              "+v"(z[0]), "+v"(z[1]), "+v"(z[2]), "+v"(z[3]), "+v"(z[4]), "+v"(z[5]), "+v"(z[6]), "+v"(z[7])
+            : "v"(a), "v"(b));
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r ^= (uint64_t)y[k] << 32 | z[k];
+    out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
+}
+
 template <bool FULL>
 __global__ __launch_bounds__(kUB) void k_probe_mul(uint64_t* out, uint32_t iters, uint32_t seed) {
     const uint64_t s = ((uint64_t)(threadIdx.x ^ seed) << 17) | blockIdx.x;
@@ -126,13 +173,16 @@ hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s) {
     hipEvent_t t0, t1;
     hipEventCreate(&t0);
     hipEventCreate(&t1);
-    const uint32_t iters = kind == 0 ? 4096u : 512u;
+    const uint32_t iters = kind == 0 || kind == 4 ? 4096u : 512u;
     double ops = 0;
     float ms = 0;
     for (int rep = 0; rep < 2; ++rep) {   // the first launch warms clocks and code
         hipEventRecord(t0, st);
         if (kind == 0) {
             hipLaunchKernelGGL(k_probe_valu, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
+            ops = (double)blocks * (kUB / 64) * iters * 24.0;   // wave64 instructions
+        } else if (kind == 4) {
+            hipLaunchKernelGGL(k_probe_valu32, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
             ops = (double)blocks * (kUB / 64) * iters * 24.0;   // wave64 instructions
         } else if (kind == 1) {
             hipLaunchKernelGGL(k_probe_mul<false>, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
