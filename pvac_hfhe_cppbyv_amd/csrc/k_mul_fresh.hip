@@ -1392,15 +1392,18 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         const uint64_t ceo = cur.ceo;
         for (int rep_ = 0; rep_ < PVAC_REP_P4; ++rep_) {   // experiment builds only (tools/exp_fresh3.py)
         {
+            // 32-bit LDS byte offsets (no 64-bit address arithmetic): a cell word's low half, limb 2
+            // of a position
+            const uint32_t tkb = Ls.tkey, lmb = Ls.lim + 16u;
             auto emit = [&](uint32_t m, uint32_t e, uint32_t p) {   // slot m's cells at p (P), p + (P present) (M)
                 if (e & 1u) {
-                    tk16[4u * m] = (uint16_t)p;
-                    lim[3u * p + 2u] = (unsigned long long)(2u * m) << 52;
+                    *(uint16_t*)(lds + (tkb + 8u * m)) = (uint16_t)p;
+                    *(unsigned long long*)(lds + (lmb + 24u * p)) = (unsigned long long)(2u * m) << 52;
                     ++p;
                 }
                 if (e & 2u) {
-                    tk16[4u * m + 2u] = (uint16_t)p;
-                    lim[3u * p + 2u] = (unsigned long long)(2u * m + 1u) << 52;
+                    *(uint16_t*)(lds + (tkb + 8u * m + 4u)) = (uint16_t)p;
+                    *(unsigned long long*)(lds + (lmb + 24u * p)) = (unsigned long long)(2u * m + 1u) << 52;
                 }
             };
             // emit offset of bucket time tb: in-segment suffix offset + segment offset (from lane

@@ -16,6 +16,7 @@ from pvac_hfhe_cppbyv_amd import Engine, load_library  # noqa: E402
 def main():
     n = 1 << 20
     res = {}
+    ref = None
     for path in sys.argv[1:]:
         lib = load_library(path)
         eng = Engine(device=0, canon_tag=0x5EED0003, lib=lib)
@@ -33,7 +34,16 @@ def main():
         eng.timing(False)
         ms, k = eng.timing_get("ct_mul_fresh")
         res[os.path.basename(path)] = round(ms / max(k, 1), 3)
-        print(os.path.basename(path), res[os.path.basename(path)], flush=True)
+        # outputs vs the first library's (the product): a variant must be bit-exact
+        out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+        dig = eng.digest(out).cpu()
+        if ref is None:
+            ref = dig
+        same = bool(torch.equal(dig, ref))
+        res[os.path.basename(path) + ":same_as_first"] = same
+        res[os.path.basename(path) + ":redo"] = eng.ct_mul_redo_count()
+        print(os.path.basename(path), res[os.path.basename(path)], "same" if same else "DIFFERENT", flush=True)
+        del out, dig
         del A, B, Cb, plan, nonces, eng
         torch.cuda.empty_cache()
     print(json.dumps(res))

@@ -32,3 +32,10 @@ for d in sorted(glob.glob(os.path.join(out, "libpvac_hip*"))):
     print(b, "ms", times.get(b + ".so"), "VALU/pair %.0f" % (m.get("SQ_INSTS_VALU", 0) / 2**20),
           "LDS/pair %.0f" % (m.get("SQ_INSTS_LDS", 0) / 2**20))
 PY
+# the issue ceilings of this GPU beside the phase costs (kind 4: 32-bit VALU, kind 0: the mad mix)
+python3 -c "
+import sys; sys.path.insert(0, '$ROOT')
+from pvac_hfhe_cppbyv_amd import Engine
+e = Engine(device=0)
+print('valu32 ceiling %.4g/s, mad-mix ceiling %.4g/s' % (e.alu_ceiling(4), e.alu_ceiling(0)))
+"
