@@ -239,13 +239,6 @@ hipError_t launch_add_merge(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac
 constexpr uint32_t kLargeLayersMax = 16384;   // |A.L| + |B.L| + |A.L||B.L| handled in LDS
 constexpr uint32_t kLargeDenseMin = 48;       // dense-owner product mode from this many edges
 
-// general path: k_large_order writes the edges itself (1) or fills an order array that a separate
-// coalesced writer gathers (0, A/B builds: -DPVAC_LARGE_FUSED_WRITE=0 on every object)
-#ifndef PVAC_LARGE_FUSED_WRITE
-#define PVAC_LARGE_FUSED_WRITE 1
-#endif
-constexpr bool kLargeFusedWrite = PVAC_LARGE_FUSED_WRITE != 0;
-
 struct large_desc {
     uint64_t pair;               // index of the pair in the batch
     uint64_t n;                  // |A.E| * |B.E|  (< 2^32)

@@ -621,11 +621,6 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     uint32_t* order = S + d.o_order;
     uint32_t* hpos = S + d.o_hpos;
     const uint32_t* ghead = group_heads(g, d);
-    const uint32_t base = d.LA + d.LB;
-    const uint64_t ceo = g.C.e_off[pr];
-    const uint32_t* remap = S + d.o_used;
-    const ulonglong2* sums = (const ulonglong2*)(S + d.o_sums);
-    (void)order; (void)hpos; (void)base; (void)ceo; (void)remap; (void)sums;
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
         const uint32_t ts = tkey[s];
         if (ts == kInf) continue;
@@ -653,29 +648,6 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
             hp += etot[s2];
         }
         const uint32_t p = canonical ? cpos[s] : hp;
-#if PVAC_LARGE_FUSED_WRITE
-        // the key's edges go straight to their positions: its sums are read here in slot order
-        // (coalesced) and the edges scattered inside the pair's output, instead of an order array
-        // scattered here and a gather of the sums by a separate writer
-        const uint32_t lp = (uint32_t)(s / Bm), r = (uint32_t)(s - (uint64_t)lp * Bm);
-        const uint32_t lid = remap[base + lp];
-        const ulonglong2* sm = sums + 2 * s;
-        if (eb & 1u) {
-            const ulonglong2 w = sm[0];
-            g.C.meta[ceo + p] = make_meta(lid, r, 0u);
-            g.C.w_lo[ceo + p] = w.x;
-            g.C.w_hi[ceo + p] = w.y;
-            if (g.salt_pos) g.salt_pos[ceo + p] = hp;   // hash-order index (== p unless canonical)
-        }
-        if (eb & 2u) {
-            const uint32_t o = eb & 1u;
-            const ulonglong2 w = sm[1];
-            g.C.meta[ceo + p + o] = make_meta(lid, r, 1u);
-            g.C.w_lo[ceo + p + o] = w.x;
-            g.C.w_hi[ceo + p + o] = w.y;
-            if (g.salt_pos) g.salt_pos[ceo + p + o] = hp + o;
-        }
-#else
         const uint32_t s32 = (uint32_t)s;
         if (eb & 1u) {
             order[p] = s32 << 1;
@@ -686,7 +658,6 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
             order[p + o] = (s32 << 1) | 1u;
             if (canonical) hpos[p + o] = hp + o;
         }
-#endif
     }
 }
 
@@ -776,9 +747,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     hipLaunchKernelGGL(k_large_rank, dim3(gs, nl), dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_scan, dim3(nl), dim3(kLBig), 0, st, a);
     hipLaunchKernelGGL(k_large_order, dim3(gs, nl), dim3(kLB), 0, st, a);
-#if !PVAC_LARGE_FUSED_WRITE
     hipLaunchKernelGGL(k_large_write, dim3(grid_x(a.max_capE, kLB * 2, 4096), nl), dim3(kLB), 0, st, a);
-#endif
     return hipGetLastError();
 }
 

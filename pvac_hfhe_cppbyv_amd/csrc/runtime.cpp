@@ -277,9 +277,8 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.o_within = o; o += d.S;
     d.o_etot = o; o += d.S;
     d.o_cpos = o; o += d.S;
-    // the order array and canonical hash positions exist only for the separate writer
-    d.o_order = o; o += kLargeFusedWrite ? 0 : d.capE;
-    d.o_hpos = o; o += kLargeFusedWrite ? 0 : d.capE;
+    d.o_order = o; o += d.capE;
+    d.o_hpos = o; o += d.capE;
     quad();
     d.words = o;
     return PVAC_OK;
