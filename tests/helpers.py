@@ -394,3 +394,24 @@ def R_for(cipher: Cipher, R_inputs):
         if L["rule"] == 0:
             R[2 * i:2 * i + 2] = table[(int(L["ztag"]), int(L["nonce_lo"]), int(L["nonce_hi"]))]
     return R
+
+
+def pack_device_batch(X, k):
+    """The first k ciphers of an engine DeviceBatch (capacity-padded CSR allowed) as host arrays in
+    the oracle's packed layout (orc_ct_mul_batch_timed): offsets with k + 1 entries, layer records,
+    meta, w_lo, w_hi."""
+    import torch
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+
+    def rows(off, cnt):
+        cnt = cnt.to(torch.int64)
+        idx = torch.repeat_interleave(off.to(torch.int64) - (torch.cumsum(cnt, 0) - cnt), cnt)
+        packed = torch.zeros(k + 1, dtype=torch.int64, device=cnt.device)
+        packed[1:] = torch.cumsum(cnt, 0)
+        return idx + torch.arange(idx.numel(), device=idx.device), packed
+
+    li, lo = rows(X.l_off[:k], X.l_cnt[:k])
+    ei, eo = rows(X.e_off[:k], X.e_cnt[:k])
+    cs = np.ascontiguousarray
+    return (cs(u(lo)), cs(X.layers[li].cpu().numpy()), cs(u(eo)), cs(u(X.meta[ei])), cs(u(X.w_lo[ei])),
+            cs(u(X.w_hi[ei])))

@@ -430,3 +430,38 @@ def test_fresh_big_buckets_no_redo_vs_oracle(oracle):
         ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0xB16)
         _same(out[p], ref, view=False)
     assert hit >= 8   # the sampled pairs do exercise big buckets with several emitting keys
+
+
+def test_enc_value_chains_depth8_digests_vs_oracle(oracle):
+    """cfg 4's workload on 64 GPU enc_value inputs at once: c_k = ct_mul(c_{k-1}, x) to depth 8 on
+    the device, every final chain's edges (per-chain FNV-1a digest over meta and w) and edge count
+    equal to the pinned CPU port's chain on the same inputs (orc_ct_mul_chain_timed, 16 threads)."""
+    import ctypes as C
+    import torch
+    from helpers import default_params, fixture_secret, pack_device_batch
+    from pvac_hfhe_cppbyv_amd import Engine
+    sk, man, em = fixture_secret()
+    eng = Engine(device=0, canon_tag=man["canon_tag"])
+    assert eng.gen_H().hex() == man["H_digest"]
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    rng = np.random.default_rng(0xC4A2)
+    n, depth = 64, 8
+    X, st = eng.enc_value(rng.integers(0, 2**64, n, dtype=np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    cur = X
+    for k in range(depth):
+        Cb, plan = eng.ct_mul_plan(cur, X)
+        nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=eng.device)
+        eng.fill_random(nonces, 0xC4B0 + k)
+        cur = eng.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
+    gdig = eng.digest(cur).cpu().numpy().view(np.uint64)
+    gcnt = cur.e_cnt[:n].cpu().numpy().view(np.uint64)
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    px = pack_device_batch(X, n)
+    cnt, dig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
+    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(man["canon_tag"])), n, *(P_(a) for a in px), depth, 16,
+                                      P_(cnt), P_(dig), P_(se))
+    assert np.array_equal(cnt, gcnt)
+    assert np.array_equal(dig, gdig)
+    assert int(se[-1]) == int(gcnt.sum()) and gcnt.min() > 300000

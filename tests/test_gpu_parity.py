@@ -474,7 +474,8 @@ def _pair_host(X, p):
 
 def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     """BASELINE cfg 3 at its full size (2^20 fresh-shaped pairs, the bench's batch and generator):
-    every reported output slot written by this launch (sentinel-filled outputs), the reference's
+    every reported output slot written by this launch (sentinel-filled outputs), every pair's
+    edges equal to the pinned CPU port's (per-pair digests, all 2^20), the reference's
     gsum invariant on every pair, 512 pairs spread over the whole batch bit-exact
     vs the oracle (weights, emit order, layers incl. ztags), every pair within its planned capacity
     with status 0, and a second run of the same batch identical (per-pair device digests)."""
@@ -501,6 +502,19 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     cap = np.diff(np.append(eoff, np.uint64(plan.total_edge_slots)))
     assert (ecnt <= cap).all() and ecnt.min() > 0
     dig1 = u(eng.digest(out)[:n]).copy()
+    # EVERY pair's edges (meta, w in emit order) against the pinned CPU port, by per-pair FNV-1a
+    # digest: the oracle runs the reference's unordered_map aggregation on 16 threads
+    import ctypes as C
+    from helpers import default_params, pack_device_batch
+    P_ = lambda x: x.ctypes.data_as(C.c_void_p)
+    pa, pb = pack_device_batch(A, n), pack_device_batch(B, n)
+    cnt, dig = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    oracle.lib.orc_ct_mul_batch_timed(C.byref(default_params(0x5EED0003)), n, *(P_(x) for x in pa), *(P_(x) for x in pb),
+                                      16, P_(cnt), P_(dig))
+    assert np.array_equal(cnt, ecnt)
+    bad = np.nonzero(dig != dig1)[0]
+    assert bad.size == 0, f"{bad.size} pairs differ from the oracle, first {bad[:8]}"
+    del pa, pb
     # the reference's gsum invariant (utils/metrics.hpp:88-113) on every one of the 2^20 pairs
     eng.set_powg(read_u64("powg_B.u64"))
     assert eng.check_mul_gsum(A, B, out, nonces) == 0
