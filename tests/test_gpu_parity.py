@@ -208,7 +208,10 @@ def test_ct_mul_synthetic_vs_oracle(engine, oracle):
         Cb, plan = eng.ct_mul_plan(A, B)
         nonces = eng.torch.empty(2 * plan.total_layer_slots, dtype=eng.torch.int64, device=eng.device)
         eng.fill_random(nonces, 77)
+        r0 = eng.ct_mul_redo_count()
         out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+        if epl != 1:   # (1 edge per layer: 1,348 key slots in 5 buckets, beyond the member list)
+            assert eng.ct_mul_redo_count() == r0, "ordinary fresh pairs fell back to the general path"
         ha, hb = A.to_host(), B.to_host()
         nz = nonces.cpu().numpy().view(np.uint64)
         loff = Cb.l_off.cpu().numpy().view(np.uint64)
@@ -240,7 +243,7 @@ def test_ct_mul_full_range_golden(engine):
     nonces = _nonce_buffer(eng, Cb, xs, ys, streams)
     redo0 = eng.ct_mul_redo_count()
     out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
-    assert eng.ct_mul_redo_count() - redo0 >= 2   # cases 2 (zero weights) and 3 (cancelling keys)
+    assert eng.ct_mul_redo_count() - redo0 == 2   # exactly cases 2 (zero weights) and 3 (cancelling keys)
     for k in ks:
         _assert_same(out[k], read_ct(os.path.join(REF, f"fr{k}_mul_w.ct"))[0])
         full = read_layers_u64(f"fr{k}_mul_layers.u64")
