@@ -445,6 +445,7 @@ def test_enc_value_chains_depth8_digests_vs_oracle(oracle):
     assert eng.gen_H().hex() == man["H_digest"]
     eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
                    em["lpn_tau_den"])
+    eng.set_powg(read_u64("powg_B.u64"))
     rng = np.random.default_rng(0xC4A2)
     n, depth = 64, 8
     X, st = eng.enc_value(rng.integers(0, 2**64, n, dtype=np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
