@@ -11,6 +11,8 @@
 //   pvac::ct_add(pk, A, B)  (ops/arithmetic.hpp:12)  -> pvac_hip::ct_add(pk, A, B)
 //   pvac::ct_sub(pk, A, B)  (ops/arithmetic.hpp:43)  -> pvac_hip::ct_sub(pk, A, B)
 //   pvac::ct_scale(pk, A,s) (ops/arithmetic.hpp:33)  -> pvac_hip::ct_scale(pk, A, s)
+//   pvac::ct_neg(pk, A)     (ops/arithmetic.hpp:39)  -> pvac_hip::ct_neg(pk, A)
+//   pvac::ct_div_const(pk, A, k) (ops/arithmetic.hpp:108) -> pvac_hip::ct_div_const(pk, A, k)
 //   pvac::enc_value(pk, sk, v) (ops/encrypt.hpp:289)  -> pvac_hip::enc_value<Cipher>(pk, sk, v)
 //   pvac::dec_value(pk, sk, C) (ops/decrypt.hpp:62)  -> pvac_hip::dec_value(pk, sk, C)
 //   saveCts / loadCts          (tests/add.cpp:22-155) -> pvac_hip::save_cts_bytes / load_cts_bytes
@@ -387,7 +389,7 @@ public:
         for (auto& x : d) x.alloc(n);
         d[0].upload(a_lo, n, stream_); d[1].upload(a_hi, n, stream_);
         const size_t nb = op == PVAC_FP_SCALE ? 1 : n;
-        if (op != PVAC_FP_NEG) { d[2].upload(b_lo, nb, stream_); d[3].upload(b_hi, nb, stream_); }
+        if (op != PVAC_FP_NEG && op != PVAC_FP_INV) { d[2].upload(b_lo, nb, stream_); d[3].upload(b_hi, nb, stream_); }
         check(pvac_hip_fp_binop(ctx_, op, d[0].p, d[1].p, d[2].p, d[3].p, d[4].p, d[5].p, n));
         d[4].download(c_lo, n, stream_); d[5].download(c_hi, n, stream_);
         detail::hip_ok(hipStreamSynchronize(stream_), "sync");
@@ -575,6 +577,28 @@ CipherT ct_scale(const PubKeyT& pk, const CipherT& A, const FpT& s) {
     engine_for(pk).fp_binop(PVAC_FP_SCALE, lo.data(), hi.data(), slo.data(), shi.data(), lo.data(), hi.data(), n);
     for (size_t i = 0; i < n; ++i) { C.E[i].w.lo = lo[i]; C.E[i].w.hi = hi[i]; }
     return C;
+}
+
+// ct_neg (ops/arithmetic.hpp:39-41): ct_scale by fp_neg(fp_from_u64(1)) = p - 1.
+template <class PubKeyT, class CipherT>
+CipherT ct_neg(const PubKeyT& pk, const CipherT& A) {
+    std::decay_t<decltype(A.E[0].w)> s{};
+    s.lo = ~0ull - 1;
+    s.hi = 0x7FFFFFFFFFFFFFFFull;
+    return ct_scale(pk, A, s);
+}
+
+// ct_div_const (ops/arithmetic.hpp:108-110): ct_scale by fp_inv(k) (core/field.hpp:229-273; the
+// inverse is unique, so the device's addition chain, PVAC_FP_INV, gives the reference's value;
+// fp_inv(0) = 0 as there).
+template <class PubKeyT, class CipherT, class FpT>
+CipherT ct_div_const(const PubKeyT& pk, const CipherT& A, const FpT& k) {
+    uint64_t lo = k.lo, hi = k.hi;
+    engine_for(pk).fp_binop(PVAC_FP_INV, &lo, &hi, nullptr, nullptr, &lo, &hi, 1);
+    FpT inv = k;
+    inv.lo = lo;
+    inv.hi = hi;
+    return ct_scale(pk, A, inv);
 }
 
 // ---- batched forms ------------------------------------------------------------------------

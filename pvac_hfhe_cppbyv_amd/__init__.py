@@ -444,6 +444,21 @@ class Engine:
         self._check(self.lib.pvac_hip_ct_scale(self.ctx, C.byref(sx), s & ((1 << 64) - 1), s >> 64))
         return X
 
+    def ct_neg(self, X: DeviceBatch):
+        """ct_neg (ops/arithmetic.hpp:39-41): ct_scale by fp_neg(1) = p - 1, in place."""
+        return self.ct_scale(X, (1 << 127) - 2)
+
+    def fp_inv(self, k: int) -> int:
+        """fp_inv (core/field.hpp:229-273) of one element on the device (PVAC_FP_INV); inv(0) = 0."""
+        a = _t(np.array([k & ((1 << 64) - 1), (k >> 64) & ((1 << 64) - 1)], np.uint64)).to(self.device)
+        lo, hi = self.fp_binop(FP_INV, a[0:1], a[1:2])
+        o = np.concatenate([lo.cpu().numpy(), hi.cpu().numpy()]).view(np.uint64)
+        return int(o[0]) | (int(o[1]) << 64)
+
+    def ct_div_const(self, X: DeviceBatch, k: int):
+        """ct_div_const (ops/arithmetic.hpp:108-110): ct_scale by fp_inv(k), in place."""
+        return self.ct_scale(X, self.fp_inv(k))
+
     def sigma(self, X: DeviceBatch, salts):
         sx = X.struct()
         self._check(self.lib.pvac_hip_sigma_batch(self.ctx, C.byref(sx), C.c_void_p(salts.data_ptr())))
@@ -498,4 +513,4 @@ class Engine:
 
 
 __all__ = ["Engine", "DeviceBatch", "HostCipher", "PvacError", "LAYER_DT", "load_library", "FP_ADD", "FP_SUB",
-           "FP_MUL", "FP_NEG", "FP_SCALE", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL"]
+           "FP_MUL", "FP_NEG", "FP_SCALE", "FP_INV", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL"]

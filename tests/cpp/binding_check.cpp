@@ -20,6 +20,8 @@ Cipher ct_add(const PubKey& pk, const Cipher& A, const Cipher& B) { return pvac_
 Cipher ct_sub(const PubKey& pk, const Cipher& A, const Cipher& B) { return pvac_hip::ct_sub(pk, A, B); }    // :43
 Cipher ct_scale(const PubKey& pk, const Cipher& A, const Fp& s) { return pvac_hip::ct_scale(pk, A, s); }    // :33
 Cipher ct_mul(const PubKey& pk, const Cipher& A, const Cipher& B) { return pvac_hip::ct_mul(pk, A, B); }    // :47
+Cipher ct_neg(const PubKey& pk, const Cipher& A) { return pvac_hip::ct_neg(pk, A); }                         // :39
+Cipher ct_div_const(const PubKey& pk, const Cipher& A, const Fp& k) { return pvac_hip::ct_div_const(pk, A, k); } // :108
 Cipher enc_value(const PubKey& pk, const SecKey& sk, uint64_t v) {                                          // encrypt.hpp:289
     return pvac_hip::enc_value<Cipher>(pk, sk, v);
 }

@@ -280,6 +280,25 @@ int main(int argc, char** argv) {
             const auto& want = r_sub.E[x.E.size() + e].w;
             MUST(ny.E[e].w.lo == want.lo && ny.E[e].w.hi == want.hi, "ct_scale pair %d edge %zu", p, e);
         }
+        // ct_neg (arithmetic.hpp:39-41) is that same scale; layers and sigmas are y's
+        const Cipher ng = pvac_hip::ct_neg(pk, y);
+        MUST(same_layers(ng, y) && ng.E.size() == y.E.size(), "ct_neg pair %d shape", p);
+        for (size_t e = 0; e < ng.E.size(); ++e) {
+            const auto& want = r_sub.E[x.E.size() + e];
+            MUST(ng.E[e].w.lo == want.w.lo && ng.E[e].w.hi == want.w.hi && ng.E[e].s.w == y.E[e].s.w,
+                 "ct_neg pair %d edge %zu", p, e);
+        }
+        // ct_div_const (arithmetic.hpp:108-110): dividing by k then scaling by k gives x back
+        // (canonical weights); k = 2 has the known inverse (p + 1) / 2 = 2^126
+        const mirror::Fp ks[3] = {{2, 0}, {0x0123456789ABCDEFull, 0x0FEDCBA987654321ull}, {~0ull - 1, 0x7FFFFFFFFFFFFFFFull}};
+        for (const auto& k : ks) {
+            const Cipher q = pvac_hip::ct_div_const(pk, x, k);
+            const Cipher back = pvac_hip::ct_scale(pk, q, k);
+            MUST(same_layers(back, x) && same_edges(back, x, true), "ct_div_const pair %d k.lo %" PRIx64, p, k.lo);
+        }
+        const Cipher h = pvac_hip::ct_div_const(pk, x, mirror::Fp{2, 0});
+        const Cipher h2 = pvac_hip::ct_scale(pk, x, mirror::Fp{0, 0x4000000000000000ull});
+        MUST(same_edges(h, h2, true), "ct_div_const by 2 == ct_scale by 2^126, pair %d", p);
     }
 
     // bounty2_data: sum.ct == combine(a.ct, b.ct) byte for byte through the adapter

@@ -555,3 +555,31 @@ def test_ct_scale_ragged(engine, oracle, s):
         want_lo, want_hi = oracle.fp("mul", c.w_lo, c.w_hi, np.full(n, s_lo, np.uint64), np.full(n, s_hi, np.uint64))
         assert np.array_equal(o.w_lo, want_lo) and np.array_equal(o.w_hi, want_hi)
         assert np.array_equal(o.meta, c.meta) and o.layers.tobytes() == c.layers.tobytes()
+
+
+def test_ct_neg_and_div_const(engine, oracle):
+    """ct_neg (ops/arithmetic.hpp:39-41) = ct_scale by p - 1 and ct_div_const (:108-110) = ct_scale
+    by fp_inv(k) (core/field.hpp:229-273), against the oracle's fp_mul / fp_inv; k = 0 scales by
+    fp_inv(0) = 0 as the reference does."""
+    chain = read_ct(os.path.join(REF, "chain3.ct"))[0]
+    fresh = read_ct(os.path.join(REF, "pair0_x.ct"))[0]
+    cs = [fresh, chain]
+    one = lambda v: (np.array([v & ((1 << 64) - 1)], np.uint64), np.array([v >> 64], np.uint64))
+    X = _dev_batch(engine, cs)
+    engine.ct_neg(X)
+    for c, o in zip(cs, X.to_host()):
+        n = len(c.w_lo)
+        want = oracle.fp("mul", c.w_lo, c.w_hi, np.full(n, ~np.uint64(1), np.uint64),
+                         np.full(n, np.uint64(0x7FFFFFFFFFFFFFFF), np.uint64))
+        assert np.array_equal(o.w_lo, want[0]) and np.array_equal(o.w_hi, want[1])
+        assert np.array_equal(o.meta, c.meta) and o.layers.tobytes() == c.layers.tobytes()
+    for k in (2, 0, 1, P - 1, (0x0123456789ABCDEF << 64) | 0xFEDCBA9876543210, (1 << 128) - 1):
+        ilo, ihi = oracle.fp("inv", *one(k))
+        assert engine.fp_inv(k) == int(ilo[0]) | (int(ihi[0]) << 64)
+        X = _dev_batch(engine, cs)
+        engine.ct_div_const(X, k)
+        for c, o in zip(cs, X.to_host()):
+            n = len(c.w_lo)
+            want = oracle.fp("mul", c.w_lo, c.w_hi, np.full(n, ilo[0], np.uint64), np.full(n, ihi[0], np.uint64))
+            assert np.array_equal(o.w_lo, want[0]) and np.array_equal(o.w_hi, want[1])
+    assert engine.fp_inv(2) == 1 << 126

@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 OUT="$ROOT/gpurun_out/chain_$TAG"
 mkdir -p "$OUT"
 (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv \
-    -- python3 "$ROOT/bench.py" --only chain --chain-inputs 1024 --chain-chunk 1024 > "$OUT/chain.log" 2>&1) || exit $?
-tail -1 "$OUT/chain.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_by_step'], d['ct_mul_per_s'])"
+    -- python3 "$ROOT/bench.py" --only chain --chain-inputs ${CHAIN_INPUTS:-4096} --chain-chunk ${CHAIN_CHUNK:-4096} --chain-check 0 --chain-ref 0 > "$OUT/chain.log" 2>&1) || exit $?
+tail -1 "$OUT/chain.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["stream_ms_by_step"], d["ct_mul_per_s"])' 
 f=$(find "$OUT" -name '*kernel_stats.csv' | head -1)
 python3 -c "
 import csv
