@@ -16,10 +16,14 @@ fi
 cp $L/libpvac_hip.so gpurun_out/lib_new.so || exit 1
 for pass in 1 2; do
   for v in new "$@"; do
-    if [ $v = new ]; then cp gpurun_out/lib_new.so $L/libpvac_hip.so; else cp $L/exp/libpvac_hip_$v.so $L/libpvac_hip.so; fi
-    timeout -k 10 300 python bench.py --only chain > gpurun_out/chain_$v$pass.log 2>&1 || { cp gpurun_out/lib_new.so $L/libpvac_hip.so; exit 1; }
+    # a variant "env:NAME=VALUE" runs the product library with that environment variable
+    envv=""
+    if [ $v = new ] || [ "${v#env:}" != "$v" ]; then cp gpurun_out/lib_new.so $L/libpvac_hip.so; else cp $L/exp/libpvac_hip_$v.so $L/libpvac_hip.so; fi
+    [ "${v#env:}" != "$v" ] && envv="${v#env:}"
+    tag=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
+    env $envv timeout -k 10 300 python bench.py --only chain > gpurun_out/chain_$tag$pass.log 2>&1 || { cp gpurun_out/lib_new.so $L/libpvac_hip.so; exit 1; }
     echo -n "$v$pass "
-    tail -1 gpurun_out/chain_$v$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d.get('errors'), round(d['ct_mul_per_s']), round(d['chain_seconds'],3), [round(x) for x in d['stream_ms_by_step']], d.get('oracle_sample_ok'))"
+    tail -1 gpurun_out/chain_$tag$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d.get('errors'), round(d['ct_mul_per_s']), round(d['chain_seconds'],3), [round(x) for x in d['stream_ms_by_step']], d.get('oracle_sample_ok'))"
   done
 done
 cp gpurun_out/lib_new.so $L/libpvac_hip.so
