@@ -583,3 +583,36 @@ def test_ct_neg_and_div_const(engine, oracle):
             want = oracle.fp("mul", c.w_lo, c.w_hi, np.full(n, ilo[0], np.uint64), np.full(n, ihi[0], np.uint64))
             assert np.array_equal(o.w_lo, want[0]) and np.array_equal(o.w_hi, want[1])
     assert engine.fp_inv(2) == 1 << 126
+
+
+def test_ct_mul_api_errors_leave_context_usable(oracle):
+    """Errors fail loudly (PvacError with the ABI's message) and leave the context usable:
+    |A| != |B| at plan time, exec with a plan a later plan made stale, and a pair whose product
+    layers exceed the general path's table (|A.L| + |B.L| + |A.L||B.L| > 16,384: PVAC_ENOSYS,
+    where the reference would run it). A normal batch on the same context is then bit-exact."""
+    from pvac_hfhe_cppbyv_amd import Engine, PvacError
+    eng = Engine(device=0, canon_tag=0x55)
+    rng = np.random.default_rng(0x55)
+    xs = [_full_range_cipher(rng, 2, 40, dup_frac=0) for _ in range(3)]
+    ys = [_full_range_cipher(rng, 2, 40, dup_frac=0) for _ in range(3)]
+    A, B = _dev_batch(eng, xs), _dev_batch(eng, ys)
+    with pytest.raises(PvacError):
+        eng.ct_mul_plan(A, _dev_batch(eng, ys[:2]))
+    Cb, plan = eng.ct_mul_plan(A, B)
+    nonces = eng.torch.empty(2 * plan.total_layer_slots, dtype=eng.torch.int64, device=eng.device)
+    eng.fill_random(nonces, 0x55)
+    Cb2, plan2 = eng.ct_mul_plan(A, B)   # `plan` is stale from here on
+    with pytest.raises(PvacError, match="latest"):
+        eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+    big_a, big_b = _full_range_cipher(rng, 200, 64, dup_frac=0), _full_range_cipher(rng, 90, 64, dup_frac=0)
+    with pytest.raises(PvacError, match="layers"):
+        eng.ct_mul_plan(_dev_batch(eng, [big_a]), _dev_batch(eng, [big_b]))
+    Cb, plan = eng.ct_mul_plan(A, B)
+    out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+    assert list(eng.ct_mul_status(3)) == [0, 0, 0]
+    nz = nonces.cpu().numpy().view(np.uint64)
+    loff = Cb.l_off.cpu().numpy().view(np.uint64)
+    for p, (x, y) in enumerate(zip(xs, ys)):
+        base = int(loff[p]) + x.nL + y.nL
+        ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0x55)
+        _assert_same(out[p], ref, layers_view=False)
