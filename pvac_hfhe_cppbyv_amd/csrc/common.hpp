@@ -254,7 +254,7 @@ struct large_desc {
     uint64_t g_head, g_next;
     // zero-initialised block [o_zero, o_zero + zero_words): cnt | hkey | hhead | bmask | bcnt | used
     uint64_t o_zero, zero_words;
-    uint64_t o_cnt;              // [8] neA, neB, invalid, total edges, canonical
+    uint64_t o_cnt;              // [8] neA, neB, invalid, total edges, canonical, A / B id allocation, deferred tasks
     uint64_t o_hkey;             // [2^hbits] u64 bucket ids + 1
     uint64_t o_hhead;            // [2^hbits] chain heads (slot + 1)
     uint64_t o_bmask;            // [nblk] u64 per 16 first-insert times: bucket-leader edge codes (2 bits
@@ -267,6 +267,8 @@ struct large_desc {
     // written before read
     uint64_t o_lstA, o_lstB;     // [2 LA] start,count per layer ++ [nA] edge ids; same for B
     uint64_t o_neA, o_neB;       // [LA] / [LB] non-empty layer lists
+    uint64_t o_defer;            // [LA LB] tasks k_large_products_la leaves to k_large_products_defer
+                                 // (la << 16 | lb index), counted in cnt[7]
     uint64_t o_info;             // [S] ebits (2 bits) | hash slot << 2
     uint64_t o_sums;             // [S] x 4 u64: P lo, P hi, M lo, M hi
     uint64_t o_nxt;              // [S] bucket chain links
@@ -290,12 +292,20 @@ struct mul_large_args {
     uint64_t canon_tag;
     uint64_t edge_budget;
     uint32_t flags;
-    uint32_t pad;
+    uint32_t n_la;               // products: descriptors sel[0, n_la) take k_large_products_la, the rest
+                                 // k_large_products (one workgroup per task)
     uint32_t* salt_pos;          // nullable: per output edge slot, its hash-order index
     const uint32_t* grp;         // static bucket-group tables (large_desc::g_head / g_next)
-    // launch sizing (maxima over the nl descriptors)
-    uint64_t max_S, max_zero, max_tasks, max_capE, max_lay;
+    const uint32_t* sel;         // [nl] descriptor indices, A-layer-major class first
+    uint32_t lds_task;           // k_large_products_la: bytes of LDS below its staged B layers (set at launch)
+    uint32_t pad;
+    // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all
+    // over all, max_la_wg = ceil(|A.L| / kLaPerWG) over the A-layer-major class)
+    uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg;
 };
+// k_large_products_la: A layers per workgroup; pairs with at most kLaMaxLB B layers take it
+constexpr uint32_t kLaPerWG = 4;
+constexpr uint32_t kLaMaxLB = 4;
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
 // measured integer-ALU ceilings (k_ubench.hip)
 hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s);

@@ -34,6 +34,10 @@
 #include "common.hpp"
 #include "sha256.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 namespace pvhip {
 
 namespace {
@@ -144,8 +148,32 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     }
 }
 
+// one edge of a layer: its words and its index in the pair's edge array (first-insert times use it)
+struct edge_rec {
+    uint64_t meta, lo, hi;
+    uint32_t e;
+};
+// the edges of one layer of one side of a pair, gathered through the layer's id list (layer-grouped
+// 32-byte records written by k_large_lists were measured: the scattered record writes cost lists
+// more than the products kernel saved)
+struct layer_src {
+    const pvac_ct_batch* X;
+    uint64_t eo;          // the pair's edge offset in X
+    const uint32_t* ids;
+    uint32_t n;
+};
+__device__ __forceinline__ edge_rec load_edge(const layer_src& L, uint32_t k) {
+    const uint32_t e = L.ids[k];
+    return edge_rec{L.X->meta[L.eo + e], L.X->w_lo[L.eo + e], L.X->w_hi[L.eo + e], e};
+}
+__device__ __forceinline__ layer_src side_layer(const pvac_ct_batch* X, uint64_t eo, const uint32_t* S, uint64_t o_lst, uint32_t L,
+                                                uint32_t l) {
+    return layer_src{X, eo, S + o_lst + 2u * L + S[o_lst + l], S[o_lst + L + l]};
+}
+
 // ---------------------------------------------------------------- products (one task per WG)
 constexpr int kLP = 384;                 // products workgroup: one lane per output index r (B = 337)
+constexpr int kLPX = 256;                // products workgroup with the matrix-core dense mode (4 waves)
 constexpr int kLPRows = 3;               // B <= kLP * kLPRows
 constexpr uint32_t kBmax = kLP * kLPRows;
 constexpr uint32_t kChunk = 128;         // sparse-side edges staged per round (chain steps: ~20)
@@ -165,28 +193,278 @@ __host__ __device__ inline uint32_t prod_lds_bytes(uint32_t Bm) {
     return dense > scat ? dense : scat;
 }
 
-__global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
-    const large_desc& d = g.desc[blockIdx.y];
+// ---- dense mode on the matrix cores (gfx950 v_mfma_i32_32x32x32_i8) --------------------------
+// An Fp value v (canonical) is taken as the signed integer V = v (v < 2^126) or v - p, written
+// with 16 balanced base-256 digits d_i in [-128, 127] (int8). For output index r of a task,
+//     sum_e D[r - idx_e] * w_e  =  sum_m 256^m  sum_e sum_j W_e[m][j] D[r - idx_e][j],
+// W_e[m][j] = digit (m - j) of w_e (zero outside 0..15): a 32 x 32 (digit position m) x (row r)
+// tile over K = 2 sparse edges x 16 digits is ONE v_mfma_i32_32x32x32_i8. Column sums stay
+// below 2^23 (<= 20 edges x 16 digit pairs x 2^14), so nothing overflows before the epilogue
+// turns the 31 digit positions of a row into Fp (mx_fold). Operand maps (tools/mfma_i8_probe.hip):
+// A lane l = (m = l & 31, half h = l >> 5) byte j  x  B lane (r = l & 31, h) byte j, for the same
+// (h, j); D lane l register i = position (i & 3) + 8 (i >> 2) + 4 h of row l & 31.
+typedef int mx_v4 __attribute__((ext_vector_type(4)));
+typedef int mx_v16 __attribute__((ext_vector_type(16)));
+constexpr int kMxKS = 10;                          // k-steps held in registers: 2 sparse edges each
+constexpr uint32_t kMxMaxSparse = 2u * kMxKS;      // sparse sides up to this size take the MFMA path
+constexpr uint64_t kDigC = 0x8080808080808080ull;  // 128 in every byte
+#ifndef PVAC_EXP_MXREP   // experiment builds only: the MFMA loop run this many times (same result)
+#define PVAC_EXP_MXREP 1
+#endif
+
+// balanced digits of a canonical value: U = V + C (C = 128 in each of the 16 bytes), d = U ^ C
+__device__ __forceinline__ void fp_digits8(const fp& v, uint64_t& dl, uint64_t& dh) {
+    const bool neg = (v.hi >> 62) != 0;            // v >= 2^126: V = v - p = v + 2^127 + 1 (mod 2^128)
+    const uint64_t l = v.lo + (neg ? 1ull : 0ull);
+    const uint64_t h = v.hi + (neg ? 0x8000000000000000ull + (l < v.lo ? 1ull : 0ull) : 0ull);
+    const uint64_t ul = l + kDigC;
+    const uint64_t uh = h + kDigC + (ul < l ? 1ull : 0ull);
+    dl = ul ^ kDigC;
+    dh = uh ^ kDigC;
+}
+
+// the four 4-position groups of a lane's 16 column sums: g[q] = sum_i c[4q + i] 256^i, at bit
+// 64 q + 32 h of the row's value (|g| < 2^47)
+__device__ __forceinline__ void mx_groups(const mx_v16& c, int64_t* g) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        g[q] = (int64_t)c[4 * q] + (int64_t)c[4 * q + 1] * 256 + (int64_t)c[4 * q + 2] * 65536 +
+               (int64_t)c[4 * q + 3] * 16777216;
+}
+
+// Z = sum_q (glo[q] + ghi[q] 2^32) 2^(64 q) mod p, canonical. 2^128 == 2 and 2^127 == 1 (mod p).
+__device__ __forceinline__ fp mx_fold(const int64_t* glo, const int64_t* ghi) {
+    const int64_t a0 = glo[0] + 2 * glo[2], a1 = ghi[0] + 2 * ghi[2];   // bits 0, 32
+    const int64_t b0 = glo[1] + 2 * glo[3], b1 = ghi[1] + 2 * ghi[3];   // bits 64, 96
+    // 32-bit words W0..W4 of Z; W4 2^128 == 2 W4 goes into W0
+    int64_t t = (int64_t)(uint32_t)a0 + 2 * (b1 >> 32);
+    const uint32_t x0 = (uint32_t)t;
+    t = (t >> 32) + (a0 >> 32) + (int64_t)(uint32_t)a1;
+    const uint32_t x1 = (uint32_t)t;
+    t = (t >> 32) + (a1 >> 32) + (int64_t)(uint32_t)b0;
+    const uint32_t x2 = (uint32_t)t;
+    t = (t >> 32) + (b0 >> 32) + (int64_t)(uint32_t)b1;
+    const uint32_t x3 = (uint32_t)t;
+    const int64_t k = t >> 32;                     // Z == X + 2 k, X = x3..x0 in [0, 2^128), |k| <= 1
+    uint64_t lo = (uint64_t)x0 | (uint64_t)x1 << 32, hi = (uint64_t)x2 | (uint64_t)x3 << 32;
+    const int64_t s = (int64_t)(hi >> 63) + 2 * k; // X = Xl + 2^127 Xh
+    hi &= kM63;
+    // Xl + s, or Xl + (p + s) when s < 0: stays in [0, 2^128)
+    const uint64_t alo = s < 0 ? kAll - (uint64_t)(-s) : (uint64_t)s;
+    const uint64_t ahi = s < 0 ? kM63 : 0ull;
+    lo += alo;
+    hi += ahi + (lo < alo ? 1ull : 0ull);
+    return fp_from_words(lo, hi);
+}
+
+__device__ __forceinline__ int64_t shfl_xor64(int64_t v, int mask) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, mask);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)v >> 32), mask);
+    return (int64_t)((uint64_t)hi << 32 | lo);
+}
+
+// LDS of the MFMA dense mode: dig[2][2B] (16 B of digits per dense slot, stored twice per channel
+// like the column mode's tables) | tt[2][2B] (the dense side's share of the first-insert time) |
+// dup; then, per sparse side, prec[kMxMaxSparse][3] (48 B per sparse edge: 16 zero bytes, its
+// digits reversed, 16 zero bytes: W_e's row m is the 16-byte window at 31 - m) and
+// pinf[kMxMaxSparse] (uint4: P and M slot offsets relative to row r, the sparse side's share of t)
+__host__ __device__ inline uint32_t mx_lds_bytes(uint32_t Bm) { return al16(80u * Bm + 4u); }
+constexpr uint32_t kMxSparseBytes = 64u * kMxMaxSparse;
+
+// the dense side of a task into dig / tt. Every thread calls it; barriers inside; false
+// (workgroup-uniform) when the layer holds duplicate (idx, ch) edges
+template <int BS>
+__device__ bool mx_stage_dense(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t tmul) {
+    uint4* dig = (uint4*)lds;
+    uint32_t* tt = (uint32_t*)(lds + 64u * Bm);
+    uint32_t* dup = (uint32_t*)(lds + 80u * Bm);
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < 4 * Bm; k += BS) {
+        dig[k] = make_uint4(0, 0, 0, 0);
+        tt[k] = kInf;
+    }
+    if (tid == 0) *dup = 0;
+    __syncthreads();
+    for (uint32_t k0 = tid; k0 < D.n; k0 += 2u * BS) {   // two edges per round, loads first
+        edge_rec x[2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const uint32_t k = k0 + (uint32_t)v * BS;
+            x[v] = load_edge(D, k < D.n ? k : 0u);
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            if (k0 + (uint32_t)v * BS >= D.n) break;
+            const uint32_t sl = meta_ch(x[v].meta) * 2u * Bm + meta_idx(x[v].meta);
+            const uint32_t te = x[v].e * tmul;   // the dense side's share of t = i |B.E| + j
+            if (atomicCAS(&tt[sl], kInf, te) != kInf) {
+                *dup = 1;
+            } else {
+                uint64_t dl, dh;
+                fp_digits8(fp_canon(x[v].lo, x[v].hi), dl, dh);
+                dig[sl] = dig[sl + Bm] = make_uint4((uint32_t)dl, (uint32_t)(dl >> 32), (uint32_t)dh, (uint32_t)(dh >> 32));
+                tt[sl + Bm] = te;
+            }
+        }
+    }
+    __syncthreads();
+    return *dup == 0;
+}
+
+// the sparse side of a task (n <= kMxMaxSparse edges) into prec / pinf; thread k writes edge k
+// (an odd count gets a zero padding edge). No barrier.
+__device__ __forceinline__ void mx_stage_sparse(uint4* prec, uint4* pinf, uint32_t Bm, const layer_src& Sd, uint32_t smul,
+                                                uint32_t k) {
+    const uint32_t nks = (Sd.n + 1u) >> 1;
+    if (k >= 2u * nks) return;
+    uint4 mid = make_uint4(0, 0, 0, 0);
+    uint4 inf = make_uint4(Bm, Bm, kInf, 0);   // padding edge: zero digits, time never smaller
+    if (k < Sd.n) {
+        const edge_rec x = load_edge(Sd, k);
+        uint64_t dl, dh;
+        fp_digits8(fp_canon(x.lo, x.hi), dl, dh);
+        const uint64_t rl = __builtin_bswap64(dh), rh = __builtin_bswap64(dl);   // digit 15 - x at byte x
+        mid = make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
+        const uint32_t sidx = meta_idx(x.meta), sch = meta_ch(x.meta);
+        // dense slot of output row r: P (dense channel == sparse channel), M (the other)
+        inf = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, x.e * smul, 0);
+    }
+    prec[3u * k] = make_uint4(0, 0, 0, 0);
+    prec[3u * k + 1u] = mid;
+    prec[3u * k + 2u] = make_uint4(0, 0, 0, 0);
+    pinf[k] = inf;
+}
+
+// where a task's results go: dense key-slot arrays of the pair
+struct task_out {
+    uint32_t* tkey;
+    uint32_t* info;
+    ulonglong2* sums;
+    const uint32_t* ghead;              // static bucket groups (nullptr: dynamic chains)
+    unsigned long long* bpack;          // bucket-leader block marks
+};
+
+// the products of one staged task on the matrix cores: each wave takes blocks of 32 output rows
+// (both channels), writes tkey / info / sums and marks lone bucket leaders. No barrier; returns
+// whether any of this thread's keys emits.
+// NKS = k-steps of two sparse edges, a compile-time count: the k-step loop is straight-line code,
+// so every k-step's LDS reads can be issued ahead of the MFMAs (a runtime guard per k-step made
+// each one a basic block of its own: two dependent LDS round trips per k-step)
+template <int BS, int NKS>
+__device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* pinf, uint32_t Bm, uint64_t slot0,
+                            const task_out& o) {
+    const uint4* dig = (const uint4*)lds;
+    const uint32_t* tt = (const uint32_t*)(lds + 64u * Bm);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t h = lane >> 5, n = lane & 31u;
+    bool any = false;
+    // A operand of k-step s: row m = n of W_e, e = 2 s + h: 16 bytes at 31 - n of prec[e]
+    mx_v4 frag[NKS];
+    {
+        const uint32_t y0 = 31u - n, sh = y0 & 3u;
+        const uint32_t* pw = (const uint32_t*)prec + (y0 >> 2) + 12u * h;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const uint32_t* q = pw + 24u * (uint32_t)s;
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+            frag[s] = mx_v4{(int)__builtin_amdgcn_alignbyte(w1, w0, sh), (int)__builtin_amdgcn_alignbyte(w2, w1, sh),
+                            (int)__builtin_amdgcn_alignbyte(w3, w2, sh), (int)__builtin_amdgcn_alignbyte(w4, w3, sh)};
+        }
+    }
+    const uint32_t nblk = (Bm + 31u) >> 5;
+    for (uint32_t blk = wave; blk < nblk; blk += BS / 64) {
+        const uint32_t r = blk * 32u + n;
+        const bool live = r < Bm;
+        const uint32_t rr = live ? r : 0u;
+        mx_v16 aP, aM;
+        uint32_t tmin;
+        for (int rep_ = 0; rep_ < PVAC_EXP_MXREP; ++rep_) {   // experiment builds repeat the loop
+            uint32_t rq = rr;
+            asm volatile("" : "+v"(rq));
+            aP = mx_v16{};
+            aM = mx_v16{};
+            tmin = kInf;
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                const uint4 in = pinf[2u * (uint32_t)s + h];
+                const uint4 dp = dig[in.x + rq], dm = dig[in.y + rq];
+                const uint32_t tp = tt[in.x + rq], tm = tt[in.y + rq];
+                aP = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dp.x, (int)dp.y, (int)dp.z, (int)dp.w}, aP, 0, 0, 0);
+                aM = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dm.x, (int)dm.y, (int)dm.z, (int)dm.w}, aM, 0, 0, 0);
+                tmin = min(tmin, min(__builtin_elementwise_add_sat(tp, in.z), __builtin_elementwise_add_sat(tm, in.z)));
+            }
+        }
+        // half 0 folds row r's P sum, half 1 its M sum; each needs the other half's groups
+        int64_t gp[4], gm[4], glo[4], ghi[4];
+        mx_groups(aP, gp);
+        mx_groups(aM, gm);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t oth = shfl_xor64(h ? gp[q] : gm[q], 32);
+            const int64_t own = h ? gm[q] : gp[q];
+            glo[q] = h ? oth : own;
+            ghi[q] = h ? own : oth;
+        }
+        const fp v = mx_fold(glo, ghi);
+        const uint32_t nz = fp_nonzero(v) ? 1u : 0u;
+        const uint32_t nzo = (uint32_t)__shfl_xor((int)nz, 32);
+        const uint32_t eb = h ? (nzo | nz << 1) : (nz | nzo << 1);
+        tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, 32));
+        if (live) {
+            const uint64_t s = slot0 + r;
+            if (h == 0) o.tkey[s] = tmin;
+            if (tmin != kInf) {
+                o.sums[2 * s + h] = make_ulonglong2(v.lo, v.hi);
+                if (h == 0) {
+                    o.info[s] = eb;
+                    if (eb && o.ghead && o.ghead[s] == 0u) leader_mark(o.bpack, tmin, __popc(eb));
+                }
+                any |= eb != 0;
+            }
+        }
+    }
+    return any;
+}
+
+template <int BS>
+__device__ bool mx_blocks(const uint8_t* lds, const uint4* prec, const uint4* pinf, uint32_t ns, uint32_t Bm, uint64_t slot0,
+                          const task_out& o) {
+    static_assert(kMxKS == 10, "one instantiation per k-step count");
+    switch ((ns + 1u) >> 1) {   // workgroup-uniform
+    case 0: return false;       // no products: the slots keep their initial time
+    case 1: return mx_blocks_n<BS, 1>(lds, prec, pinf, Bm, slot0, o);
+    case 2: return mx_blocks_n<BS, 2>(lds, prec, pinf, Bm, slot0, o);
+    case 3: return mx_blocks_n<BS, 3>(lds, prec, pinf, Bm, slot0, o);
+    case 4: return mx_blocks_n<BS, 4>(lds, prec, pinf, Bm, slot0, o);
+    case 5: return mx_blocks_n<BS, 5>(lds, prec, pinf, Bm, slot0, o);
+    case 6: return mx_blocks_n<BS, 6>(lds, prec, pinf, Bm, slot0, o);
+    case 7: return mx_blocks_n<BS, 7>(lds, prec, pinf, Bm, slot0, o);
+    case 8: return mx_blocks_n<BS, 8>(lds, prec, pinf, Bm, slot0, o);
+    case 9: return mx_blocks_n<BS, 9>(lds, prec, pinf, Bm, slot0, o);
+    default: return mx_blocks_n<BS, 10>(lds, prec, pinf, Bm, slot0, o);
+    }
+}
+
+// One (la, lb) task: the matrix-core dense mode when MX and the sparse side is small, else the
+// column-accumulator dense mode (when col26_ok), else (sparse x sparse, duplicate edges) the
+// scatter mode. Every thread of the workgroup calls it (barriers inside); LDS from plds,
+// prod_lds_bytes(B) (col26 / scatter) or al16(mx_lds_bytes(B)) + kMxSparseBytes (MX), 52 B (scatter).
+template <int BS, bool MX>
+__device__ void run_task(const mul_large_args& g, const large_desc& d, uint32_t la, uint32_t lb, uint8_t* plds,
+                         bool col26_ok = true) {
     uint32_t* S = g.scratch;
-    const uint32_t* cnt = S + d.o_cnt;
-    if (cnt[2]) return;
     const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
-    const uint32_t tl = blockIdx.x;
-    const uint32_t la_i = tl / LB, lb_i = tl - la_i * LB;
-    if (la_i >= cnt[0] || lb_i >= cnt[1]) return;
-    const uint32_t la = S[d.o_neA + la_i], lb = S[d.o_neB + lb_i];
-    const uint32_t a0 = S[d.o_lstA + la], na = S[d.o_lstA + LA + la];
-    const uint32_t b0 = S[d.o_lstB + lb], nb = S[d.o_lstB + LB + lb];
-    const uint32_t* idsA = S + d.o_lstA + 2 * LA + a0;
-    const uint32_t* idsB = S + d.o_lstB + 2 * LB + b0;
-    const uint64_t pr = d.pair;
-    const uint64_t aeo = g.A.e_off[pr], beo = g.B.e_off[pr];
+    const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
+    const layer_src srcB = side_layer(&g.B, g.B.e_off[d.pair], S, d.o_lstB, LB, lb);
+    const uint32_t na = srcA.n, nb = srcB.n;
     const uint32_t lp = la * LB + lb;
     const uint64_t slot0 = (uint64_t)lp * Bm;
     const int tid = threadIdx.x;
     const bool denseA = na >= nb;
     const uint32_t nd = denseA ? na : nb, ns = denseA ? nb : na;
+    const layer_src& Dn = denseA ? srcA : srcB;
+    const layer_src& Sp = denseA ? srcB : srcA;
+    const uint32_t tmulD = denseA ? nB : 1u, tmulS = denseA ? 1u : nB;   // shares of t = i |B.E| + j
     uint32_t* tkey = S + d.o_tkey;
     uint32_t* info = S + d.o_info;
     ulonglong2* sums = (ulonglong2*)(S + d.o_sums);
@@ -196,8 +474,15 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
     unsigned long long* bpack = (unsigned long long*)w64(S, d.o_bmask);
     bool any = false;
 
-    bool dense = nd >= kLargeDenseMin;
-    if (dense) {
+    bool dense = col26_ok && nd >= kLargeDenseMin;
+    if (MX && dense && ns <= kMxMaxSparse) {
+        uint4* prec = (uint4*)(plds + mx_lds_bytes(Bm));
+        uint4* pinf = prec + 3u * kMxMaxSparse;
+        mx_stage_sparse(prec, pinf, Bm, Sp, tmulS, (uint32_t)tid);   // made visible by the dense staging's barriers
+        dense = mx_stage_dense<BS>(plds, Bm, Dn, tmulD);
+        if (dense) any = mx_blocks<BS>(plds, prec, pinf, ns, Bm, slot0, task_out{tkey, info, sums, ghead, bpack});
+        __syncthreads();
+    } else if (dense) {
         // Dense-owner mode with column accumulators (fp127.hpp col26_*): both sides are staged as
         // 26-bit limbs, each probe is 25 v_mad_u64_u32 into the lane's P or M columns and a
         // saturating add + min for the first-insert time. Empty dense slots hold zero limbs and
@@ -209,50 +494,34 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         uint32_t* sinf = sl1 + kChunk;
         uint32_t* sidv = sinf + kChunk;
         uint32_t* dup = sidv + kChunk;
-        const uint32_t* sids = denseA ? idsB : idsA;
-        const pvac_ct_batch& Sp = denseA ? g.B : g.A;
-        const uint64_t seo = denseA ? beo : aeo;
         // the first sparse chunk's loads go out before the dense staging, so the two sides' global
-        // round trips overlap (thread k < kChunk < kLP stages sparse edge k)
-        uint32_t pe = 0;
-        uint64_t pmeta = 0, plo = 0, phi = 0;
-        if (tid < min(ns, kChunk)) {
-            pe = sids[tid];
-            pmeta = Sp.meta[seo + pe];
-            plo = Sp.w_lo[seo + pe];
-            phi = Sp.w_hi[seo + pe];
-        }
-        for (uint32_t k = tid; k < 4 * Bm; k += kLP) {
+        // round trips overlap (thread k < kChunk < BS stages sparse edge k)
+        edge_rec pr0{0, 0, 0, 0};
+        if ((uint32_t)tid < min(ns, kChunk)) pr0 = load_edge(Sp, tid);
+        for (uint32_t k = tid; k < 4 * Bm; k += BS) {
             dl4[k] = make_uint4(0, 0, 0, 0);
             dx[k] = make_uint2(0, kInf);
         }
         if (tid == 0) *dup = 0;
         __syncthreads();
-        const uint32_t* dids = denseA ? idsA : idsB;
-        const pvac_ct_batch& D = denseA ? g.A : g.B;
-        const uint64_t deo = denseA ? aeo : beo;
-        for (uint32_t k0 = tid; k0 < nd; k0 += 2u * kLP) {   // two edges per round, loads first
-            uint32_t e[2];
-            uint64_t m[2], wl[2], wh[2];
+        for (uint32_t k0 = tid; k0 < nd; k0 += 2u * BS) {   // two edges per round, loads first
+            edge_rec x[2];
 #pragma unroll
             for (int v = 0; v < 2; ++v) {
-                const uint32_t k = k0 + (uint32_t)v * kLP;
-                e[v] = k < nd ? dids[k] : 0u;
-                m[v] = k < nd ? D.meta[deo + e[v]] : 0ull;
-                wl[v] = k < nd ? D.w_lo[deo + e[v]] : 0ull;
-                wh[v] = k < nd ? D.w_hi[deo + e[v]] : 0ull;
+                const uint32_t k = k0 + (uint32_t)v * BS;
+                x[v] = load_edge(Dn, k < nd ? k : 0u);
             }
 #pragma unroll
             for (int v = 0; v < 2; ++v) {
-                if (k0 + (uint32_t)v * kLP >= nd) break;
-                const uint32_t sl = meta_ch(m[v]) * 2u * Bm + meta_idx(m[v]);
+                if (k0 + (uint32_t)v * BS >= nd) break;
+                const uint32_t sl = meta_ch(x[v].meta) * 2u * Bm + meta_idx(x[v].meta);
                 // dx.y holds the dense side's share of the first-insert time t = i |B.E| + j
-                const uint32_t te = denseA ? e[v] * nB : e[v];
+                const uint32_t te = x[v].e * tmulD;
                 if (atomicCAS(&dx[sl].y, kInf, te) != kInf) {
                     *dup = 1;
                 } else {   // canonical operands: the limb split needs a, b < 2^127
                     uint32_t l[5];
-                    fp_split26(fp_canon(wl[v], wh[v]), l);
+                    fp_split26(fp_canon(x[v].lo, x[v].hi), l);
                     dl4[sl] = dl4[sl + Bm] = make_uint4(l[0], l[1], l[2], l[3]);
                     dx[sl].x = l[4];
                     dx[sl + Bm] = make_uint2(l[4], te);
@@ -262,9 +531,9 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
         __syncthreads();
         dense = *dup == 0;   // duplicate (layer, idx, ch) edges: use the scatter mode instead
         if (dense) {
-            const uint32_t rows = (Bm + kLP - 1) / kLP;   // workgroup-uniform (1 for B <= 384)
+            const uint32_t rows = (Bm + BS - 1) / BS;   // workgroup-uniform (1 for B <= BS)
             for (uint32_t u = 0; u < rows; ++u) {
-                const uint32_t r = tid + u * kLP;
+                const uint32_t r = tid + u * BS;
                 const bool live = r < Bm;
                 const uint4* dl4r = dl4 + (live ? r : 0u);
                 const uint2* dxr = dx + (live ? r : 0u);
@@ -278,17 +547,16 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                     if ((uint32_t)tid < cn) {
                         const uint32_t k = (uint32_t)tid;
                         const bool first = u == 0 && c0 == 0;   // prefetched above
-                        const uint32_t e = first ? pe : sids[c0 + k];
-                        const uint64_t m = first ? pmeta : Sp.meta[seo + e];
+                        const edge_rec x = first ? pr0 : load_edge(Sp, c0 + k);
                         uint32_t l[5];
-                        fp_split26(fp_canon(first ? plo : Sp.w_lo[seo + e], first ? phi : Sp.w_hi[seo + e]), l);
+                        fp_split26(fp_canon(x.lo, x.hi), l);
                         sl4[k] = make_uint4(l[0], l[1], l[2], l[3]);
                         sl1[k] = l[4];
                         // wave-uniform offsets of the P and M slots relative to lane r: the dense
                         // channel equal to the sparse one gives P, the other M
-                        const uint32_t sidx = meta_idx(m), sch = meta_ch(m);
+                        const uint32_t sidx = meta_idx(x.meta), sch = meta_ch(x.meta);
                         sinf[k] = (sch * 2u * Bm + Bm - sidx) | (((sch ^ 1u) * 2u * Bm + Bm - sidx) << 16);
-                        sidv[k] = denseA ? e : e * nB;   // the sparse side's share of t
+                        sidv[k] = x.e * tmulS;   // the sparse side's share of t
                     }
                     __syncthreads();
                     if (live) {
@@ -331,27 +599,26 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
     if (!dense) {
         unsigned long long* acc = (unsigned long long*)plds;
         uint32_t* tk = (uint32_t*)(plds + 48u * Bm);
-        for (uint32_t k = tid; k < 6 * Bm; k += kLP) acc[k] = 0ull;
-        for (uint32_t k = tid; k < Bm; k += kLP) tk[k] = kInf;
+        for (uint32_t k = tid; k < 6 * Bm; k += BS) acc[k] = 0ull;
+        for (uint32_t k = tid; k < Bm; k += BS) tk[k] = kInf;
         __syncthreads();
         const uint64_t np = (uint64_t)na * nb;
-        for (uint64_t t = tid; t < np; t += kLP) {
+        for (uint64_t t = tid; t < np; t += BS) {
             const uint32_t ai = (uint32_t)(t / nb), bj = (uint32_t)(t - (uint64_t)ai * nb);
-            const uint32_t i = idsA[ai], j = idsB[bj];
-            const uint64_t ma = g.A.meta[aeo + i], mb = g.B.meta[beo + j];
-            const uint32_t r = mod_small(meta_idx(ma) + meta_idx(mb), Bm);
-            const uint32_t chn = meta_ch(ma) ^ meta_ch(mb);
-            const fp pv = fp_mul(fp{g.A.w_lo[aeo + i], g.A.w_hi[aeo + i]}, fp{g.B.w_lo[beo + j], g.B.w_hi[beo + j]});
+            const edge_rec xa = load_edge(srcA, ai), xb = load_edge(srcB, bj);
+            const uint32_t r = mod_small(meta_idx(xa.meta) + meta_idx(xb.meta), Bm);
+            const uint32_t chn = meta_ch(xa.meta) ^ meta_ch(xb.meta);
+            const fp pv = fp_mul(fp{xa.lo, xa.hi}, fp{xb.lo, xb.hi});
             uint64_t l0, l1, l2;
             fp_split3(pv, l0, l1, l2);
             unsigned long long* q = acc + (size_t)(r * 2 + chn) * 3;
             atomicAdd(q + 0, (unsigned long long)l0);
             atomicAdd(q + 1, (unsigned long long)l1);
             atomicAdd(q + 2, (unsigned long long)l2);
-            atomicMin(&tk[r], i * nB + j);
+            atomicMin(&tk[r], xa.e * nB + xb.e);
         }
         __syncthreads();
-        for (uint32_t r = tid; r < Bm; r += kLP) {
+        for (uint32_t r = tid; r < Bm; r += BS) {
             const uint64_t s = slot0 + r;
             const uint32_t tkr = tk[r];
             tkey[s] = tkr;
@@ -367,8 +634,122 @@ __global__ __launch_bounds__(kLP) void k_large_products(mul_large_args g) {
                 if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tkr, __popc(eb));
             }
         }
+        __syncthreads();   // the caller may reuse the LDS
     }
     if (any) S[d.o_used + (LA + LB) + lp] = 1;   // benign race: every writer stores 1
+}
+
+// one workgroup per task (la, lb): pairs with many B layers (squares)
+template <int BS, bool MX>
+__global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
+    const large_desc& d = g.desc[g.sel[g.n_la + blockIdx.y]];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const uint32_t LB = d.LB;
+    const uint32_t tl = blockIdx.x;
+    const uint32_t la_i = tl / LB, lb_i = tl - la_i * LB;
+    if (la_i >= cnt[0] || lb_i >= cnt[1]) return;
+    run_task<BS, MX>(g, d, S[d.o_neA + la_i], S[d.o_neB + lb_i], plds);
+}
+
+// One workgroup per (pair, kLaPerWG A layers) for pairs with at most kLaMaxLB B layers (chain
+// steps): the B layers' sparse sides are staged once per workgroup and each A layer's dense table
+// once for all B layers, so a chain step reads every A edge once (a task per workgroup read it
+// |B.L| times) and pays the dependent header loads once per kLaPerWG x |B.L| tasks. The kernel is
+// latency-bound: 4 workgroups per CU (<= 128 VGPRs, 32 KB of LDS) against 3: -10%; forced to 96
+// VGPRs for 5 per CU it was 28% slower.
+// Tasks the matrix-core mode does not take: sparse x sparse (and layers with duplicate edges) run
+// the scatter mode in place; dense tasks with a large sparse side (column mode, 33 KB of LDS) go to
+// a per-pair list for k_large_products_defer.
+#ifndef PVAC_LA_MINB   // resident workgroups per CU the A-layer-major kernel is compiled for
+#define PVAC_LA_MINB 4
+#endif
+template <int BS>
+__global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
+    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const uint32_t neA = cnt[0], neB = min(cnt[1], kLaMaxLB);   // the host sends pairs with |B.L| <= kLaMaxLB
+    const uint32_t i0 = blockIdx.x * kLaPerWG;
+    if (i0 >= neA) return;
+    const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
+    uint8_t* sreg = plds + g.lds_task;   // per B layer: prec | pinf
+    uint32_t lbv[kLaMaxLB], nbv[kLaMaxLB];
+    uint32_t okm = 0;   // B layers staged as MX sparse sides
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) {
+        lbv[k] = 0;
+        nbv[k] = 0;
+        if (k < neB) {
+            const uint32_t lb = S[d.o_neB + k];
+            const layer_src srcB = side_layer(&g.B, g.B.e_off[d.pair], S, d.o_lstB, LB, lb);
+            lbv[k] = lb;
+            nbv[k] = srcB.n;
+            if (srcB.n <= kMxMaxSparse) {
+                okm |= 1u << k;
+                uint4* prec = (uint4*)(sreg + k * kMxSparseBytes);
+                mx_stage_sparse(prec, prec + 3u * kMxMaxSparse, Bm, srcB, 1u, threadIdx.x);
+            }
+        }
+    }
+    const task_out o{S + d.o_tkey, S + d.o_info, (ulonglong2*)(S + d.o_sums), group_heads(g, d),
+                     (unsigned long long*)w64(S, d.o_bmask)};
+    const uint32_t i1 = min(neA, i0 + kLaPerWG);
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t la = S[d.o_neA + i];
+        const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
+        const uint32_t na = srcA.n;
+        uint32_t mxm = 0;   // B layers whose task with this A layer runs on the matrix cores
+        bool dupA = false;
+        if (na >= kLargeDenseMin)
+#pragma unroll
+            for (uint32_t k = 0; k < kLaMaxLB; ++k)
+                if (((okm >> k) & 1u) && na >= nbv[k]) mxm |= 1u << k;
+        if (mxm) {
+            if (mx_stage_dense<BS>(plds, Bm, srcA, nB)) {   // barriers inside (they also publish the B staging)
+#pragma unroll
+                for (uint32_t k = 0; k < kLaMaxLB; ++k) {
+                    if (!((mxm >> k) & 1u)) continue;
+                    const uint4* prec = (const uint4*)(sreg + k * kMxSparseBytes);
+                    const uint32_t lp = la * LB + lbv[k];
+                    if (mx_blocks<BS>(plds, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, (uint64_t)lp * Bm, o))
+                        S[d.o_used + (LA + LB) + lp] = 1;
+                }
+            } else {
+                mxm = 0;   // duplicate edges in this A layer: its tasks take run_task's scatter mode
+                dupA = true;
+            }
+            __syncthreads();
+        }
+        for (uint32_t k = 0; k < neB; ++k) {
+            if ((mxm >> k) & 1u) continue;
+            if (!dupA && max(na, nbv[k]) >= kLargeDenseMin) {
+                if (threadIdx.x == 0) S[d.o_defer + atomicAdd((uint32_t*)cnt + 7, 1u)] = i << 16 | k;
+            } else {
+                run_task<BS, false>(g, d, la, lbv[k], plds, false);   // scatter mode
+            }
+        }
+    }
+}
+
+// the column-mode tasks k_large_products_la deferred: kDeferWG workgroups per pair walk its list
+constexpr uint32_t kDeferWG = 4;
+template <int BS>
+__global__ __launch_bounds__(BS) void k_large_products_defer(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
+    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const uint32_t nq = cnt[7];
+    for (uint32_t q = blockIdx.x; q < nq; q += kDeferWG) {
+        const uint32_t v = S[d.o_defer + q];
+        run_task<BS, false>(g, d, S[d.o_neA + (v >> 16)], S[d.o_neB + (v & 0xFFFFu)], plds);
+    }
 }
 
 // ---------------------------------------------------------------- compact_layers + layer records
@@ -740,7 +1121,29 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     hipLaunchKernelGGL(k_large_init, dim3(grid_x(a.max_zero > a.max_S ? a.max_zero : a.max_S, kLB * 4, 4096), nl),
                        dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_lists, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
-    hipLaunchKernelGGL(k_large_products, dim3((unsigned)a.max_tasks, nl), dim3(kLP), plds, st, a);
+    // products: the matrix-core dense mode in 4-wave workgroups (A-layer-major for pairs with few B
+    // layers, one task per workgroup for the rest) unless PVAC_LARGE_PRODUCTS=col26 selects the
+    // column-accumulator kernel of round 2 for every pair (A/B runs)
+    static const bool col26_only = [] {
+        const char* e = std::getenv("PVAC_LARGE_PRODUCTS");
+        return e && std::strcmp(e, "col26") == 0;
+    }();
+    if (col26_only) {
+        mul_large_args b = a;
+        b.n_la = 0;
+        hipLaunchKernelGGL((k_large_products<kLP, false>), dim3((unsigned)a.max_tasks_all, nl), dim3(kLP), plds, st, b);
+    } else {
+        const size_t lx = std::max<size_t>(plds, mx_lds_bytes(a.Bm) + kMxSparseBytes);
+        if (nl > a.n_la && a.max_tasks)
+            hipLaunchKernelGGL((k_large_products<kLPX, true>), dim3((unsigned)a.max_tasks, nl - a.n_la), dim3(kLPX), lx, st, a);
+        if (a.n_la && a.max_la_wg) {
+            mul_large_args b = a;
+            b.lds_task = mx_lds_bytes(a.Bm);   // the scatter mode (52 B per slot) fits below it
+            hipLaunchKernelGGL((k_large_products_la<kLPX>), dim3((unsigned)a.max_la_wg, a.n_la), dim3(kLPX),
+                               (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes, st, b);
+            hipLaunchKernelGGL((k_large_products_defer<kLPX>), dim3(kDeferWG, a.n_la), dim3(kLPX), plds, st, a);
+        }
+    }
     hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
     const unsigned gs = grid_x(a.max_S, kLB * 2, 4096);
     hipLaunchKernelGGL(k_large_link, dim3(gs, nl), dim3(kLB), 0, st, a);

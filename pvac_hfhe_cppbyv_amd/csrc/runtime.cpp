@@ -84,6 +84,9 @@ struct pvac_hip_ctx {
     uint64_t redo_total = 0;           // pairs re-run by redo_fresh_pairs since the context was created
     large_desc* desc_dev = nullptr;
     size_t desc_cap = 0;
+    uint32_t* sel_dev = nullptr;       // products: descriptor order per sub-batch (A-layer-major class first)
+    size_t sel_cap = 0;
+    std::vector<uint32_t> sel_host;
     uint32_t* arena = nullptr;
     size_t arena_words = 0;
     // static bucket-group tables of the last plan (one per distinct bucket count) + build scratch
@@ -269,6 +272,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.o_lstB = o; o += 2 * LB + nB;
     d.o_neA = o; o += LA;
     d.o_neB = o; o += LB;
+    d.o_defer = o; o += LA * LB <= kLaMaxLB * LA ? LA * LB : 0;   // A-layer-major pairs only
     d.o_info = o; o += d.S;
     quad();
     d.o_sums = o; o += 8 * d.S;
@@ -286,7 +290,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
 
 void rebase_desc(large_desc& d, uint64_t base) {
     uint64_t* f[] = {&d.o_zero, &d.o_cnt, &d.o_hkey, &d.o_hhead, &d.o_bmask, &d.o_bcnt, &d.o_used, &d.o_tkey,
-                     &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
+                     &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_defer, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
                      &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos};
     for (uint64_t* p : f) *p += base;
 }
@@ -347,6 +351,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->redo_ids);
     hipFree(c->redo_cnt);
     hipFree(c->desc_dev);
+    hipFree(c->sel_dev);
     hipFree(c->arena);
     hipFree(c->grp);
     hipFree(c->grp_tmp);
@@ -579,7 +584,9 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
               pvac_ct_batch* C, uint32_t flags, uint32_t* salt_pos) {
     const size_t nl = c->large_host.size();
     int rc = ensure_dev(c, c->desc_dev, c->desc_cap, nl, "alloc large descriptors");
+    if (!rc) rc = ensure_dev(c, c->sel_dev, c->sel_cap, nl, "alloc large descriptor order");
     if (rc) return rc;
+    c->sel_host.resize(nl);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
     uint64_t budget = std::max<uint64_t>((uint64_t)(free_b / 2) / 4 + c->arena_words, 1ull << 24);
@@ -589,7 +596,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
     while (i < nl) {
         uint64_t words = 0;
         size_t j = i;
-        uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0;
+        uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0;
         while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
             large_desc& d = c->large_exec[j];
             const uint64_t w = d.words;
@@ -597,10 +604,24 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             words += w;
             mS = std::max(mS, d.S);
             mZ = std::max(mZ, d.zero_words);
-            mT = std::max<uint64_t>(mT, (uint64_t)d.LA * d.LB);
             mE = std::max(mE, d.capE);
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
+        }
+        // products: pairs with few B layers (chain steps) take the A-layer-major kernel
+        uint32_t n_la = 0;
+        for (size_t k = i; k < j; ++k)
+            if (c->large_exec[k].LB <= kLaMaxLB) c->sel_host[i + n_la++] = (uint32_t)(k - i);
+        for (size_t k = i, q = n_la; k < j; ++k) {
+            const large_desc& d = c->large_exec[k];
+            const uint64_t tasks = (uint64_t)d.LA * d.LB;
+            mTa = std::max(mTa, tasks);
+            if (d.LB <= kLaMaxLB) {
+                mLa = std::max<uint64_t>(mLa, (d.LA + kLaPerWG - 1) / kLaPerWG);
+            } else {
+                mT = std::max(mT, tasks);
+                c->sel_host[i + q++] = (uint32_t)(k - i);
+            }
         }
         if (words > c->arena_words) {
             // grow with 1/8 headroom (within the budget): batches of similar pairs differ by a few
@@ -621,6 +642,9 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         }
         hipError_t e = hipMemcpyAsync(c->desc_dev + i, c->large_exec.data() + i, (j - i) * sizeof(large_desc),
                                       hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->sel_dev + i, c->sel_host.data() + i, (j - i) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "upload large descriptors");
         mul_large_args a{};
         a.A = *A; a.B = *B; a.C = *C;
@@ -635,7 +659,10 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.flags = flags;
         a.salt_pos = salt_pos;
         a.grp = c->grp;
+        a.sel = c->sel_dev + i;
+        a.n_la = n_la;
         a.max_S = mS; a.max_zero = mZ; a.max_tasks = mT; a.max_capE = mE; a.max_lay = mL;
+        a.max_tasks_all = mTa; a.max_la_wg = mLa;
         e = launch_ct_mul_large(a, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "ct_mul_large");
         i = j;
