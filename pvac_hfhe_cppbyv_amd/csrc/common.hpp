@@ -298,12 +298,15 @@ struct mul_large_args {
     const uint32_t* grp;         // static bucket-group tables (large_desc::g_head / g_next)
     const uint32_t* sel;         // [nl] descriptor indices, A-layer-major class first
     uint32_t lds_task;           // k_large_products_la: bytes of LDS below its staged B layers (set at launch)
+    uint32_t la_per_wg;          // k_large_products_la: A layers per workgroup (max_la_wg = ceil(|A.L| / it))
+    uint32_t la_xcd;             // k_large_products_la: 1 = all workgroups of a pair on one XCD (grid y padded to 8)
     uint32_t pad;
     // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all
     // over all, max_la_wg = ceil(|A.L| / kLaPerWG) over the A-layer-major class)
     uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg;
 };
-// k_large_products_la: A layers per workgroup; pairs with at most kLaMaxLB B layers take it
+// k_large_products_la: A layers per workgroup (default; PVAC_LA_PER_WG); pairs with at most
+// kLaMaxLB B layers take it
 constexpr uint32_t kLaPerWG = 4;
 constexpr uint32_t kLaMaxLB = 4;
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);

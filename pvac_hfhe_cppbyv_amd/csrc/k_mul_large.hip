@@ -208,6 +208,11 @@ typedef int mx_v16 __attribute__((ext_vector_type(16)));
 constexpr int kMxKS = 10;                          // k-steps held in registers: 2 sparse edges each
 constexpr uint32_t kMxMaxSparse = 2u * kMxKS;      // sparse sides up to this size take the MFMA path
 constexpr uint64_t kDigC = 0x8080808080808080ull;  // 128 in every byte
+#ifdef PVAC_ASM_MARKS   // ISA census builds only (tools/asm_phases.py)
+#define MXMARK(ph) asm volatile("; PVAC_MARK " #ph ::: "memory")
+#else
+#define MXMARK(ph) do {} while (0)
+#endif
 #ifndef PVAC_EXP_MXREP   // experiment builds only: the MFMA loop run this many times (same result)
 #define PVAC_EXP_MXREP 1
 #endif
@@ -223,19 +228,20 @@ __device__ __forceinline__ void fp_digits8(const fp& v, uint64_t& dl, uint64_t& 
     dh = uh ^ kDigC;
 }
 
-// the four 4-position groups of a lane's 16 column sums: g[q] = sum_i c[4q + i] 256^i, at bit
-// 64 q + 32 h of the row's value (|g| < 2^47)
-__device__ __forceinline__ void mx_groups(const mx_v16& c, int64_t* g) {
+// A lane's 16 column sums c[i] sit at digit positions k(i) = (i & 3) + 8 (i >> 2) + 4 h, and
+// k(i + 8) = k(i) + 16: 256^16 = 2^128 == 2 (mod p), so d[i] = c[i] + 2 c[i + 8] (32-bit, |d| < 2^24
+// for <= 20 sparse edges) leaves positions 4h..4h+3 (d[0..3]) and 8+4h..11+4h (d[4..7]), i.e. the
+// 32-bit words h and 2 + h of the row's value: ga, gb (|g| < 2^48.1).
+__device__ __forceinline__ void mx_groups(const mx_v16& c, int64_t& ga, int64_t& gb) {
+    int32_t d[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        g[q] = (int64_t)c[4 * q] + (int64_t)c[4 * q + 1] * 256 + (int64_t)c[4 * q + 2] * 65536 +
-               (int64_t)c[4 * q + 3] * 16777216;
+    for (int i = 0; i < 8; ++i) d[i] = c[i] + 2 * c[i + 8];
+    ga = (int64_t)d[0] + (int64_t)d[1] * 256 + (int64_t)d[2] * 65536 + (int64_t)d[3] * 16777216;
+    gb = (int64_t)d[4] + (int64_t)d[5] * 256 + (int64_t)d[6] * 65536 + (int64_t)d[7] * 16777216;
 }
 
-// Z = sum_q (glo[q] + ghi[q] 2^32) 2^(64 q) mod p, canonical. 2^128 == 2 and 2^127 == 1 (mod p).
-__device__ __forceinline__ fp mx_fold(const int64_t* glo, const int64_t* ghi) {
-    const int64_t a0 = glo[0] + 2 * glo[2], a1 = ghi[0] + 2 * ghi[2];   // bits 0, 32
-    const int64_t b0 = glo[1] + 2 * glo[3], b1 = ghi[1] + 2 * ghi[3];   // bits 64, 96
+// Z = H0 + H1 2^32 + H2 2^64 + H3 2^96 mod p (|H| < 2^56), canonical. 2^128 == 2, 2^127 == 1 (mod p).
+__device__ __forceinline__ fp mx_fold(int64_t a0, int64_t a1, int64_t b0, int64_t b1) {
     // 32-bit words W0..W4 of Z; W4 2^128 == 2 W4 goes into W0
     int64_t t = (int64_t)(uint32_t)a0 + 2 * (b1 >> 32);
     const uint32_t x0 = (uint32_t)t;
@@ -372,18 +378,25 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
         }
     }
     const uint32_t nblk = (Bm + 31u) >> 5;
+    MXMARK(1);
     for (uint32_t blk = wave; blk < nblk; blk += BS / 64) {
+        MXMARK(2);
         const uint32_t r = blk * 32u + n;
         const bool live = r < Bm;
         const uint32_t rr = live ? r : 0u;
-        mx_v16 aP, aM;
-        uint32_t tmin;
+        mx_v16 aP{}, aM{};
+        uint32_t tmin = kInf;
         for (int rep_ = 0; rep_ < PVAC_EXP_MXREP; ++rep_) {   // experiment builds repeat the loop
             uint32_t rq = rr;
             asm volatile("" : "+v"(rq));
+            if (rep_) {   // keep the previous repetition live: add x - y where x == y at run time
+                int zp = aP[0], zm = aM[0];
+                asm volatile("" : "+v"(zp), "+v"(zm));
+                tmin += (uint32_t)(zp - aP[0]) + (uint32_t)(zm - aM[0]);
+            }
             aP = mx_v16{};
             aM = mx_v16{};
-            tmin = kInf;
+            tmin = min(tmin, kInf);
 #pragma unroll
             for (int s = 0; s < NKS; ++s) {
                 const uint4 in = pinf[2u * (uint32_t)s + h];
@@ -394,18 +407,15 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
                 tmin = min(tmin, min(__builtin_elementwise_add_sat(tp, in.z), __builtin_elementwise_add_sat(tm, in.z)));
             }
         }
-        // half 0 folds row r's P sum, half 1 its M sum; each needs the other half's groups
-        int64_t gp[4], gm[4], glo[4], ghi[4];
-        mx_groups(aP, gp);
-        mx_groups(aM, gm);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t oth = shfl_xor64(h ? gp[q] : gm[q], 32);
-            const int64_t own = h ? gm[q] : gp[q];
-            glo[q] = h ? oth : own;
-            ghi[q] = h ? own : oth;
-        }
-        const fp v = mx_fold(glo, ghi);
+        MXMARK(3);
+        // half 0 folds row r's P sum, half 1 its M sum; each needs the other half's two words
+        int64_t paw, pbw, maw, mbw;
+        mx_groups(aP, paw, pbw);
+        mx_groups(aM, maw, mbw);
+        const int64_t ra = shfl_xor64(h ? paw : maw, 32), rb = shfl_xor64(h ? pbw : mbw, 32);
+        MXMARK(4);
+        const fp v = mx_fold(h ? ra : paw, h ? maw : ra, h ? rb : pbw, h ? mbw : rb);
+        MXMARK(5);
         const uint32_t nz = fp_nonzero(v) ? 1u : 0u;
         const uint32_t nzo = (uint32_t)__shfl_xor((int)nz, 32);
         const uint32_t eb = h ? (nzo | nz << 1) : (nz | nzo << 1);
@@ -669,12 +679,19 @@ __global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
 template <int BS>
 __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
-    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    uint32_t py = blockIdx.y, px = blockIdx.x;
+    if (g.la_xcd) {   // workgroups go to XCDs round-robin by linear id: XCD x takes pairs x, x + 8, ...
+        const uint32_t lin = blockIdx.x + blockIdx.y * gridDim.x, k = lin >> 3;
+        py = (k / gridDim.x) * 8u + (lin & 7u);
+        px = k % gridDim.x;
+        if (py >= g.n_la) return;
+    }
+    const large_desc& d = g.desc[g.sel[py]];
     uint32_t* S = g.scratch;
     const uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
     const uint32_t neA = cnt[0], neB = min(cnt[1], kLaMaxLB);   // the host sends pairs with |B.L| <= kLaMaxLB
-    const uint32_t i0 = blockIdx.x * kLaPerWG;
+    const uint32_t i0 = px * g.la_per_wg;
     if (i0 >= neA) return;
     const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
     uint8_t* sreg = plds + g.lds_task;   // per B layer: prec | pinf
@@ -698,7 +715,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
     }
     const task_out o{S + d.o_tkey, S + d.o_info, (ulonglong2*)(S + d.o_sums), group_heads(g, d),
                      (unsigned long long*)w64(S, d.o_bmask)};
-    const uint32_t i1 = min(neA, i0 + kLaPerWG);
+    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
     for (uint32_t i = i0; i < i1; ++i) {
         const uint32_t la = S[d.o_neA + i];
         const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
@@ -710,6 +727,9 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
             for (uint32_t k = 0; k < kLaMaxLB; ++k)
                 if (((okm >> k) & 1u) && na >= nbv[k]) mxm |= 1u << k;
         if (mxm) {
+#ifdef PVAC_EXP_STAGE2   // experiment builds only: the dense staging twice (same result)
+            mx_stage_dense<BS>(plds, Bm, srcA, nB);
+#endif
             if (mx_stage_dense<BS>(plds, Bm, srcA, nB)) {   // barriers inside (they also publish the B staging)
 #pragma unroll
                 for (uint32_t k = 0; k < kLaMaxLB; ++k) {
@@ -1139,7 +1159,8 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
         if (a.n_la && a.max_la_wg) {
             mul_large_args b = a;
             b.lds_task = mx_lds_bytes(a.Bm);   // the scatter mode (52 B per slot) fits below it
-            hipLaunchKernelGGL((k_large_products_la<kLPX>), dim3((unsigned)a.max_la_wg, a.n_la), dim3(kLPX),
+            hipLaunchKernelGGL((k_large_products_la<kLPX>), dim3((unsigned)a.max_la_wg, a.la_xcd ? (a.n_la + 7u) & ~7u : a.n_la),
+                               dim3(kLPX),
                                (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes, st, b);
             hipLaunchKernelGGL((k_large_products_defer<kLPX>), dim3(kDeferWG, a.n_la), dim3(kLPX), plds, st, a);
         }

@@ -587,6 +587,16 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
     if (!rc) rc = ensure_dev(c, c->sel_dev, c->sel_cap, nl, "alloc large descriptor order");
     if (rc) return rc;
     c->sel_host.resize(nl);
+    // A/B knobs of k_large_products_la (environment, read once)
+    static const uint32_t la_per_wg = [] {
+        const char* e = std::getenv("PVAC_LA_PER_WG");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= 64 ? (uint32_t)v : kLaPerWG;
+    }();
+    static const uint32_t la_xcd = [] {
+        const char* e = std::getenv("PVAC_LA_XCD");
+        return e && e[0] == '1' ? 1u : 0u;
+    }();
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
     uint64_t budget = std::max<uint64_t>((uint64_t)(free_b / 2) / 4 + c->arena_words, 1ull << 24);
@@ -617,7 +627,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             const uint64_t tasks = (uint64_t)d.LA * d.LB;
             mTa = std::max(mTa, tasks);
             if (d.LB <= kLaMaxLB) {
-                mLa = std::max<uint64_t>(mLa, (d.LA + kLaPerWG - 1) / kLaPerWG);
+                mLa = std::max<uint64_t>(mLa, (d.LA + la_per_wg - 1) / la_per_wg);
             } else {
                 mT = std::max(mT, tasks);
                 c->sel_host[i + q++] = (uint32_t)(k - i);
@@ -663,6 +673,8 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.n_la = n_la;
         a.max_S = mS; a.max_zero = mZ; a.max_tasks = mT; a.max_capE = mE; a.max_lay = mL;
         a.max_tasks_all = mTa; a.max_la_wg = mLa;
+        a.la_per_wg = la_per_wg;
+        a.la_xcd = la_xcd;
         e = launch_ct_mul_large(a, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "ct_mul_large");
         i = j;
