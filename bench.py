@@ -932,16 +932,17 @@ def chain_bench(eng, args):
     out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
                                  "step, on the device (untimed)", "pair_steps": gp, "failed": gf,
                         "invariant_ok": gf == 0 and gp == n * depth, "check_seconds": check_s}
-    # ALU roofline: products per second against the column-accumulated product ceiling measured on
-    # this GPU (register-resident col26_mac probe, k_ubench.hip: the dense loop's own multiply, 25
-    # v_mad_u64_u32 per product); the fp_mul_fold1 ceiling of round 1 is reported beside it
+    # Roofline of the products: per second against the matrix-core ceiling measured on this GPU
+    # (k_ubench.hip k_probe_mfma8: back-to-back v_mfma_i32_32x32x32_i8, 64 dense-mode products
+    # each); the round-2 column-accumulator (col26_mac) and round-1 fp_mul_fold1 VALU ceilings
+    # beside it. The chain step is bound by memory latency and traffic, not by either.
     try:
-        ceil = eng.alu_ceiling(3)
-        out["roofline"] = {"bound": "valu", "achieved": products / chain_s, "peak": ceil, "unit": "products/s",
+        ceil = eng.alu_ceiling(5)
+        out["roofline"] = {"bound": "mfma", "achieved": products / chain_s, "peak": ceil, "unit": "products/s",
                            "frac": products / chain_s / ceil,
-                           "peak_source": "pvac_hip_alu_ceiling(3): register-resident col26_mac (two column "
-                                          "accumulators per lane), 8 waves/SIMD",
-                           "fold1_ceiling": eng.alu_ceiling(1)}
+                           "peak_source": "pvac_hip_alu_ceiling(5): back-to-back v_mfma_i32_32x32x32_i8 x 64 "
+                                          "products, 8 waves/SIMD",
+                           "col26_ceiling": eng.alu_ceiling(3), "fold1_ceiling": eng.alu_ceiling(1)}
     except Exception as ex:
         out["roofline"] = {"error": repr(ex)}
     if errors:

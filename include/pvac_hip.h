@@ -128,7 +128,8 @@ int pvac_hip_ctx_gen_H(pvac_hip_ctx* ctx, uint8_t digest_out[32]);
  * kind 0 = wave64 integer VALU instructions (v_mad_u64_u32 / v_add_co_u32 / v_alignbit_b32 mix),
  * 1 = lazy fp_mul_fold1 products, 2 = full fp_mul products, 3 = column-accumulated products
  * (col26_mac, the general path's dense loop), 4 = wave64 single-pass 32-bit VALU instructions
- * (v_add_u32 / v_xor_b32 / v_alignbit_b32: the issue ceiling of a mostly 32-bit VALU stream).
+ * (v_add_u32 / v_xor_b32 / v_alignbit_b32: the issue ceiling of a mostly 32-bit VALU stream),
+ * 5 = general-path dense-mode products on the matrix cores (v_mfma_i32_32x32x32_i8 rate x 64).
  * Synchronous. */
 int pvac_hip_alu_ceiling(pvac_hip_ctx* ctx, int kind, double* per_s);
 /* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */

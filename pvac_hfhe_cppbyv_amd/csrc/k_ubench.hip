@@ -162,6 +162,27 @@ __global__ __launch_bounds__(kUB) void k_probe_col26(uint64_t* out, uint32_t ite
     out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = r;
 }
 
+// the matrix-core product ceiling of the general path's dense mode (k_mul_large.hip): back-to-back
+// v_mfma_i32_32x32x32_i8 on four independent accumulators per wave; one such MFMA is 64 Fp
+// products there (32 output rows x 2 sparse edges, 16 x 16 digit pairs each)
+typedef int pb_v4 __attribute__((ext_vector_type(4)));
+typedef int pb_v16 __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(kUB) void k_probe_mfma8(uint64_t* out, uint32_t iters, uint32_t seed) {
+    const int s = (int)((threadIdx.x ^ seed) * 2654435761u + blockIdx.x);
+    const pb_v4 a{s, s >> 3, s >> 5, s >> 7}, b{s >> 11, s >> 13, s >> 17, s >> 19};
+    pb_v16 c0{}, c1{}, c2{}, c3{};
+    for (uint32_t i = 0; i < iters; ++i) {
+        c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, a, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, a, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, b, c3, 0, 0, 0);
+    }
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r ^= c0[k] ^ c1[k] ^ c2[k] ^ c3[k];
+    out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = (uint32_t)r;
+}
+
 }  // namespace
 
 // ops per second of probe `kind` (see above), timed with HIP events on `st` (synchronises)
@@ -173,7 +194,7 @@ hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s) {
     hipEvent_t t0, t1;
     hipEventCreate(&t0);
     hipEventCreate(&t1);
-    const uint32_t iters = kind == 0 || kind == 4 ? 4096u : 512u;
+    const uint32_t iters = kind == 0 || kind == 4 || kind == 5 ? 4096u : 512u;
     double ops = 0;
     float ms = 0;
     for (int rep = 0; rep < 2; ++rep) {   // the first launch warms clocks and code
@@ -190,6 +211,9 @@ hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s) {
         } else if (kind == 3) {
             hipLaunchKernelGGL(k_probe_col26, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
             ops = (double)blocks * kUB * iters * 2.0;           // lane products
+        } else if (kind == 5) {
+            hipLaunchKernelGGL(k_probe_mfma8, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
+            ops = (double)blocks * (kUB / 64) * iters * 4.0 * 64.0;   // dense-mode products (64 per MFMA)
         } else {
             hipLaunchKernelGGL(k_probe_mul<true>, dim3(blocks), dim3(kUB), 0, st, buf, iters, 0x5EEDu + rep);
             ops = (double)blocks * kUB * iters * 4.0;

@@ -1188,7 +1188,7 @@ int pvac_hip_base_R(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* R_out) {
 
 // ---------------------------------------------------------------- measured ALU ceilings
 int pvac_hip_alu_ceiling(pvac_hip_ctx* c, int kind, double* per_s) {
-    if (!c || !per_s || kind < 0 || kind > 4) return fail(c, PVAC_EINVAL, "alu_ceiling: bad arguments");
+    if (!c || !per_s || kind < 0 || kind > 5) return fail(c, PVAC_EINVAL, "alu_ceiling: bad arguments");
     const hipError_t e = run_alu_probe(kind, c->num_cus, c->stream, per_s);
     return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "alu_ceiling");
 }
