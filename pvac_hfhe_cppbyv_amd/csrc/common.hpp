@@ -248,13 +248,19 @@ struct large_desc {
     uint64_t capE;               // 2 min(n, S) output edge capacity
     fastmod64 nbm;               // libstdc++ bucket count after reserve(n)
     uint32_t LA, LB, nA, nB;
-    uint32_t hbits, pad;         // bucket hash table capacity = 2^hbits >= 2 S (dynamic chains only)
+    uint32_t hbits;              // bucket hash table capacity = 2^hbits >= 2 S (dynamic chains only)
+    // 1: emit order from per-A-edge counts (o_icnt) instead of the n/16 block marks (o_bmask): static
+    // bucket groups, A-layer-major products, 1 <= |B.E| <= 63. The pair falls back to the block marks
+    // (cnt[kCntIFail]) when a B layer is too big for the matrix-core mode or an A layer cannot be
+    // staged as a dense table
+    uint32_t iblk;
     // static bucket groups (bucket_count >= 2 S): per-slot chain head / next of the slots sharing
     // a libstdc++ bucket, word offsets into mul_large_args::grp (kNoGrp: dynamic chains via link)
     uint64_t g_head, g_next;
     // zero-initialised block [o_zero, o_zero + zero_words): cnt | hkey | hhead | bmask | bcnt | used
     uint64_t o_zero, zero_words;
-    uint64_t o_cnt;              // [8] neA, neB, invalid, total edges, canonical, A / B id allocation, deferred tasks
+    uint64_t o_cnt;              // [16] neA, neB, invalid, total edges, canonical, A / B id allocation, deferred tasks,
+                                 // [kCntIFail] per-A-edge order abandoned (iblk pairs)
     uint64_t o_hkey;             // [2^hbits] u64 bucket ids + 1
     uint64_t o_hhead;            // [2^hbits] chain heads (slot + 1)
     uint64_t o_bmask;            // [nblk] u64 per 16 first-insert times: bucket-leader edge codes (2 bits
@@ -278,6 +284,8 @@ struct large_desc {
     uint64_t o_cpos;             // [S] canonical positions (guard_budget order)
     uint64_t o_order;            // [capE] emit order: slot << 1 | ch
     uint64_t o_hpos;             // [capE] hash-order index of each canonical-order edge
+    uint64_t o_icnt;             // [nA] iblk: edges whose emit time lies in A edge i's product range
+                                 // [i |B.E|, (i + 1) |B.E|), then their exclusive suffix offset
     uint64_t words;              // end of this pair's scratch (absolute)
 };
 
@@ -319,6 +327,9 @@ hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, con
                              const uint64_t* powg, uint32_t Bm, const unsigned int* mx_host, uint32_t* status,
                              unsigned long long* n_bad, int num_cus, hipStream_t st);
 constexpr uint64_t kNoGrp = ~0ull;
+constexpr uint32_t kCntWords = 16;    // large_desc::o_cnt words
+constexpr uint32_t kCntIFail = 8;     // cnt word: an iblk pair uses the block marks after all
+constexpr uint32_t kIblkMaxNB = 63;   // iblk: |B.E| <= 63 (a 64-bit mask per A edge, bit 63 a flag)
 // static bucket groups of key slots [0, S) for one bucket count: head[s] = 0 when s is alone in
 // its bucket, else the first slot + 1 of the bucket's chain; next[s] = the following slot + 1
 // (0 ends). tmp_key / tmp_head: 2^hbits entries, zeroed by the caller.

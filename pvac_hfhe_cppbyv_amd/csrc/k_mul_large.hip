@@ -43,6 +43,7 @@ namespace pvhip {
 namespace {
 
 constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr uint32_t kIblkMaxSparse = 20;   // == kMxMaxSparse: B layers the matrix-core mode takes
 constexpr int kLB = 256;            // threads per workgroup (task / grid-stride kernels)
 constexpr int kLBig = 1024;         // threads per workgroup (per-pair kernels)
 
@@ -69,12 +70,15 @@ __device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* part
 }
 
 // ---------------------------------------------------------------- init
+// iblk pairs leave the block marks alone (k_large_layers clears them for a pair that falls back):
+// only cnt and the used flags are zeroed (static groups have no bucket table)
 __global__ __launch_bounds__(kLB) void k_large_init(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.y];
     const uint64_t stride = (uint64_t)gridDim.x * kLB;
-    const uint64_t lim = d.zero_words > d.S ? d.zero_words : d.S;
+    const uint64_t nz = d.iblk ? kCntWords + d.Lc : d.zero_words;
+    const uint64_t lim = nz > d.S ? nz : d.S;
     for (uint64_t w = (uint64_t)blockIdx.x * kLB + threadIdx.x; w < lim; w += stride) {
-        if (w < d.zero_words) g.scratch[d.o_zero + w] = 0;
+        if (w < nz) g.scratch[d.iblk && w >= kCntWords ? d.o_used + (w - kCntWords) : d.o_zero + w] = 0;
         if (w < d.S) g.scratch[d.o_tkey + w] = kInf;
     }
 }
@@ -121,6 +125,7 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     // layer ranges by atomic allocation; non-empty layer lists by atomic append
     for (uint32_t l = tid; l < LA + LB; l += kLBig) {
         const uint32_t c = hist[l];
+        if (d.iblk && l >= LA && c > kIblkMaxSparse) cnt[kCntIFail] = 1;   // its tasks would be deferred
         const bool a = l < LA;
         uint32_t* lst = a ? S + d.o_lstA : S + d.o_lstB;
         const uint32_t ll = a ? l : l - LA;
@@ -207,6 +212,7 @@ typedef int mx_v4 __attribute__((ext_vector_type(4)));
 typedef int mx_v16 __attribute__((ext_vector_type(16)));
 constexpr int kMxKS = 10;                          // k-steps held in registers: 2 sparse edges each
 constexpr uint32_t kMxMaxSparse = 2u * kMxKS;      // sparse sides up to this size take the MFMA path
+static_assert(kMxMaxSparse == kIblkMaxSparse, "iblk pairs need every B layer on the matrix cores");
 constexpr uint64_t kDigC = 0x8080808080808080ull;  // 128 in every byte
 #ifdef PVAC_ASM_MARKS   // ISA census builds only (tools/asm_phases.py)
 #define MXMARK(ph) asm volatile("; PVAC_MARK " #ph ::: "memory")
@@ -276,6 +282,7 @@ __device__ __forceinline__ int64_t shfl_xor64(int64_t v, int mask) {
 // pinf[kMxMaxSparse] (uint4: P and M slot offsets relative to row r, the sparse side's share of t)
 __host__ __device__ inline uint32_t mx_lds_bytes(uint32_t Bm) { return al16(80u * Bm + 4u); }
 constexpr uint32_t kMxSparseBytes = 64u * kMxMaxSparse;
+constexpr uint32_t kIblkBjtBytes = 4u * 64u;       // k_large_products_la: B edge table of iblk pairs
 
 // the dense side of a task into dig / tt. Every thread calls it; barriers inside; false
 // (workgroup-uniform) when the layer holds duplicate (idx, ch) edges
@@ -427,7 +434,7 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
                 o.sums[2 * s + h] = make_ulonglong2(v.lo, v.hi);
                 if (h == 0) {
                     o.info[s] = eb;
-                    if (eb && o.ghead && o.ghead[s] == 0u) leader_mark(o.bpack, tmin, __popc(eb));
+                    if (eb && o.bpack && o.ghead && o.ghead[s] == 0u) leader_mark(o.bpack, tmin, __popc(eb));
                 }
                 any |= eb != 0;
             }
@@ -481,7 +488,9 @@ __device__ void run_task(const mul_large_args& g, const large_desc& d, uint32_t 
     // keys alone in their bucket are their own bucket leaders: mark them here, where the atomic
     // overlaps the multiply-bound loop of other waves, and `rank` skips them
     const uint32_t* ghead = group_heads(g, d);
-    unsigned long long* bpack = (unsigned long long*)w64(S, d.o_bmask);
+    // iblk pairs: no block marks here (k_large_products_la counts per A edge; a pair that falls back
+    // has its lone leaders marked by k_large_rank)
+    unsigned long long* bpack = d.iblk ? nullptr : (unsigned long long*)w64(S, d.o_bmask);
     bool any = false;
 
     bool dense = col26_ok && nd >= kLargeDenseMin;
@@ -599,7 +608,7 @@ __device__ void run_task(const mul_large_args& g, const large_desc& d, uint32_t 
                         sums[2 * s] = make_ulonglong2(ps.lo, ps.hi);
                         sums[2 * s + 1] = make_ulonglong2(ms.lo, ms.hi);
                         any |= eb != 0;
-                        if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tmin, __popc(eb));
+                        if (eb && bpack && ghead && ghead[s] == 0u) leader_mark(bpack, tmin, __popc(eb));
                     }
                 }
             }
@@ -641,7 +650,7 @@ __device__ void run_task(const mul_large_args& g, const large_desc& d, uint32_t 
                 sums[2 * s] = make_ulonglong2(p.lo, p.hi);
                 sums[2 * s + 1] = make_ulonglong2(m.lo, m.hi);
                 any |= eb != 0;
-                if (eb && ghead && ghead[s] == 0u) leader_mark(bpack, tkr, __popc(eb));
+                if (eb && bpack && ghead && ghead[s] == 0u) leader_mark(bpack, tkr, __popc(eb));
             }
         }
         __syncthreads();   // the caller may reuse the LDS
@@ -662,6 +671,102 @@ __global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
     const uint32_t la_i = tl / LB, lb_i = tl - la_i * LB;
     if (la_i >= cnt[0] || lb_i >= cnt[1]) return;
     run_task<BS, MX>(g, d, S[d.o_neA + la_i], S[d.o_neB + lb_i], plds);
+}
+
+// ---- per-A-edge emit order (iblk pairs) ---------------------------------------------------
+// The reference emits keys in hash-list order: bucket first-insert time DESC, then key time DESC
+// (see k_mul_fresh.hip). A first-insert time t = i |B.E| + j names A edge i and B edge j, and the
+// key lies in product layer (layer(i), layer(j)): every key whose time falls in A edge i's range
+// [i |B.E|, (i + 1) |B.E|) belongs to ONE A layer, which one k_large_products_la workgroup
+// multiplies against every B layer. So that workgroup can count the edges of A edge i's keys and
+// rank each key among them (by j DESC) in LDS; a suffix scan over the |A.E| counts then gives
+// every key's position: offset(i) + rank. This replaces the n/16-word block marks (zeroed, marked
+// with random 64-bit atomics, scanned and read back at random: k_large_init / products / scan /
+// order) with |A.E| plain counts. Keys that share a libstdc++ bucket with another slot of the
+// static group (a few percent) are emitted at their bucket leader's time: k_large_rank moves their
+// edges from their own A edge's count to the leader's, and every A edge range holding such a key
+// is flagged so that `order` ranks its keys by probing the range's |B.E| times instead.
+
+// t = i D + j for D <= 63: m = floor(2^32 / D), i = (t m) >> 32 is i or i - 1
+__device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t D, uint64_t m, uint32_t& j) {
+    uint32_t i = (uint32_t)(((uint64_t)t * m) >> 32);
+    uint32_t r = t - i * D;
+    if (r >= D) {
+        ++i;
+        r -= D;
+    }
+    j = r;
+    return i;
+}
+
+// After the tasks of A layer la (all B layers) have stored tkey / info: M1[d] / M2[d] = bit j for
+// the keys whose first-insert time is (A edge at dense slot d, B edge j) and that have >= 1 / 2
+// edges, bit 63 of M1 = a key of a shared bucket lies in the range; then icnt[i] and each key's
+// rank (info bits 8..15, bit 2 = probe in `order`). M1 / M2 use the dense digit table's LDS (dead
+// now), tt still maps A edge i to its dense slot. Barriers inside; every thread calls it.
+template <int BS>
+__device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_desc& d, uint32_t la, uint4 lbq,
+                           uint32_t neB, const uint32_t* bjt, uint32_t* icnt) {
+    const uint32_t Bm = g.Bm, nB = d.nB, LB = d.LB;
+    uint32_t* S = g.scratch;
+    const uint32_t* tkey = S + d.o_tkey;
+    uint32_t* info = S + d.o_info;
+    const uint32_t* ghead = group_heads(g, d);
+    unsigned long long* M1 = (unsigned long long*)plds;
+    unsigned long long* M2 = M1 + 2u * Bm;
+    const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
+    const uint64_t m = (1ull << 32) / nB;
+    const uint32_t tid = threadIdx.x, nk = neB * Bm;
+    for (uint32_t k = tid; k < 4u * Bm; k += BS) M1[k] = 0ull;
+    __syncthreads();
+    // a key's A edge i sits at dense slot (ch, (r - idx_j) mod B) for ch 0 or 1: tt names it
+    auto locate = [&](uint32_t q, uint64_t& s, uint32_t& t, uint32_t& j, uint32_t& dd) {
+        uint32_t kb = 0, r = q;
+        while (r >= Bm) {
+            r -= Bm;
+            ++kb;
+        }
+        const uint32_t lb = kb == 0 ? lbq.x : kb == 1 ? lbq.y : kb == 2 ? lbq.z : lbq.w;
+        s = (uint64_t)(la * LB + lb) * Bm + r;
+        t = tkey[s];
+        if (t == kInf) return;
+        const uint32_t i = div_small(t, nB, m, j);
+        const uint32_t ij = bjt[j] & 0xFFFFu;
+        const uint32_t x = r >= ij ? r - ij : r + Bm - ij;
+        dd = tt[x] == i * nB ? x : Bm + x;
+    };
+    for (uint32_t q = tid; q < nk; q += BS) {
+        uint64_t s;
+        uint32_t t, j, dd;
+        locate(q, s, t, j, dd);
+        if (t == kInf) continue;
+        const uint32_t e = info[s] & 3u;
+        const bool shared = ghead && ghead[s] != 0u;
+        if (e) atomicOr(&M1[dd], (1ull << j) | (shared ? 1ull << 63 : 0ull));
+        else if (shared) atomicOr(&M1[dd], 1ull << 63);   // no edges, but it may lead its bucket
+        if (e == 3u) atomicOr(&M2[dd], 1ull << j);
+    }
+    __syncthreads();
+    for (uint32_t dd = tid; dd < 2u * Bm; dd += BS) {
+        const uint32_t ch = dd >= Bm ? 1u : 0u;
+        const uint32_t te = tt[dd + ch * Bm];   // tt slot ch 2B + idx
+        if (te == kInf) continue;
+        uint32_t j;
+        icnt[div_small(te, nB, m, j)] = (uint32_t)__popcll(M1[dd] & ~(1ull << 63)) + (uint32_t)__popcll(M2[dd]);
+    }
+    for (uint32_t q = tid; q < nk; q += BS) {
+        uint64_t s;
+        uint32_t t, j, dd;
+        locate(q, s, t, j, dd);
+        if (t == kInf) continue;
+        const uint32_t e = info[s] & 3u;
+        if (!e) continue;
+        const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
+        const unsigned long long x1 = M1[dd];
+        const uint32_t rank = (uint32_t)__popcll(x1 & above) + (uint32_t)__popcll(M2[dd] & above);
+        info[s] = e | (uint32_t)(x1 >> 63) << 2 | rank << 8;
+    }
+    __syncthreads();   // the next A layer's staging overwrites M1 / M2 and tt
 }
 
 // One workgroup per (pair, kLaPerWG A layers) for pairs with at most kLaMaxLB B layers (chain
@@ -713,8 +818,16 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
             }
         }
     }
+    // iblk: per-A-edge counts and ranks (iblk_layer) instead of block marks, unless the pair has
+    // fallen back (cnt[kCntIFail], set by k_large_lists or by a workgroup below)
+    bool ib = d.iblk && !S[d.o_cnt + kCntIFail];
+    uint32_t* bjt = (uint32_t*)(sreg + kLaMaxLB * kMxSparseBytes);   // B edge j: idx | ch << 16
+    if (ib && threadIdx.x < nB) {   // published by the dense staging's barriers
+        const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + threadIdx.x];
+        bjt[threadIdx.x] = meta_idx(mb) | meta_ch(mb) << 16;
+    }
     const task_out o{S + d.o_tkey, S + d.o_info, (ulonglong2*)(S + d.o_sums), group_heads(g, d),
-                     (unsigned long long*)w64(S, d.o_bmask)};
+                     d.iblk ? nullptr : (unsigned long long*)w64(S, d.o_bmask)};
     const uint32_t i1 = min(neA, i0 + g.la_per_wg);
     for (uint32_t i = i0; i < i1; ++i) {
         const uint32_t la = S[d.o_neA + i];
@@ -751,6 +864,17 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
                 if (threadIdx.x == 0) S[d.o_defer + atomicAdd((uint32_t*)cnt + 7, 1u)] = i << 16 | k;
             } else {
                 run_task<BS, false>(g, d, la, lbv[k], plds, false);   // scatter mode
+            }
+        }
+        if (ib) {
+            // every task of this A layer ran on the matrix cores (its dense table staged, no duplicate
+            // (idx, ch) edges): count and rank per A edge; otherwise the pair falls back
+            if (mxm == (1u << neB) - 1u) {
+                static_assert(kLaMaxLB == 4, "iblk_layer takes the B layers as a uint4");
+                iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, bjt, S + d.o_icnt);
+            } else {
+                if (threadIdx.x == 0) atomicExch(&S[d.o_cnt + kCntIFail], 1u);
+                ib = false;
             }
         }
     }
@@ -802,6 +926,8 @@ __global__ __launch_bounds__(kLBig) void k_large_layers(mul_large_args g) {
     const uint64_t alo = g.A.l_off[pr], blo = g.B.l_off[pr], clo = g.C.l_off[pr];
     uint32_t* used = S + d.o_used;
     const int tid = threadIdx.x;
+    if (d.iblk && S[d.o_cnt + kCntIFail])   // k_large_rank marks this pair's leaders next
+        for (uint64_t w = tid; w < 2 * d.nblk; w += kLBig) S[d.o_bmask + w] = 0;
     for (uint32_t l = tid; l < Lc; l += kLBig) keep[l] = l >= base ? (used[l] != 0) : 0u;
     for (;;) {
         __syncthreads();
@@ -903,10 +1029,22 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     const bool stat = d.g_head != kNoGrp;
     const uint32_t* ghead = g.grp + (stat ? d.g_head : 0);
     const uint32_t* gnext = g.grp + (stat ? d.g_next : 0);
+    // iblk: bucket-sharing keys move their edges to their leader's A edge count; a pair that fell
+    // back marks blocks here, lone leaders included (products did not)
+    const bool fb = d.iblk && S[d.o_cnt + kCntIFail];
+    const bool ib = d.iblk && !fb;
+    uint32_t* icnt = S + d.o_icnt;
+    const uint64_t m = ib ? (1ull << 32) / d.nB : 0ull;
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
-        // static groups: a key alone in its bucket (the common case) was marked by `products`
+        // static groups: a key alone in its bucket (the common case) was counted by `products`
         // and `order` takes t_b = its own time, within = 0
         const uint32_t q0 = stat ? ghead[s] : 1u;
+        if (!q0 && fb) {
+            const uint32_t t = tkey[s];
+            const uint32_t E = t == kInf ? 0u : __popc(info[s] & 3u);
+            if (E) leader_mark(bpack, t, E);
+            continue;
+        }
         if (!q0) continue;
         const uint32_t t = tkey[s];
         if (t == kInf) continue;
@@ -942,7 +1080,16 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
         within[s] = w;
         if (tmin == t) {
             etot[s] = E;
-            if (E) leader_mark(bpack, t, E);   // one atomic per leader
+            if (E && !ib) leader_mark(bpack, t, E);   // one atomic per leader
+        } else if (ib) {
+            // products counted this key's edges in its own A edge's range: move them to the leader's
+            const uint32_t e = __popc(info[s] & 3u);
+            uint32_t j;
+            const uint32_t is = div_small(t, d.nB, m, j), il = div_small(tmin, d.nB, m, j);
+            if (e && is != il) {
+                atomicSub(&icnt[is], e);
+                atomicAdd(&icnt[il], e);
+            }
         }
     }
 }
@@ -958,10 +1105,35 @@ __global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
     const int tid = threadIdx.x;
     unsigned long long* bpack = (unsigned long long*)w64(S, d.o_bmask);
     const uint32_t nblk = (uint32_t)d.nblk;
+    uint32_t total = 0;
+    if (d.iblk && !cnt[kCntIFail]) {
+        // per-A-edge counts -> exclusive suffix offsets in place (A edge nA-1 first), as below
+        uint32_t* icnt = S + d.o_icnt;
+        const uint32_t nA = d.nA;
+        for (uint32_t base = 0; base < nA; base += 4u * kLBig) {
+            const uint32_t r0 = base + 4u * (uint32_t)tid;
+            uint32_t v[4];
+            uint32_t local = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t r = r0 + (uint32_t)k;
+                v[k] = r < nA ? icnt[nA - 1 - r] : 0u;
+                local += v[k];
+            }
+            uint32_t tot;
+            uint32_t run = total + wg_exclusive_scan<kLBig>(local, part, tot);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t r = r0 + (uint32_t)k;
+                if (r < nA) icnt[nA - 1 - r] = run;
+                run += v[k];
+            }
+            total += tot;
+        }
+    }
     // reversed block index r (block nblk-1-r) in rounds of 4 kLBig: thread t takes r = base + 4t .. 4t+3
     // (adjacent threads, adjacent words: coalesced), one workgroup scan per round
-    uint32_t total = 0;
-    for (uint32_t base = 0; base < nblk; base += 4u * kLBig) {
+    for (uint32_t base = 0; base < (d.iblk && !cnt[kCntIFail] ? 0u : nblk); base += 4u * kLBig) {
         const uint32_t r0 = base + 4u * (uint32_t)tid;
         unsigned long long v[4];
         uint32_t local = 0;
@@ -1022,12 +1194,57 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     uint32_t* order = S + d.o_order;
     uint32_t* hpos = S + d.o_hpos;
     const uint32_t* ghead = group_heads(g, d);
+    const bool ib = d.iblk && !cnt[kCntIFail];
+    const uint32_t* icnt = S + d.o_icnt;
+    const uint64_t m = ib ? (1ull << 32) / nB : 0ull;
+    // iblk: edges emitted before the emit time (i, j) inside A edge i's range, by probing its later
+    // times (i, j'): the key slot of (i, j') is known from the two edges, and (i, j') is an emit time
+    // when it is that key's first-insert time and the key is alone in its bucket or leads it
+    auto probe_rank = [&](uint32_t i, uint32_t j) {
+        const uint64_t ma = g.A.meta[aeo + i];
+        const uint32_t sa = meta_layer(ma) * LB, ia = meta_idx(ma);
+        uint32_t w = 0;
+        for (uint32_t j2 = j + 1; j2 < nB; ++j2) {
+            const uint64_t mb = g.B.meta[beo + j2];
+            const uint64_t s2 = (uint64_t)(sa + meta_layer(mb)) * Bm + mod_small(ia + meta_idx(mb), Bm);
+            const uint32_t t2 = i * nB + j2;
+            if (tkey[s2] != t2) continue;
+            if (ghead[s2] == 0u) w += __popc(info[s2] & 3u);
+            else if (tb[s2] == t2) w += etot[s2];
+        }
+        return w;
+    };
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
         const uint32_t ts = tkey[s];
         if (ts == kInf) continue;
-        const uint32_t eb = info[s] & 3u;
+        const uint32_t inf = info[s];
+        const uint32_t eb = inf & 3u;
         if (!eb) continue;
         const bool lone = ghead && ghead[s] == 0u;   // its own bucket leader, nothing before it
+        if (ib) {
+            uint32_t hp;
+            if (lone && !(inf & 4u)) {   // ranked by products
+                uint32_t j;
+                hp = icnt[div_small(ts, nB, m, j)] + (inf >> 8);
+            } else {
+                const uint32_t tu = lone ? ts : tb[s];
+                uint32_t j;
+                const uint32_t i = div_small(tu, nB, m, j);
+                hp = icnt[i] + probe_rank(i, j) + (lone ? 0u : within[s]);
+            }
+            const uint32_t p = canonical ? cpos[s] : hp;
+            const uint32_t s32 = (uint32_t)s;
+            if (eb & 1u) {
+                order[p] = s32 << 1;
+                if (canonical) hpos[p] = hp;
+            }
+            if (eb & 2u) {
+                const uint32_t o = eb & 1u;
+                order[p + o] = (s32 << 1) | 1u;
+                if (canonical) hpos[p + o] = hp + o;
+            }
+            continue;
+        }
         const uint32_t t = lone ? ts : tb[s], blk = t >> 4, bit = t & 15u;
         const unsigned long long v = bpack[blk];
         // edge codes of the leaders later in this block (2 bits per time): 1 and 2 are their edge
@@ -1161,7 +1378,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
             b.lds_task = mx_lds_bytes(a.Bm);   // the scatter mode (52 B per slot) fits below it
             hipLaunchKernelGGL((k_large_products_la<kLPX>), dim3((unsigned)a.max_la_wg, a.la_xcd ? (a.n_la + 7u) & ~7u : a.n_la),
                                dim3(kLPX),
-                               (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes, st, b);
+                               (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes + kIblkBjtBytes, st, b);
             hipLaunchKernelGGL((k_large_products_defer<kLPX>), dim3(kDeferWG, a.n_la), dim3(kLPX), plds, st, a);
         }
     }

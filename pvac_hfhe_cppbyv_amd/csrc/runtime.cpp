@@ -223,6 +223,18 @@ uint32_t ceil_log2(uint64_t x) {
     return b;
 }
 
+// Per-A-edge emit order for eligible pairs (large_desc::iblk). PVAC_LARGE_IBLK=0 keeps the n/16
+// block marks for every pair (A/B runs); so does PVAC_LARGE_PRODUCTS=col26, whose per-task products
+// kernel does not see an A layer's keys in one workgroup.
+bool large_iblk_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("PVAC_LARGE_IBLK");
+        const char* p = std::getenv("PVAC_LARGE_PRODUCTS");
+        return !(e && e[0] == '0') && !(p && std::strcmp(p, "col26") == 0);
+    }();
+    return on;
+}
+
 // Scratch layout of one general-path pair (k_mul_large.hip), offsets relative to 0; the
 // executor rebases them into the arena. 64-bit arrays on even words, 16-byte arrays on
 // multiples of four.
@@ -259,7 +271,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     auto quad = [&]() { o = (o + 3) & ~3ull; };
     quad();
     d.o_zero = o;
-    d.o_cnt = o; o += 8;
+    d.o_cnt = o; o += kCntWords;
     d.o_hkey = o; o += 2 * hcap;
     d.o_hhead = o; o += hcap;
     even();
@@ -283,6 +295,9 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.o_cpos = o; o += d.S;
     d.o_order = o; o += d.capE;
     d.o_hpos = o; o += d.capE;
+    // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
+    d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
+    d.o_icnt = o; o += d.iblk ? nA : 0;
     quad();
     d.words = o;
     return PVAC_OK;
@@ -291,7 +306,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
 void rebase_desc(large_desc& d, uint64_t base) {
     uint64_t* f[] = {&d.o_zero, &d.o_cnt, &d.o_hkey, &d.o_hhead, &d.o_bmask, &d.o_bcnt, &d.o_used, &d.o_tkey,
                      &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_defer, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
-                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos};
+                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos, &d.o_icnt};
     for (uint64_t* p : f) *p += base;
 }
 

@@ -322,6 +322,58 @@ def test_static_bucket_groups_and_escape_codes_vs_oracle(oracle):
     assert plan.n_large == len(xs)
 
 
+def _mk_layers(rng, counts, dup_layers=(), B=337):
+    """A cipher with exactly counts[l] edges in layer l (distinct (idx, ch) cells, in shuffled
+    order), except layers in dup_layers, which repeat some of their cells."""
+    nl = len(counts)
+    L = np.zeros(nl, LAYER_DT)
+    L["ztag"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+    L["nonce_lo"] = rng.integers(0, 2**63, nl, dtype=np.uint64)
+    metas = []
+    for l, c in enumerate(counts):
+        cells = rng.choice(2 * B, size=c, replace=l in dup_layers).astype(np.uint64)
+        metas.append(np.uint64(l) | ((cells >> np.uint64(1)) << np.uint64(32)) | ((cells & np.uint64(1)) << np.uint64(48)))
+    meta = np.concatenate(metas) if metas else np.zeros(0, np.uint64)
+    meta = meta[rng.permutation(len(meta))]
+    ne = len(meta)
+    lo = rng.integers(0, 2**64 - 1, ne, dtype=np.uint64, endpoint=True)
+    hi = rng.integers(0, 2**64 - 1, ne, dtype=np.uint64, endpoint=True)
+    return Cipher(L, meta, lo, hi)
+
+
+def test_iblk_order_and_fallbacks_vs_oracle(oracle):
+    """Per-A-edge emit order (k_mul_large.hip iblk_layer / order): chain-step shapes (dense A layers
+    x B layers of <= 20 edges, |B.E| up to 63, keys sharing libstdc++ buckets) bit-exact vs the
+    oracle, next to the pairs that must fall back to the block marks inside the same batch: a B
+    layer of 21+ edges, an A layer with duplicate (idx, ch) cells, an A layer below the dense
+    threshold (48 edges), and |B.E| = 64; and small-|B.E| pairs whose keys share buckets."""
+    rng = np.random.default_rng(0x1B1C)
+    xs, ys = [], []
+    full = [674, 674, 674, 674]
+    for k in range(4):   # iblk: saturated and partly filled A layers x fresh-like B
+        xs.append(_mk_layers(rng, full if k % 2 == 0 else [500, 674, 300, 650]))
+        ys.append(_mk_layers(rng, [20, 20] if k < 2 else [19, 17]))
+    xs.append(_mk_layers(rng, [600, 674, 674])); ys.append(_mk_layers(rng, [15, 15, 15]))   # 3 B layers
+    xs.append(_mk_layers(rng, [674, 674])); ys.append(_mk_layers(rng, [16, 16, 16, 15]))     # |B.E| = 63
+    xs.append(_mk_layers(rng, full)); ys.append(_mk_layers(rng, [16, 16, 16, 16]))            # 64: not iblk
+    xs.append(_mk_layers(rng, full)); ys.append(_mk_layers(rng, [25, 15]))                    # B layer > 20
+    xs.append(_mk_layers(rng, [674, 600, 674], dup_layers=(1,))); ys.append(_mk_layers(rng, [20, 20]))   # duplicates
+    xs.append(_mk_layers(rng, [674, 30, 674])); ys.append(_mk_layers(rng, [20, 20]))          # A layer < 48
+    xs.append(_mk_layers(rng, [674, 674, 0, 674])); ys.append(_mk_layers(rng, [20, 0, 20]))   # empty layers
+    shared = [_max_bucket_edges(oracle, x, y) for x, y in zip(xs, ys)]
+    assert all(st for _, st in shared), shared   # static bucket groups everywhere
+    # iblk pairs whose keys share libstdc++ buckets (up to 4 keys per bucket): chain-step shapes
+    # have none (the multiplicative hash spreads their keys), small |B.E| puts the bucket count near
+    # 2 S. `rank` moves edges between A edge counts; `order` probes the flagged ranges
+    for a, b in [([674, 674], [1, 1]), ([674] * 4, [2, 1]), ([674, 674], [3, 2]), ([674] * 3, [2, 2, 1]),
+                 ([400, 674], [2, 2])]:
+        xs.append(_mk_layers(rng, a)); ys.append(_mk_layers(rng, b))
+        mx, st = _max_bucket_edges(oracle, xs[-1], ys[-1])
+        assert st and mx >= 4, (a, b, mx, st)
+    plan = _check_vs_oracle(oracle, {"canon_tag": 0x1B}, xs, ys, 0x1B2)
+    assert plan.n_large == len(xs)
+
+
 def test_engine_chain_depth8_vs_oracle(oracle):
     """BASELINE cfg 4 at its full depth: c_k = c_{k-1} * x for two fresh inputs to depth 8
     (345,088 edges, 6.8 M products per pair at step 8, static bucket groups and 16-time leader
