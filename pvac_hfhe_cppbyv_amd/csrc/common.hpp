@@ -254,6 +254,7 @@ struct large_desc {
     // (cnt[kCntIFail]) when a B layer is too big for the matrix-core mode or an A layer cannot be
     // staged as a dense table
     uint32_t iblk;
+    uint64_t nb_m;               // floor(2^32 / |B.E|): t / |B.E| by div_small (k_mul_large.hip)
     // static bucket groups (bucket_count >= 2 S): per-slot chain head / next of the slots sharing
     // a libstdc++ bucket, word offsets into mul_large_args::grp (kNoGrp: dynamic chains via link)
     uint64_t g_head, g_next;

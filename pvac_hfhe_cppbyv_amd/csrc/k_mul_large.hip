@@ -715,7 +715,7 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
     unsigned long long* M1 = (unsigned long long*)plds;
     unsigned long long* M2 = M1 + 2u * Bm;
     const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
-    const uint64_t m = (1ull << 32) / nB;
+    const uint64_t m = d.nb_m;
     const uint32_t tid = threadIdx.x, nk = neB * Bm;
     for (uint32_t k = tid; k < 4u * Bm; k += BS) M1[k] = 0ull;
     __syncthreads();
@@ -735,17 +735,27 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         const uint32_t x = r >= ij ? r - ij : r + Bm - ij;
         dd = tt[x] == i * nB ? x : Bm + x;
     };
-    for (uint32_t q = tid; q < nk; q += BS) {
+    // pass A; the first kQ keys of each thread keep dd | j << 12 | e << 18 (0: no edges) for pass B
+    constexpr int kQ = 6;
+    uint32_t keep[kQ];
+    auto mark = [&](uint32_t q) -> uint32_t {
         uint64_t s;
         uint32_t t, j, dd;
         locate(q, s, t, j, dd);
-        if (t == kInf) continue;
+        if (t == kInf) return 0u;
         const uint32_t e = info[s] & 3u;
         const bool shared = ghead && ghead[s] != 0u;
         if (e) atomicOr(&M1[dd], (1ull << j) | (shared ? 1ull << 63 : 0ull));
         else if (shared) atomicOr(&M1[dd], 1ull << 63);   // no edges, but it may lead its bucket
         if (e == 3u) atomicOr(&M2[dd], 1ull << j);
+        return e ? dd | j << 12 | e << 18 : 0u;
+    };
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        const uint32_t q = tid + (uint32_t)k * BS;
+        keep[k] = q < nk ? mark(q) : 0u;
     }
+    for (uint32_t q = tid + kQ * BS; q < nk; q += BS) mark(q);
     __syncthreads();
     for (uint32_t dd = tid; dd < 2u * Bm; dd += BS) {
         const uint32_t ch = dd >= Bm ? 1u : 0u;
@@ -754,17 +764,33 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         uint32_t j;
         icnt[div_small(te, nB, m, j)] = (uint32_t)__popcll(M1[dd] & ~(1ull << 63)) + (uint32_t)__popcll(M2[dd]);
     }
-    for (uint32_t q = tid; q < nk; q += BS) {
+    auto ranked = [&](uint64_t s, uint32_t dd, uint32_t j, uint32_t e) {
+        const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
+        const unsigned long long x1 = M1[dd];
+        const uint32_t rank = (uint32_t)__popcll(x1 & above) + (uint32_t)__popcll(M2[dd] & above);
+        info[s] = e | (uint32_t)(x1 >> 63) << 2 | rank << 8;
+    };
+    auto slot_of = [&](uint32_t q) {
+        uint32_t kb = 0, r = q;
+        while (r >= Bm) {
+            r -= Bm;
+            ++kb;
+        }
+        const uint32_t lb = kb == 0 ? lbq.x : kb == 1 ? lbq.y : kb == 2 ? lbq.z : lbq.w;
+        return (uint64_t)(la * LB + lb) * Bm + r;
+    };
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        const uint32_t v = keep[k];
+        if (v) ranked(slot_of(tid + (uint32_t)k * BS), v & 0xFFFu, (v >> 12) & 63u, v >> 18);
+    }
+    for (uint32_t q = tid + kQ * BS; q < nk; q += BS) {
         uint64_t s;
         uint32_t t, j, dd;
         locate(q, s, t, j, dd);
         if (t == kInf) continue;
         const uint32_t e = info[s] & 3u;
-        if (!e) continue;
-        const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
-        const unsigned long long x1 = M1[dd];
-        const uint32_t rank = (uint32_t)__popcll(x1 & above) + (uint32_t)__popcll(M2[dd] & above);
-        info[s] = e | (uint32_t)(x1 >> 63) << 2 | rank << 8;
+        if (e) ranked(s, dd, j, e);
     }
     __syncthreads();   // the next A layer's staging overwrites M1 / M2 and tt
 }
@@ -1034,7 +1060,7 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     const bool fb = d.iblk && S[d.o_cnt + kCntIFail];
     const bool ib = d.iblk && !fb;
     uint32_t* icnt = S + d.o_icnt;
-    const uint64_t m = ib ? (1ull << 32) / d.nB : 0ull;
+    const uint64_t m = d.nb_m;
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
         // static groups: a key alone in its bucket (the common case) was counted by `products`
         // and `order` takes t_b = its own time, within = 0
@@ -1196,7 +1222,7 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     const uint32_t* ghead = group_heads(g, d);
     const bool ib = d.iblk && !cnt[kCntIFail];
     const uint32_t* icnt = S + d.o_icnt;
-    const uint64_t m = ib ? (1ull << 32) / nB : 0ull;
+    const uint64_t m = d.nb_m;
     // iblk: edges emitted before the emit time (i, j) inside A edge i's range, by probing its later
     // times (i, j'): the key slot of (i, j') is known from the two edges, and (i, j') is an emit time
     // when it is that key's first-insert time and the key is alone in its bucket or leads it

@@ -298,6 +298,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
     d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
     d.o_icnt = o; o += d.iblk ? nA : 0;
+    d.nb_m = nB ? (1ull << 32) / nB : 0;
     quad();
     d.words = o;
     return PVAC_OK;
