@@ -287,6 +287,8 @@ struct large_desc {
     uint64_t o_hpos;             // [capE] hash-order index of each canonical-order edge
     uint64_t o_icnt;             // [nA] iblk: edges whose emit time lies in A edge i's product range
                                  // [i |B.E|, (i + 1) |B.E|), then their exclusive suffix offset
+    uint64_t o_imask;            // [nA] x 2 u64 iblk: the range's keys with a P edge / an M edge (bit j
+                                 // = B edge j), read by k_large_write_ranges
     uint64_t words;              // end of this pair's scratch (absolute)
 };
 
@@ -309,10 +311,10 @@ struct mul_large_args {
     uint32_t lds_task;           // k_large_products_la: bytes of LDS below its staged B layers (set at launch)
     uint32_t la_per_wg;          // k_large_products_la: A layers per workgroup (max_la_wg = ceil(|A.L| / it))
     uint32_t la_xcd;             // k_large_products_la: 1 = all workgroups of a pair on one XCD (grid y padded to 8)
-    uint32_t pad;
+    uint32_t any_dyn;            // some pair has dynamic bucket chains (k_large_link runs)
     // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all
     // over all, max_la_wg = ceil(|A.L| / kLaPerWG) over the A-layer-major class)
-    uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg;
+    uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg, max_nA;
 };
 // k_large_products_la: A layers per workgroup (default; PVAC_LA_PER_WG); pairs with at most
 // kLaMaxLB B layers take it
@@ -330,6 +332,7 @@ hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, con
 constexpr uint64_t kNoGrp = ~0ull;
 constexpr uint32_t kCntWords = 16;    // large_desc::o_cnt words
 constexpr uint32_t kCntIFail = 8;     // cnt word: an iblk pair uses the block marks after all
+constexpr uint32_t kCntIShared = 9;   // cnt word: an iblk pair has keys sharing a bucket (order probes)
 constexpr uint32_t kIblkMaxNB = 63;   // iblk: |B.E| <= 63 (a 64-bit mask per A edge, bit 63 a flag)
 // static bucket groups of key slots [0, S) for one bucket count: head[s] = 0 when s is alone in
 // its bucket, else the first slot + 1 of the bucket's chain; next[s] = the following slot + 1

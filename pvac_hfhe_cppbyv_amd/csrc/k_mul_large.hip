@@ -700,13 +700,13 @@ __device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t D, uint64_t m
 }
 
 // After the tasks of A layer la (all B layers) have stored tkey / info: M1[d] / M2[d] = bit j for
-// the keys whose first-insert time is (A edge at dense slot d, B edge j) and that have >= 1 / 2
-// edges, bit 63 of M1 = a key of a shared bucket lies in the range; then icnt[i] and each key's
-// rank (info bits 8..15, bit 2 = probe in `order`). M1 / M2 use the dense digit table's LDS (dead
-// now), tt still maps A edge i to its dense slot. Barriers inside; every thread calls it.
+// the keys whose first-insert time is (A edge at dense slot d, B edge j) and that emit a P / an M
+// edge, bit 63 of M1 = a key of a shared bucket lies in the range; then icnt[i], imask[i] and each
+// key's rank (info bits 8..15, bit 2 = probe in `order`). M1 / M2 use the dense digit table's LDS
+// (dead now), tt still maps A edge i to its dense slot. Barriers inside; every thread calls it.
 template <int BS>
 __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_desc& d, uint32_t la, uint4 lbq,
-                           uint32_t neB, const uint32_t* bjt, uint32_t* icnt) {
+                           uint32_t neB, const uint32_t* bjt, uint32_t* icnt, ulonglong2* imask) {
     const uint32_t Bm = g.Bm, nB = d.nB, LB = d.LB;
     uint32_t* S = g.scratch;
     const uint32_t* tkey = S + d.o_tkey;
@@ -745,9 +745,12 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         if (t == kInf) return 0u;
         const uint32_t e = info[s] & 3u;
         const bool shared = ghead && ghead[s] != 0u;
-        if (e) atomicOr(&M1[dd], (1ull << j) | (shared ? 1ull << 63 : 0ull));
-        else if (shared) atomicOr(&M1[dd], 1ull << 63);   // no edges, but it may lead its bucket
-        if (e == 3u) atomicOr(&M2[dd], 1ull << j);
+        if (e & 1u) atomicOr(&M1[dd], 1ull << j);
+        if (e & 2u) atomicOr(&M2[dd], 1ull << j);
+        if (shared) {   // with or without edges: it may lead its bucket
+            atomicOr(&M1[dd], 1ull << 63);
+            S[d.o_cnt + kCntIShared] = 1u;
+        }
         return e ? dd | j << 12 | e << 18 : 0u;
     };
 #pragma unroll
@@ -762,7 +765,10 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         const uint32_t te = tt[dd + ch * Bm];   // tt slot ch 2B + idx
         if (te == kInf) continue;
         uint32_t j;
-        icnt[div_small(te, nB, m, j)] = (uint32_t)__popcll(M1[dd] & ~(1ull << 63)) + (uint32_t)__popcll(M2[dd]);
+        const uint32_t i = div_small(te, nB, m, j);
+        const unsigned long long x1 = M1[dd] & ~(1ull << 63), x2 = M2[dd];
+        icnt[i] = (uint32_t)__popcll(x1) + (uint32_t)__popcll(x2);
+        imask[i] = make_ulonglong2(x1, x2);
     }
     auto ranked = [&](uint64_t s, uint32_t dd, uint32_t j, uint32_t e) {
         const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
@@ -897,7 +903,8 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
             // (idx, ch) edges): count and rank per A edge; otherwise the pair falls back
             if (mxm == (1u << neB) - 1u) {
                 static_assert(kLaMaxLB == 4, "iblk_layer takes the B layers as a uint4");
-                iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, bjt, S + d.o_icnt);
+                iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, bjt, S + d.o_icnt,
+                                  (ulonglong2*)(S + d.o_imask));
             } else {
                 if (threadIdx.x == 0) atomicExch(&S[d.o_cnt + kCntIFail], 1u);
                 ib = false;
@@ -1059,6 +1066,7 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     // back marks blocks here, lone leaders included (products did not)
     const bool fb = d.iblk && S[d.o_cnt + kCntIFail];
     const bool ib = d.iblk && !fb;
+    if (ib && !S[d.o_cnt + kCntIShared]) return;   // every key alone in its bucket: nothing to rank
     uint32_t* icnt = S + d.o_icnt;
     const uint64_t m = d.nb_m;
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
@@ -1221,6 +1229,7 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     uint32_t* hpos = S + d.o_hpos;
     const uint32_t* ghead = group_heads(g, d);
     const bool ib = d.iblk && !cnt[kCntIFail];
+    if (ib && !canonical && !cnt[kCntIShared]) return;   // k_large_write_ranges
     const uint32_t* icnt = S + d.o_icnt;
     const uint64_t m = d.nb_m;
     // iblk: edges emitted before the emit time (i, j) inside A edge i's range, by probing its later
@@ -1312,6 +1321,7 @@ __global__ __launch_bounds__(kLB) void k_large_write(mul_large_args g) {
     if (cnt[2]) return;
     const uint32_t total = cnt[3];
     const bool canonical = cnt[4] != 0;
+    if (d.iblk && !cnt[kCntIFail] && !canonical && !cnt[kCntIShared]) return;   // k_large_write_ranges
     const uint32_t Bm = g.Bm, base = d.LA + d.LB;
     const uint64_t ceo = g.C.e_off[d.pair];
     const uint32_t* order = S + d.o_order;
@@ -1327,6 +1337,89 @@ __global__ __launch_bounds__(kLB) void k_large_write(mul_large_args g) {
         g.C.w_lo[ceo + p] = w.x;
         g.C.w_hi[ceo + p] = w.y;
         if (g.salt_pos) g.salt_pos[ceo + p] = canonical ? hpos[p] : p;
+    }
+}
+
+// iblk pairs without shared buckets, hash order: the edges are written range by range. A edge
+// i's keys take positions [off(i), off(i) + cnt(i)), and off decreases with i, so ranges in DESCENDING
+// i are consecutive in the output. A wave takes 64 ranges (lane l: i = nA - 1 - (64 c + l)), scans
+// their edge counts and writes its positions coalesced: position q of the chunk finds its lane
+// (binary search over the scanned counts) and its key inside the range (j DESC; P before M: the
+// k-th edge sits below the highest bit x with popc(P >> x) + popc(M >> x) <= k), the key slot from
+// (A edge i, B edge j), and gathers its sum. No order array, no per-slot pass (k_large_order).
+__global__ __launch_bounds__(kLB) void k_large_write_ranges(mul_large_args g) {
+    __shared__ uint32_t bjt[64];   // B edge j: idx | layer << 16
+    const large_desc& d = g.desc[blockIdx.y];
+    uint32_t* S = g.scratch;
+    const uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2] || !d.iblk || cnt[kCntIFail] || cnt[4] || cnt[kCntIShared]) return;
+    const uint32_t Bm = g.Bm, LB = d.LB, nA = d.nA, nB = d.nB, base = d.LA + d.LB;
+    const uint64_t pr = d.pair;
+    const uint64_t aeo = g.A.e_off[pr], beo = g.B.e_off[pr], ceo = g.C.e_off[pr];
+    if (threadIdx.x < nB) {
+        const uint64_t mb = g.B.meta[beo + threadIdx.x];
+        bjt[threadIdx.x] = meta_idx(mb) | meta_layer(mb) << 16;
+    }
+    __syncthreads();
+    const uint32_t* off = S + d.o_icnt;
+    const ulonglong2* imask = (const ulonglong2*)(S + d.o_imask);
+    const uint32_t* remap = S + d.o_used;
+    const ulonglong2* sums = (const ulonglong2*)(S + d.o_sums);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nch = (nA + 63u) >> 6;
+    for (uint32_t c = blockIdx.x * (kLB / 64) + (threadIdx.x >> 6); c < nch; c += gridDim.x * (kLB / 64)) {
+        const uint32_t r = c * 64u + lane;
+        const bool live = r < nA;
+        const uint32_t i = live ? nA - 1u - r : 0u;
+        const ulonglong2 mk = live ? imask[i] : make_ulonglong2(0ull, 0ull);
+        const uint32_t o0 = off[nA - 1u - c * 64u];   // the chunk's first position (lane 0's range)
+        const uint64_t ma = live ? g.A.meta[aeo + i] : 0ull;
+        const uint32_t la_idx = meta_idx(ma) | meta_layer(ma) << 16;
+        const uint32_t E = (uint32_t)__popcll(mk.x) + (uint32_t)__popcll(mk.y);
+        const uint32_t incl = wave_incl_scan_u32(E);
+        const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+        for (uint32_t q0 = 0; q0 < T; q0 += 64u) {   // wave-uniform: every lane takes part in the bpermutes
+            const uint32_t q = q0 + lane;
+            // lane l of the range holding q: the first lane whose inclusive count exceeds q
+            uint32_t l = 0;
+#pragma unroll
+            for (uint32_t b = 32; b; b >>= 1) {
+                const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l + b - 1u) << 2), (int)incl);
+                if (v <= q) l += b;
+            }
+            l = min(l, 63u);
+            const int bl = (int)(l << 2);
+            const uint32_t il = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)incl) -
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)E);
+            const uint64_t mp = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.x) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.x >> 32)) << 32;
+            const uint64_t mm = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.y) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.y >> 32)) << 32;
+            const uint32_t ai = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)la_idx);
+            if (q >= T) continue;
+            const uint32_t k = q - il;   // edge k of the range
+            // edges of keys at bits >= y: A(y) = popc(mp >> y) + popc(mm >> y), non-increasing; the
+            // key holding edge k is the largest j with A(j) > k
+            uint32_t j = 0;
+#pragma unroll
+            for (uint32_t b = 32; b; b >>= 1) {
+                const uint32_t y = j + b;
+                if ((uint32_t)__popcll(mp >> y) + (uint32_t)__popcll(mm >> y) > k) j = y;
+            }
+            const uint32_t fa = j == 63u ? 0u : (uint32_t)__popcll(mp >> (j + 1u)) + (uint32_t)__popcll(mm >> (j + 1u));
+            const uint32_t hasP = (uint32_t)(mp >> j) & 1u;
+            const uint32_t ch = (k - fa == 0u && hasP) ? 0u : 1u;
+            const uint32_t bj = bjt[j];
+            const uint32_t lp = (ai >> 16) * LB + (bj >> 16);
+            const uint32_t rr = mod_small((ai & 0xFFFFu) + (bj & 0xFFFFu), Bm);
+            const uint64_t s = (uint64_t)lp * Bm + rr;
+            const ulonglong2 w = sums[2 * s + ch];
+            const uint64_t p = ceo + o0 + q;
+            g.C.meta[p] = make_meta(remap[base + lp], rr, ch);
+            g.C.w_lo[p] = w.x;
+            g.C.w_hi[p] = w.y;
+            if (g.salt_pos) g.salt_pos[p] = o0 + q;
+        }
     }
 }
 
@@ -1410,11 +1503,12 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     }
     hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
     const unsigned gs = grid_x(a.max_S, kLB * 2, 4096);
-    hipLaunchKernelGGL(k_large_link, dim3(gs, nl), dim3(kLB), 0, st, a);
+    if (a.any_dyn) hipLaunchKernelGGL(k_large_link, dim3(gs, nl), dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_rank, dim3(gs, nl), dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_scan, dim3(nl), dim3(kLBig), 0, st, a);
     hipLaunchKernelGGL(k_large_order, dim3(gs, nl), dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_write, dim3(grid_x(a.max_capE, kLB * 2, 4096), nl), dim3(kLB), 0, st, a);
+    if (a.max_nA) hipLaunchKernelGGL(k_large_write_ranges, dim3(grid_x(a.max_nA, kLB, 4096), nl), dim3(kLB), 0, st, a);
     return hipGetLastError();
 }
 

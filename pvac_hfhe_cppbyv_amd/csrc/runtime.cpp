@@ -298,6 +298,8 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
     d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
     d.o_icnt = o; o += d.iblk ? nA : 0;
+    quad();
+    d.o_imask = o; o += d.iblk ? 4 * nA : 0;
     d.nb_m = nB ? (1ull << 32) / nB : 0;
     quad();
     d.words = o;
@@ -307,7 +309,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
 void rebase_desc(large_desc& d, uint64_t base) {
     uint64_t* f[] = {&d.o_zero, &d.o_cnt, &d.o_hkey, &d.o_hhead, &d.o_bmask, &d.o_bcnt, &d.o_used, &d.o_tkey,
                      &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_defer, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
-                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos, &d.o_icnt};
+                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos, &d.o_icnt, &d.o_imask};
     for (uint64_t* p : f) *p += base;
 }
 
@@ -622,7 +624,8 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
     while (i < nl) {
         uint64_t words = 0;
         size_t j = i;
-        uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0;
+        uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0, mA = 0;
+        bool dyn = false;
         while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
             large_desc& d = c->large_exec[j];
             const uint64_t w = d.words;
@@ -631,6 +634,8 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             mS = std::max(mS, d.S);
             mZ = std::max(mZ, d.zero_words);
             mE = std::max(mE, d.capE);
+            mA = std::max<uint64_t>(mA, d.iblk ? d.nA : 0);
+            dyn |= d.g_head == kNoGrp;
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
         }
@@ -688,7 +693,8 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.sel = c->sel_dev + i;
         a.n_la = n_la;
         a.max_S = mS; a.max_zero = mZ; a.max_tasks = mT; a.max_capE = mE; a.max_lay = mL;
-        a.max_tasks_all = mTa; a.max_la_wg = mLa;
+        a.max_tasks_all = mTa; a.max_la_wg = mLa; a.max_nA = mA;
+        a.any_dyn = dyn ? 1u : 0u;
         a.la_per_wg = la_per_wg;
         a.la_xcd = la_xcd;
         e = launch_ct_mul_large(a, c->stream);
