@@ -312,6 +312,8 @@ struct mul_large_args {
     uint32_t la_per_wg;          // k_large_products_la: A layers per workgroup (max_la_wg = ceil(|A.L| / it))
     uint32_t la_xcd;             // k_large_products_la: 1 = all workgroups of a pair on one XCD (grid y padded to 8)
     uint32_t any_dyn;            // some pair has dynamic bucket chains (k_large_link runs)
+    uint32_t all_iblk;           // every pair is iblk (rank / order / write on reduced grids)
+    uint32_t pad2;
     // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all
     // over all, max_la_wg = ceil(|A.L| / kLaPerWG) over the A-layer-major class)
     uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg, max_nA;

@@ -1378,8 +1378,8 @@ __global__ __launch_bounds__(kLB) void k_large_write_ranges(mul_large_args g) {
         const uint32_t E = (uint32_t)__popcll(mk.x) + (uint32_t)__popcll(mk.y);
         const uint32_t incl = wave_incl_scan_u32(E);
         const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-        for (uint32_t q0 = 0; q0 < T; q0 += 64u) {   // wave-uniform: every lane takes part in the bpermutes
-            const uint32_t q = q0 + lane;
+        // position q of the chunk -> key slot s and channel; every lane takes part in the bpermutes
+        auto resolve = [&](uint32_t q, uint64_t& s, uint32_t& ch, uint32_t& lp, uint32_t& rr) {
             // lane l of the range holding q: the first lane whose inclusive count exceeds q
             uint32_t l = 0;
 #pragma unroll
@@ -1396,8 +1396,7 @@ __global__ __launch_bounds__(kLB) void k_large_write_ranges(mul_large_args g) {
             const uint64_t mm = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.y) |
                                 (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.y >> 32)) << 32;
             const uint32_t ai = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)la_idx);
-            if (q >= T) continue;
-            const uint32_t k = q - il;   // edge k of the range
+            const uint32_t k = q - il;   // edge k of the range (q < T)
             // edges of keys at bits >= y: A(y) = popc(mp >> y) + popc(mm >> y), non-increasing; the
             // key holding edge k is the largest j with A(j) > k
             uint32_t j = 0;
@@ -1408,17 +1407,34 @@ __global__ __launch_bounds__(kLB) void k_large_write_ranges(mul_large_args g) {
             }
             const uint32_t fa = j == 63u ? 0u : (uint32_t)__popcll(mp >> (j + 1u)) + (uint32_t)__popcll(mm >> (j + 1u));
             const uint32_t hasP = (uint32_t)(mp >> j) & 1u;
-            const uint32_t ch = (k - fa == 0u && hasP) ? 0u : 1u;
+            ch = (k - fa == 0u && hasP) ? 0u : 1u;   // a key emits P before M
             const uint32_t bj = bjt[j];
-            const uint32_t lp = (ai >> 16) * LB + (bj >> 16);
-            const uint32_t rr = mod_small((ai & 0xFFFFu) + (bj & 0xFFFFu), Bm);
-            const uint64_t s = (uint64_t)lp * Bm + rr;
-            const ulonglong2 w = sums[2 * s + ch];
-            const uint64_t p = ceo + o0 + q;
-            g.C.meta[p] = make_meta(remap[base + lp], rr, ch);
-            g.C.w_lo[p] = w.x;
-            g.C.w_hi[p] = w.y;
-            if (g.salt_pos) g.salt_pos[p] = o0 + q;
+            lp = (ai >> 16) * LB + (bj >> 16);
+            rr = mod_small((ai & 0xFFFFu) + (bj & 0xFFFFu), Bm);
+            s = (uint64_t)lp * Bm + rr;
+        };
+        // two positions per lane and round: both gathers in flight before the stores
+        for (uint32_t q0 = 0; q0 < T; q0 += 128u) {   // wave-uniform
+            uint64_t s[2];
+            uint32_t ch[2], lp[2], rr[2];
+            ulonglong2 w[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t q = q0 + 64u * (uint32_t)u + lane;
+                resolve(min(q, T - 1u), s[u], ch[u], lp[u], rr[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) w[u] = sums[2 * s[u] + ch[u]];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t q = q0 + 64u * (uint32_t)u + lane;
+                if (q >= T) break;
+                const uint64_t p = ceo + o0 + q;
+                g.C.meta[p] = make_meta(remap[base + lp[u]], rr[u], ch[u]);
+                g.C.w_lo[p] = w[u].x;
+                g.C.w_hi[p] = w[u].y;
+                if (g.salt_pos) g.salt_pos[p] = o0 + q;
+            }
         }
     }
 }
@@ -1503,11 +1519,17 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     }
     hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
     const unsigned gs = grid_x(a.max_S, kLB * 2, 4096);
+    // a batch of iblk pairs runs rank / order / write only for the few that share buckets, need the
+    // canonical order or fell back: 1/16 of the workgroups (grid-stride loops; an empty workgroup per
+    // 512 slots cost 5 ms per sub-batch and kernel at cfg 4's depth 8)
+    const unsigned sh = a.all_iblk ? 4u : 0u;
+    const unsigned gsr = (gs + (1u << sh) - 1u) >> sh;
     if (a.any_dyn) hipLaunchKernelGGL(k_large_link, dim3(gs, nl), dim3(kLB), 0, st, a);
-    hipLaunchKernelGGL(k_large_rank, dim3(gs, nl), dim3(kLB), 0, st, a);
+    hipLaunchKernelGGL(k_large_rank, dim3(gsr, nl), dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_scan, dim3(nl), dim3(kLBig), 0, st, a);
-    hipLaunchKernelGGL(k_large_order, dim3(gs, nl), dim3(kLB), 0, st, a);
-    hipLaunchKernelGGL(k_large_write, dim3(grid_x(a.max_capE, kLB * 2, 4096), nl), dim3(kLB), 0, st, a);
+    hipLaunchKernelGGL(k_large_order, dim3(gsr, nl), dim3(kLB), 0, st, a);
+    const unsigned gw = grid_x(a.max_capE, kLB * 2, 4096);
+    hipLaunchKernelGGL(k_large_write, dim3((gw + (1u << sh) - 1u) >> sh, nl), dim3(kLB), 0, st, a);
     if (a.max_nA) hipLaunchKernelGGL(k_large_write_ranges, dim3(grid_x(a.max_nA, kLB, 4096), nl), dim3(kLB), 0, st, a);
     return hipGetLastError();
 }

@@ -625,7 +625,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         uint64_t words = 0;
         size_t j = i;
         uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0, mA = 0;
-        bool dyn = false;
+        bool dyn = false, all_ib = true;
         while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
             large_desc& d = c->large_exec[j];
             const uint64_t w = d.words;
@@ -636,6 +636,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             mE = std::max(mE, d.capE);
             mA = std::max<uint64_t>(mA, d.iblk ? d.nA : 0);
             dyn |= d.g_head == kNoGrp;
+            all_ib &= d.iblk != 0;
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
         }
@@ -695,6 +696,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.max_S = mS; a.max_zero = mZ; a.max_tasks = mT; a.max_capE = mE; a.max_lay = mL;
         a.max_tasks_all = mTa; a.max_la_wg = mLa; a.max_nA = mA;
         a.any_dyn = dyn ? 1u : 0u;
+        a.all_iblk = all_ib ? 1u : 0u;
         a.la_per_wg = la_per_wg;
         a.la_xcd = la_xcd;
         e = launch_ct_mul_large(a, c->stream);

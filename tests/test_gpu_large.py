@@ -341,12 +341,14 @@ def _mk_layers(rng, counts, dup_layers=(), B=337):
     return Cipher(L, meta, lo, hi)
 
 
-def test_iblk_order_and_fallbacks_vs_oracle(oracle):
+@pytest.mark.parametrize("all_iblk", [False, True])
+def test_iblk_order_and_fallbacks_vs_oracle(oracle, all_iblk):
     """Per-A-edge emit order (k_mul_large.hip iblk_layer / order): chain-step shapes (dense A layers
     x B layers of <= 20 edges, |B.E| up to 63, keys sharing libstdc++ buckets) bit-exact vs the
     oracle, next to the pairs that must fall back to the block marks inside the same batch: a B
     layer of 21+ edges, an A layer with duplicate (idx, ch) cells, an A layer below the dense
-    threshold (48 edges), and |B.E| = 64; and small-|B.E| pairs whose keys share buckets."""
+    threshold (48 edges), and |B.E| = 64; and small-|B.E| pairs whose keys share buckets. A batch of
+    iblk pairs only runs rank / order / write on 1/16 of the workgroups."""
     rng = np.random.default_rng(0x1B1C)
     xs, ys = [], []
     full = [674, 674, 674, 674]
@@ -355,7 +357,8 @@ def test_iblk_order_and_fallbacks_vs_oracle(oracle):
         ys.append(_mk_layers(rng, [20, 20] if k < 2 else [19, 17]))
     xs.append(_mk_layers(rng, [600, 674, 674])); ys.append(_mk_layers(rng, [15, 15, 15]))   # 3 B layers
     xs.append(_mk_layers(rng, [674, 674])); ys.append(_mk_layers(rng, [16, 16, 16, 15]))     # |B.E| = 63
-    xs.append(_mk_layers(rng, full)); ys.append(_mk_layers(rng, [16, 16, 16, 16]))            # 64: not iblk
+    if not all_iblk:   # with a pair that is not iblk the batch runs the per-slot passes on full grids
+        xs.append(_mk_layers(rng, full)); ys.append(_mk_layers(rng, [16, 16, 16, 16]))        # 64: not iblk
     xs.append(_mk_layers(rng, full)); ys.append(_mk_layers(rng, [25, 15]))                    # B layer > 20
     xs.append(_mk_layers(rng, [674, 600, 674], dup_layers=(1,))); ys.append(_mk_layers(rng, [20, 20]))   # duplicates
     xs.append(_mk_layers(rng, [674, 30, 674])); ys.append(_mk_layers(rng, [20, 20]))          # A layer < 48
@@ -372,6 +375,15 @@ def test_iblk_order_and_fallbacks_vs_oracle(oracle):
         assert st and mx >= 4, (a, b, mx, st)
     plan = _check_vs_oracle(oracle, {"canon_tag": 0x1B}, xs, ys, 0x1B2)
     assert plan.n_large == len(xs)
+
+
+def test_iblk_guard_budget_vs_oracle(oracle):
+    """iblk pairs above edge_budget take the canonical (layer, idx, P<M) order with hash-order salt
+    positions (k_large_order on the reduced grid of an all-iblk batch), next to iblk pairs below it."""
+    rng = np.random.default_rng(0x1B3)
+    xs = [_mk_layers(rng, [674, 674, 500]) for _ in range(3)] + [_mk_layers(rng, [300, 200])]
+    ys = [_mk_layers(rng, [20, 20]) for _ in range(4)]
+    _check_vs_oracle(oracle, {"canon_tag": 0x1C, "edge_budget": 30000}, xs, ys, 0x1B4)
 
 
 def test_engine_chain_depth8_vs_oracle(oracle):
