@@ -219,6 +219,9 @@ constexpr uint64_t kDigC = 0x8080808080808080ull;  // 128 in every byte
 #else
 #define MXMARK(ph) do {} while (0)
 #endif
+#ifndef PVAC_EXP_IBREP   // experiment builds only: the per-A-edge passes run this many times (same result)
+#define PVAC_EXP_IBREP 1
+#endif
 #ifndef PVAC_EXP_MXREP   // experiment builds only: the MFMA loop run this many times (same result)
 #define PVAC_EXP_MXREP 1
 #endif
@@ -903,8 +906,9 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
             // (idx, ch) edges): count and rank per A edge; otherwise the pair falls back
             if (mxm == (1u << neB) - 1u) {
                 static_assert(kLaMaxLB == 4, "iblk_layer takes the B layers as a uint4");
-                iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, bjt, S + d.o_icnt,
-                                  (ulonglong2*)(S + d.o_imask));
+                for (int rep_ = 0; rep_ < PVAC_EXP_IBREP; ++rep_)   // experiment builds repeat it (idempotent)
+                    iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, bjt, S + d.o_icnt,
+                                   (ulonglong2*)(S + d.o_imask));
             } else {
                 if (threadIdx.x == 0) atomicExch(&S[d.o_cnt + kCntIFail], 1u);
                 ib = false;
