@@ -226,6 +226,18 @@ constexpr uint64_t kDigC = 0x8080808080808080ull;  // 128 in every byte
 #define PVAC_EXP_MXREP 1
 #endif
 
+// t = i D + j for D <= 63: m = floor(2^32 / D), i = (t m) >> 32 is i or i - 1
+__device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t D, uint64_t m, uint32_t& j) {
+    uint32_t i = (uint32_t)(((uint64_t)t * m) >> 32);
+    uint32_t r = t - i * D;
+    if (r >= D) {
+        ++i;
+        r -= D;
+    }
+    j = r;
+    return i;
+}
+
 // balanced digits of a canonical value: U = V + C (C = 128 in each of the 16 bytes), d = U ^ C
 __device__ __forceinline__ void fp_digits8(const fp& v, uint64_t& dl, uint64_t& dh) {
     const bool neg = (v.hi >> 62) != 0;            // v >= 2^126: V = v - p = v + 2^127 + 1 (mod 2^128)
@@ -358,7 +370,14 @@ struct task_out {
     ulonglong2* sums;
     const uint32_t* ghead;              // static bucket groups (nullptr: dynamic chains)
     unsigned long long* bpack;          // bucket-leader block marks
+    // iblk (k_large_products_la): per output row of this B layer, the key's record for iblk_layer:
+    // dense slot of its A edge | j << 12 | edge bits << 18 | shared << 20 | 1 << 21 (0: no key)
+    uint32_t* recs = nullptr;
+    const uint32_t* bjt = nullptr;      // B edge j: idx | ch << 16
+    uint32_t nB = 0;
+    uint64_t nb_m = 0;
 };
+constexpr uint32_t kRecKey = 1u << 21, kRecShared = 1u << 20;
 
 // the products of one staged task on the matrix cores: each wave takes blocks of 32 output rows
 // (both channels), writes tkey / info / sums and marks lone bucket leaders. No barrier; returns
@@ -440,6 +459,19 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
                     if (eb && o.bpack && o.ghead && o.ghead[s] == 0u) leader_mark(o.bpack, tmin, __popc(eb));
                 }
                 any |= eb != 0;
+            }
+            if (o.recs && h == 0) {   // iblk: the key's A edge (dense slot) and B edge j
+                uint32_t rv = 0;
+                const bool shared = tmin != kInf && o.ghead && o.ghead[s] != 0u;
+                if (tmin != kInf && (eb || shared)) {
+                    uint32_t j;
+                    const uint32_t i = div_small(tmin, o.nB, o.nb_m, j);
+                    const uint32_t ij = o.bjt[j] & 0xFFFFu;
+                    const uint32_t x = r >= ij ? r - ij : r + Bm - ij;
+                    const uint32_t dd = tt[x] == i * o.nB ? x : Bm + x;
+                    rv = dd | j << 12 | eb << 18 | (shared ? kRecShared : 0u) | kRecKey;
+                }
+                o.recs[r] = rv;
             }
         }
     }
@@ -690,31 +722,18 @@ __global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
 // edges from their own A edge's count to the leader's, and every A edge range holding such a key
 // is flagged so that `order` ranks its keys by probing the range's |B.E| times instead.
 
-// t = i D + j for D <= 63: m = floor(2^32 / D), i = (t m) >> 32 is i or i - 1
-__device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t D, uint64_t m, uint32_t& j) {
-    uint32_t i = (uint32_t)(((uint64_t)t * m) >> 32);
-    uint32_t r = t - i * D;
-    if (r >= D) {
-        ++i;
-        r -= D;
-    }
-    j = r;
-    return i;
-}
-
-// After the tasks of A layer la (all B layers) have stored tkey / info: M1[d] / M2[d] = bit j for
-// the keys whose first-insert time is (A edge at dense slot d, B edge j) and that emit a P / an M
-// edge, bit 63 of M1 = a key of a shared bucket lies in the range; then icnt[i], imask[i] and each
-// key's rank (info bits 8..15, bit 2 = probe in `order`). M1 / M2 use the dense digit table's LDS
-// (dead now), tt still maps A edge i to its dense slot. Barriers inside; every thread calls it.
+// After the tasks of A layer la (all B layers) have left one record per key in recs (the MFMA
+// epilogue: the dense slot d of the key's A edge, its B edge j, its edge bits): M1[d] / M2[d] = bit j
+// for the keys whose first-insert time is (A edge at d, B edge j) and that emit a P / an M edge,
+// bit 63 of M1 = a key of a shared bucket lies in the range; then icnt[i], imask[i] and each key's
+// rank (info bits 8..15, bit 2 = probe in `order`). M1 / M2 use the dense digit table's LDS (dead
+// now), tt maps dense slot d back to its A edge. Barriers inside; every thread calls it.
 template <int BS>
 __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_desc& d, uint32_t la, uint4 lbq,
-                           uint32_t neB, const uint32_t* bjt, uint32_t* icnt, ulonglong2* imask) {
+                           uint32_t neB, const uint32_t* recs, uint32_t* icnt, ulonglong2* imask) {
     const uint32_t Bm = g.Bm, nB = d.nB, LB = d.LB;
     uint32_t* S = g.scratch;
-    const uint32_t* tkey = S + d.o_tkey;
     uint32_t* info = S + d.o_info;
-    const uint32_t* ghead = group_heads(g, d);
     unsigned long long* M1 = (unsigned long long*)plds;
     unsigned long long* M2 = M1 + 2u * Bm;
     const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
@@ -722,46 +741,19 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
     const uint32_t tid = threadIdx.x, nk = neB * Bm;
     for (uint32_t k = tid; k < 4u * Bm; k += BS) M1[k] = 0ull;
     __syncthreads();
-    // a key's A edge i sits at dense slot (ch, (r - idx_j) mod B) for ch 0 or 1: tt names it
-    auto locate = [&](uint32_t q, uint64_t& s, uint32_t& t, uint32_t& j, uint32_t& dd) {
-        uint32_t kb = 0, r = q;
-        while (r >= Bm) {
-            r -= Bm;
-            ++kb;
-        }
-        const uint32_t lb = kb == 0 ? lbq.x : kb == 1 ? lbq.y : kb == 2 ? lbq.z : lbq.w;
-        s = (uint64_t)(la * LB + lb) * Bm + r;
-        t = tkey[s];
-        if (t == kInf) return;
-        const uint32_t i = div_small(t, nB, m, j);
-        const uint32_t ij = bjt[j] & 0xFFFFu;
-        const uint32_t x = r >= ij ? r - ij : r + Bm - ij;
-        dd = tt[x] == i * nB ? x : Bm + x;
-    };
-    // pass A; the first kQ keys of each thread keep dd | j << 12 | e << 18 (0: no edges) for pass B
-    constexpr int kQ = 6;
-    uint32_t keep[kQ];
-    auto mark = [&](uint32_t q) -> uint32_t {
-        uint64_t s;
-        uint32_t t, j, dd;
-        locate(q, s, t, j, dd);
-        if (t == kInf) return 0u;
-        const uint32_t e = info[s] & 3u;
-        const bool shared = ghead && ghead[s] != 0u;
+    bool shared = false;
+    for (uint32_t q = tid; q < nk; q += BS) {
+        const uint32_t v = recs[q];
+        if (!v) continue;
+        const uint32_t dd = v & 0xFFFu, j = (v >> 12) & 63u, e = (v >> 18) & 3u;
         if (e & 1u) atomicOr(&M1[dd], 1ull << j);
         if (e & 2u) atomicOr(&M2[dd], 1ull << j);
-        if (shared) {   // with or without edges: it may lead its bucket
+        if (v & kRecShared) {   // with or without edges: it may lead its bucket
             atomicOr(&M1[dd], 1ull << 63);
-            S[d.o_cnt + kCntIShared] = 1u;
+            shared = true;
         }
-        return e ? dd | j << 12 | e << 18 : 0u;
-    };
-#pragma unroll
-    for (int k = 0; k < kQ; ++k) {
-        const uint32_t q = tid + (uint32_t)k * BS;
-        keep[k] = q < nk ? mark(q) : 0u;
     }
-    for (uint32_t q = tid + kQ * BS; q < nk; q += BS) mark(q);
+    if (shared) S[d.o_cnt + kCntIShared] = 1u;
     __syncthreads();
     for (uint32_t dd = tid; dd < 2u * Bm; dd += BS) {
         const uint32_t ch = dd >= Bm ? 1u : 0u;
@@ -773,35 +765,23 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         icnt[i] = (uint32_t)__popcll(x1) + (uint32_t)__popcll(x2);
         imask[i] = make_ulonglong2(x1, x2);
     }
-    auto ranked = [&](uint64_t s, uint32_t dd, uint32_t j, uint32_t e) {
-        const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
-        const unsigned long long x1 = M1[dd];
-        const uint32_t rank = (uint32_t)__popcll(x1 & above) + (uint32_t)__popcll(M2[dd] & above);
-        info[s] = e | (uint32_t)(x1 >> 63) << 2 | rank << 8;
-    };
-    auto slot_of = [&](uint32_t q) {
+    for (uint32_t q = tid; q < nk; q += BS) {
+        const uint32_t v = recs[q];
+        const uint32_t e = (v >> 18) & 3u;
+        if (!e) continue;
+        const uint32_t dd = v & 0xFFFu, j = (v >> 12) & 63u;
         uint32_t kb = 0, r = q;
         while (r >= Bm) {
             r -= Bm;
             ++kb;
         }
         const uint32_t lb = kb == 0 ? lbq.x : kb == 1 ? lbq.y : kb == 2 ? lbq.z : lbq.w;
-        return (uint64_t)(la * LB + lb) * Bm + r;
-    };
-#pragma unroll
-    for (int k = 0; k < kQ; ++k) {
-        const uint32_t v = keep[k];
-        if (v) ranked(slot_of(tid + (uint32_t)k * BS), v & 0xFFFu, (v >> 12) & 63u, v >> 18);
+        const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
+        const unsigned long long x1 = M1[dd];
+        const uint32_t rank = (uint32_t)__popcll(x1 & above) + (uint32_t)__popcll(M2[dd] & above);
+        info[(uint64_t)(la * LB + lb) * Bm + r] = e | (uint32_t)(x1 >> 63) << 2 | rank << 8;
     }
-    for (uint32_t q = tid + kQ * BS; q < nk; q += BS) {
-        uint64_t s;
-        uint32_t t, j, dd;
-        locate(q, s, t, j, dd);
-        if (t == kInf) continue;
-        const uint32_t e = info[s] & 3u;
-        if (e) ranked(s, dd, j, e);
-    }
-    __syncthreads();   // the next A layer's staging overwrites M1 / M2 and tt
+    __syncthreads();   // the next A layer's staging overwrites M1 / M2, tt and recs
 }
 
 // One workgroup per (pair, kLaPerWG A layers) for pairs with at most kLaMaxLB B layers (chain
@@ -857,6 +837,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
     // fallen back (cnt[kCntIFail], set by k_large_lists or by a workgroup below)
     bool ib = d.iblk && !S[d.o_cnt + kCntIFail];
     uint32_t* bjt = (uint32_t*)(sreg + kLaMaxLB * kMxSparseBytes);   // B edge j: idx | ch << 16
+    uint32_t* recs = bjt + 64;                                           // [kLaMaxLB][B] key records
     if (ib && threadIdx.x < nB) {   // published by the dense staging's barriers
         const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + threadIdx.x];
         bjt[threadIdx.x] = meta_idx(mb) | meta_ch(mb) << 16;
@@ -884,7 +865,14 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
                     if (!((mxm >> k) & 1u)) continue;
                     const uint4* prec = (const uint4*)(sreg + k * kMxSparseBytes);
                     const uint32_t lp = la * LB + lbv[k];
-                    if (mx_blocks<BS>(plds, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, (uint64_t)lp * Bm, o))
+                    task_out ok = o;
+                    if (ib) {
+                        ok.recs = recs + k * Bm;
+                        ok.bjt = bjt;
+                        ok.nB = nB;
+                        ok.nb_m = d.nb_m;
+                    }
+                    if (mx_blocks<BS>(plds, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, (uint64_t)lp * Bm, ok))
                         S[d.o_used + (LA + LB) + lp] = 1;
                 }
             } else {
@@ -907,7 +895,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
             if (mxm == (1u << neB) - 1u) {
                 static_assert(kLaMaxLB == 4, "iblk_layer takes the B layers as a uint4");
                 for (int rep_ = 0; rep_ < PVAC_EXP_IBREP; ++rep_)   // experiment builds repeat it (idempotent)
-                    iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, bjt, S + d.o_icnt,
+                    iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, recs, S + d.o_icnt,
                                    (ulonglong2*)(S + d.o_imask));
             } else {
                 if (threadIdx.x == 0) atomicExch(&S[d.o_cnt + kCntIFail], 1u);
@@ -1517,7 +1505,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
             b.lds_task = mx_lds_bytes(a.Bm);   // the scatter mode (52 B per slot) fits below it
             hipLaunchKernelGGL((k_large_products_la<kLPX>), dim3((unsigned)a.max_la_wg, a.la_xcd ? (a.n_la + 7u) & ~7u : a.n_la),
                                dim3(kLPX),
-                               (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes + kIblkBjtBytes, st, b);
+                               (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes + kIblkBjtBytes + kLaMaxLB * 4u * a.Bm, st, b);
             hipLaunchKernelGGL((k_large_products_defer<kLPX>), dim3(kDeferWG, a.n_la), dim3(kLPX), plds, st, a);
         }
     }
