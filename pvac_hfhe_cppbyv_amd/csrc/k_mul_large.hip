@@ -70,17 +70,26 @@ __device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* part
 }
 
 // ---------------------------------------------------------------- init
-// iblk pairs leave the block marks alone (k_large_layers clears them for a pair that falls back):
-// only cnt and the used flags are zeroed (static groups have no bucket table)
+// iblk pairs leave the block marks alone (k_large_layers clears them for a pair that falls back)
+// and tkey (iblk_dead): only cnt and the used flags are zeroed (static groups have no bucket table)
 __global__ __launch_bounds__(kLB) void k_large_init(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.y];
     const uint64_t stride = (uint64_t)gridDim.x * kLB;
     const uint64_t nz = d.iblk ? kCntWords + d.Lc : d.zero_words;
-    const uint64_t lim = nz > d.S ? nz : d.S;
+    const uint64_t nt = d.iblk ? 0 : d.S;   // iblk: products sets every slot of a live layer pair
+    const uint64_t lim = nz > nt ? nz : nt;
     for (uint64_t w = (uint64_t)blockIdx.x * kLB + threadIdx.x; w < lim; w += stride) {
         if (w < nz) g.scratch[d.iblk && w >= kCntWords ? d.o_used + (w - kCntWords) : d.o_zero + w] = 0;
-        if (w < d.S) g.scratch[d.o_tkey + w] = kInf;
+        if (w < nt) g.scratch[d.o_tkey + w] = kInf;
     }
+}
+
+// iblk pairs leave tkey unset in the layer pairs (la, lb) with no edges on one side: no products
+// there, so no keys; the passes that walk every slot skip them
+__device__ __forceinline__ bool iblk_dead(const uint32_t* S, const large_desc& d, uint64_t s, uint32_t Bm) {
+    if (!d.iblk) return false;
+    const uint32_t lp = (uint32_t)s / Bm, la = lp / d.LB, lb = lp - la * d.LB;
+    return S[d.o_lstA + d.LA + la] == 0u || S[d.o_lstB + d.LB + lb] == 0u;
 }
 
 // ---------------------------------------------------------------- per-layer edge lists
@@ -1066,12 +1075,13 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
         // and `order` takes t_b = its own time, within = 0
         const uint32_t q0 = stat ? ghead[s] : 1u;
         if (!q0 && fb) {
+            if (iblk_dead(S, d, s, g.Bm)) continue;
             const uint32_t t = tkey[s];
             const uint32_t E = t == kInf ? 0u : __popc(info[s] & 3u);
             if (E) leader_mark(bpack, t, E);
             continue;
         }
-        if (!q0) continue;
+        if (!q0 || iblk_dead(S, d, s, g.Bm)) continue;
         const uint32_t t = tkey[s];
         if (t == kInf) continue;
         uint32_t tmin = t, w = 0, E = 0;
@@ -1082,7 +1092,7 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
             while (q) {
                 const uint32_t s2 = q - 1;
                 q = gnext[s2];
-                if (s2 >= d.S) continue;
+                if (s2 >= d.S || iblk_dead(S, d, s2, g.Bm)) continue;
                 const uint32_t t2 = tkey[s2];
                 if (t2 == kInf) continue;
                 const uint32_t e2 = __popc(info[s2] & 3u);
@@ -1193,7 +1203,7 @@ __global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
     uint32_t carry = 0;
     for (uint64_t s0 = 0; s0 < d.S; s0 += kLBig) {
         const uint64_t s = s0 + tid;
-        const uint32_t v = (s < d.S && tkey[s] != kInf) ? (uint32_t)__popc(info[s] & 3u) : 0u;
+        const uint32_t v = (s < d.S && !iblk_dead(S, d, s, g.Bm) && tkey[s] != kInf) ? (uint32_t)__popc(info[s] & 3u) : 0u;
         uint32_t tot;
         const uint32_t ex = wg_exclusive_scan<kLBig>(v, part, tot);
         if (s < d.S) cpos[s] = carry + ex;
@@ -1242,6 +1252,7 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
         return w;
     };
     for (uint64_t s = (uint64_t)blockIdx.x * kLB + threadIdx.x; s < d.S; s += (uint64_t)gridDim.x * kLB) {
+        if (iblk_dead(S, d, s, Bm)) continue;
         const uint32_t ts = tkey[s];
         if (ts == kInf) continue;
         const uint32_t inf = info[s];
