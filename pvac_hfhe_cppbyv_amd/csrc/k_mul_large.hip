@@ -109,11 +109,21 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     for (uint32_t l = tid; l < LA + LB; l += kLBig) hist[l] = 0;
     if (tid == 0) flag = 0;
     __syncthreads();
-    for (uint32_t i = tid; i < nA; i += kLBig) {
-        const uint64_t m = g.A.meta[aeo + i];
-        const uint32_t la = meta_layer(m);
-        if (la >= LA || meta_idx(m) >= Bm || meta_ch(m) > 1) flag = 1;
-        else atomicAdd(&hist[la], 1u);
+    // four edges per thread and round, loads first (one WG walks a pair's |A.E| edges twice)
+    for (uint32_t i0 = tid; i0 < nA; i0 += 4u * kLBig) {
+        uint64_t m[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * kLBig;
+            m[u] = i < nA ? g.A.meta[aeo + i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i0 + (uint32_t)u * kLBig >= nA) break;
+            const uint32_t la = meta_layer(m[u]);
+            if (la >= LA || meta_idx(m[u]) >= Bm || meta_ch(m[u]) > 1) flag = 1;
+            else atomicAdd(&hist[la], 1u);
+        }
     }
     for (uint32_t j = tid; j < nB; j += kLBig) {
         const uint64_t m = g.B.meta[beo + j];
@@ -152,9 +162,19 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     __syncthreads();
     uint32_t* idsA = S + d.o_lstA + 2 * LA;
     uint32_t* idsB = S + d.o_lstB + 2 * LB;
-    for (uint32_t i = tid; i < nA; i += kLBig) {
-        const uint32_t la = meta_layer(g.A.meta[aeo + i]);
-        idsA[atomicAdd(&hist[la], 1u)] = i;
+    for (uint32_t i0 = tid; i0 < nA; i0 += 4u * kLBig) {
+        uint32_t la[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * kLBig;
+            la[u] = i < nA ? meta_layer(g.A.meta[aeo + i]) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * kLBig;
+            if (i >= nA) break;
+            idsA[atomicAdd(&hist[la[u]], 1u)] = i;
+        }
     }
     for (uint32_t j = tid; j < nB; j += kLBig) {
         const uint32_t lb = meta_layer(g.B.meta[beo + j]);
