@@ -754,15 +754,14 @@ __global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
 // After the tasks of A layer la (all B layers) have left one record per key in recs (the MFMA
 // epilogue: the dense slot d of the key's A edge, its B edge j, its edge bits): M1[d] / M2[d] = bit j
 // for the keys whose first-insert time is (A edge at d, B edge j) and that emit a P / an M edge,
-// bit 63 of M1 = a key of a shared bucket lies in the range; then icnt[i], imask[i] and each key's
-// rank (info bits 8..15, bit 2 = probe in `order`). M1 / M2 use the dense digit table's LDS (dead
-// now), tt maps dense slot d back to its A edge. Barriers inside; every thread calls it.
+// bit 63 of M1 = a key of a shared bucket lies in the range (`order` probes it); then icnt[i] and,
+// for ranges with keys, imask[i] = (M1, M2). M1 / M2 use the dense digit table's LDS (dead now), tt
+// maps dense slot d back to its A edge. Barriers inside; every thread calls it.
 template <int BS>
 __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_desc& d, uint32_t la, uint4 lbq,
                            uint32_t neB, const uint32_t* recs, uint32_t* icnt, ulonglong2* imask) {
-    const uint32_t Bm = g.Bm, nB = d.nB, LB = d.LB;
+    const uint32_t Bm = g.Bm, nB = d.nB;
     uint32_t* S = g.scratch;
-    uint32_t* info = S + d.o_info;
     unsigned long long* M1 = (unsigned long long*)plds;
     unsigned long long* M2 = M1 + 2u * Bm;
     const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
@@ -790,25 +789,11 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         if (te == kInf) continue;
         uint32_t j;
         const uint32_t i = div_small(te, nB, m, j);
-        const unsigned long long x1 = M1[dd] & ~(1ull << 63), x2 = M2[dd];
-        icnt[i] = (uint32_t)__popcll(x1) + (uint32_t)__popcll(x2);
-        imask[i] = make_ulonglong2(x1, x2);
-    }
-    for (uint32_t q = tid; q < nk; q += BS) {
-        const uint32_t v = recs[q];
-        const uint32_t e = (v >> 18) & 3u;
-        if (!e) continue;
-        const uint32_t dd = v & 0xFFFu, j = (v >> 12) & 63u;
-        uint32_t kb = 0, r = q;
-        while (r >= Bm) {
-            r -= Bm;
-            ++kb;
-        }
-        const uint32_t lb = kb == 0 ? lbq.x : kb == 1 ? lbq.y : kb == 2 ? lbq.z : lbq.w;
-        const unsigned long long above = (~0ull << (j + 1)) & ~(1ull << 63);
-        const unsigned long long x1 = M1[dd];
-        const uint32_t rank = (uint32_t)__popcll(x1 & above) + (uint32_t)__popcll(M2[dd] & above);
-        info[(uint64_t)(la * LB + lb) * Bm + r] = e | (uint32_t)(x1 >> 63) << 2 | rank << 8;
+        const unsigned long long x1 = M1[dd], x2 = M2[dd];
+        icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
+        // only ranges that hold keys are read back (write_ranges, order): most A edges of a deep
+        // chain step hold none (their keys were all inserted by earlier A edges)
+        if (x1 | x2) imask[i] = make_ulonglong2(x1, x2);
     }
     __syncthreads();   // the next A layer's staging overwrites M1 / M2, tt and recs
 }
@@ -1253,6 +1238,7 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     const bool ib = d.iblk && !cnt[kCntIFail];
     if (ib && !canonical && !cnt[kCntIShared]) return;   // k_large_write_ranges
     const uint32_t* icnt = S + d.o_icnt;
+    const ulonglong2* imask = (const ulonglong2*)(S + d.o_imask);
     const uint64_t m = d.nb_m;
     // iblk: edges emitted before the emit time (i, j) inside A edge i's range, by probing its later
     // times (i, j'): the key slot of (i, j') is known from the two edges, and (i, j') is an emit time
@@ -1280,10 +1266,12 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
         if (!eb) continue;
         const bool lone = ghead && ghead[s] == 0u;   // its own bucket leader, nothing before it
         if (ib) {
-            uint32_t hp;
-            if (lone && !(inf & 4u)) {   // ranked by products
-                uint32_t j;
-                hp = icnt[div_small(ts, nB, m, j)] + (inf >> 8);
+            uint32_t hp, j0;
+            const uint32_t i0 = lone ? div_small(ts, nB, m, j0) : 0u;
+            const ulonglong2 mk = lone ? imask[i0] : make_ulonglong2(0ull, 0ull);
+            if (lone && !(mk.x >> 63)) {   // a range without shared keys: rank from its masks
+                const unsigned long long above = (~0ull << (j0 + 1)) & ~(1ull << 63);
+                hp = icnt[i0] + (uint32_t)__popcll(mk.x & above) + (uint32_t)__popcll(mk.y & above);
             } else {
                 const uint32_t tu = lone ? ts : tb[s];
                 uint32_t j;
@@ -1394,11 +1382,14 @@ __global__ __launch_bounds__(kLB) void k_large_write_ranges(mul_large_args g) {
         const uint32_t r = c * 64u + lane;
         const bool live = r < nA;
         const uint32_t i = live ? nA - 1u - r : 0u;
-        const ulonglong2 mk = live ? imask[i] : make_ulonglong2(0ull, 0ull);
+        // the range's edge count from the offsets (off[i - 1] - off[i], the total for i = 0); the
+        // masks and the A edge are read only for ranges that hold keys
+        const uint32_t oi = live ? off[i] : 0u;
+        const uint32_t E = live ? (i ? off[i - 1] : cnt[3]) - oi : 0u;
+        const ulonglong2 mk = E ? imask[i] : make_ulonglong2(0ull, 0ull);
         const uint32_t o0 = off[nA - 1u - c * 64u];   // the chunk's first position (lane 0's range)
-        const uint64_t ma = live ? g.A.meta[aeo + i] : 0ull;
+        const uint64_t ma = E ? g.A.meta[aeo + i] : 0ull;
         const uint32_t la_idx = meta_idx(ma) | meta_layer(ma) << 16;
-        const uint32_t E = (uint32_t)__popcll(mk.x) + (uint32_t)__popcll(mk.y);
         const uint32_t incl = wave_incl_scan_u32(E);
         const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
         // position q of the chunk -> key slot s and channel; every lane takes part in the bpermutes
