@@ -818,6 +818,10 @@ def chain_bench(eng, args):
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
     n_chk = max(0, min(args.chain_check, chunk))
     S = max(1, args.chain_streams)
+    # the earlier side legs' cached blocks go back to the driver first: with them the chain's
+    # streams ran out of free HBM mid-run and torch's free-and-retry stalled single steps for seconds
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)
     _enc_keys(eng)
     vals = torch.empty(n, dtype=torch.int64, device=dev)
