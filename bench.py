@@ -51,9 +51,10 @@ def parse():
                          "with the pinned CPU port, which is also timed on them (cpu_baseline)")
     ap.add_argument("--chain-ref", type=int, default=2, help="cfg 4: reference chains (oracle/_ref) timed, depth 4")
     ap.add_argument("--chain-streams", type=int, default=4,
-                    help="cfg 4: host threads / HIP streams running chunks: one chunk's host planning and "
-                         "dependent launches overlap the other chunks' kernels (tools/chain_streams_cmp.sh: "
-                         "1 x 4096: 273 K ct_mul/s, 4 x 1024: 371-433 K, same 141 GB of HBM)")
+                    help="cfg 4: worker streams of the engine's chain call (pvac_hip_ct_mul_chain): one chunk's "
+                         "host planning and dependent launches overlap the other chunks' kernels")
+    ap.add_argument("--chain-compare-streams", action="store_true",
+                    help="cfg 4: also time the chain call with 1 worker stream on a subset (side field)")
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
     ap.add_argument("--only", choices=["chain", "sigma", "fp", "enc", "add"], default=None,
                     help="run one side measurement alone (profiling) and print its JSON")
@@ -806,24 +807,28 @@ def _ref_enc_baseline():
 
 def chain_bench(eng, args):
     """cfg 4 (SURVEY 8(d) restatement of test_depth): x_i = enc_value(v_i) on the GPU for all 2^16
-    inputs (timed on its own), then c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) to depth 8 in chunks.
-    Every ct_mul step is plan + exec on the general path. Chunks are dealt to `--chain-streams`
-    host threads, each with its own engine context on its own HIP stream, so one chunk's
-    VALU-bound products overlap another chunk's atomic / memory-bound ordering kernels."""
-    import threading
+    inputs (timed on its own), then c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) to depth 8
+    (tests/test_main.cpp:289-295). One library call (pvac_hip_ct_mul_chain) runs every chain: the
+    engine cuts the inputs into chunks and runs them on `--chain-streams` internal worker streams,
+    each step plan + exec on the general path. The timed pass does nothing else: no checks, no
+    read-backs, wall clock from the call to its return. A second, untimed pass with the same nonces
+    runs the reference's gsum invariant on every pair of every step and digests every final chain;
+    its digests must equal the timed pass's (first chains) and the pinned CPU port's."""
     import numpy as np
     import torch
-    from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine, powg_table
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, powg_table
     dev = eng.device
     n, chunk, depth = args.chain_inputs, min(args.chain_chunk, args.chain_inputs), args.chain_depth
-    n_chk = max(0, min(args.chain_check, chunk))
+    n_chk = max(0, min(args.chain_check, n))
     S = max(1, args.chain_streams)
-    # the earlier side legs' cached blocks go back to the driver first: with them the chain's
-    # streams ran out of free HBM mid-run and torch's free-and-retry stalled single steps for seconds
+    seed = 0x5EED0040
+    # the earlier side legs' cached blocks go back to the driver first (the chain's workers size
+    # their scratch from the free HBM)
     torch.cuda.synchronize(dev)
     torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)
     _enc_keys(eng)
+    eng.set_powg(powg_table(eng.params.B))
     vals = torch.empty(n, dtype=torch.int64, device=dev)
     rnd = torch.empty(n * ENC_STRIDE, dtype=torch.int64, device=dev)
     eng.fill_random(vals, 0x5EED0004)
@@ -840,107 +845,43 @@ def chain_bench(eng, args):
         return DeviceBatch(k, X_all.l_off[c0:c0 + k], X_all.l_cnt[c0:c0 + k], X_all.layers, X_all.e_off[c0:c0 + k],
                            X_all.e_cnt[c0:c0 + k], X_all.meta, X_all.w_lo, X_all.w_hi)
 
-    results = [dict(step_ms=[0.0] * depth, step_edges=[0.0] * depth, products=0.0, last_ms=[], gsum_failed=0,
-                    gsum_pairs=0, check_s=0.0) for _ in range(S)]
-    ready = threading.Barrier(S + 1)
-
-    def warm(e2, stream):
-        # one untimed chunk through every depth: sizes the context's scratch arena and this
-        # stream's cached blocks (a first allocation of tens of GB waits for the driver to clear
-        # the VRAM, ~1.5 s, once)
-        k = min(chunk, n)
-        X = view(0, k)
-        cur = X
-        for d in range(depth):
-            Cb, plan = e2.ct_mul_plan(cur, X)
-            nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=dev)
-            e2.fill_random(nonces, 0x5EED0F40 + d)
-            cur = e2.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
-        stream.synchronize()
-
-    def worker(w):
-        r = results[w]
-        released = False
-        try:
-            stream = torch.cuda.Stream(dev)
-            with torch.cuda.device(dev), torch.cuda.stream(stream):
-                e2 = Engine(device=dev.index, canon_tag=eng.params.canon_tag)   # binds to `stream`
-                e2.set_powg(powg_table(e2.params.B))
-                warm(e2, stream)
-                ready.wait()
-                released = True
-                for c0 in range(w * chunk, n, S * chunk):
-                    k = min(chunk, n - c0)
-                    X = view(c0, k)
-                    cur = X
-                    for d in range(depth):
-                        ts = time.perf_counter()
-                        Cb, plan = e2.ct_mul_plan(cur, X)
-                        nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=dev)
-                        e2.fill_random(nonces, 0x5EED0040 + 97 * c0 + d)
-                        out = e2.ct_mul(cur, X, nonces=nonces, C_=Cb, plan=plan)
-                        stream.synchronize()
-                        r["step_ms"][d] += 1000.0 * (time.perf_counter() - ts)
-                        if d == depth - 1:
-                            r["last_ms"].append(round(1000.0 * (time.perf_counter() - ts), 1))
-                        # the gsum invariant on every pair of every step (its time is taken out)
-                        tc = time.perf_counter()
-                        r["gsum_failed"] += e2.check_mul_gsum(cur, X, out, nonces)
-                        r["gsum_pairs"] += k
-                        if c0 == 0 and d == depth - 1 and n_chk:   # the oracle sample's GPU side
-                            r["chk_digests"] = e2.digest(_head(out, n_chk)).cpu().numpy().view(np.uint64).copy()
-                            r["chk_counts"] = out.e_cnt[:n_chk].cpu().numpy().view(np.uint64).copy()
-                        # the line's product / edge statistics (torch reductions + read-backs) are
-                        # bookkeeping, taken out of the timed region with the checks
-                        r["products"] += float((cur.e_cnt[:k].to(torch.float64) *
-                                                X.e_cnt[:k].to(torch.float64)).sum().item())
-                        r["step_edges"][d] += float(out.e_cnt[:k].sum().item())
-                        r["check_s"] += time.perf_counter() - tc
-                        del Cb, nonces, plan
-                        cur = out
-                    # chunks reuse this stream's cached blocks (re-allocating ~10 GB per chunk made
-                    # the driver clear fresh VRAM and stalled single steps for seconds)
-                    del cur, X, out
-                stream.synchronize()
-                del e2
-        except Exception as ex:   # reported, never hidden
-            r["error"] = repr(ex)
-            if not released:
-                ready.abort()
-
-    threads = [threading.Thread(target=worker, args=(w,)) for w in range(S)]
-    for t in threads:
-        t.start()
-    try:
-        ready.wait()   # every worker warmed up
-    except threading.BrokenBarrierError:
-        pass
-    t1 = time.perf_counter()
-    for t in threads:
-        t.join()
+    # warm-up (untimed): one chunk per worker through every depth sizes each worker's arena and
+    # output buffers (a first allocation of tens of GB waits for the driver to clear the VRAM)
+    eng.ct_mul_chain(view(0, min(n, S * chunk)), depth, nonce_seed=seed ^ 0xFFFF, streams=S, chunk=chunk)
     torch.cuda.synchronize(dev)
-    # minus the untimed invariant checks (workers run them in turn on their own stream)
-    check_s = max(r["check_s"] for r in results)
-    chain_s = time.perf_counter() - t1 - check_s
+    # timed pass: the chains and nothing else
+    t1 = time.perf_counter()
+    r = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, digest_n=n_chk)
+    torch.cuda.synchronize(dev)
+    chain_s = time.perf_counter() - t1
+    peak = torch.cuda.max_memory_reserved(dev) / 1e9
+    # check pass (untimed): same nonces, gsum invariant on every pair-step, every final digest
+    t2 = time.perf_counter()
+    rc = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, check_gsum=True, digest_n=n)
+    check_s = time.perf_counter() - t2
+    same = bool(n_chk == 0 or (np.array_equal(rc["digests"][:n_chk], r["digests"]) and
+                               np.array_equal(rc["counts"][:n_chk], r["counts"])))
     x_host = _pack_host(X_all, n_chk) if n_chk else None   # the sampled chains' inputs
     del X_all, vals
-    errors = [r["error"] for r in results if "error" in r]
-    step_ms = [sum(r["step_ms"][d] for r in results) for d in range(depth)]
-    step_edges = [sum(r["step_edges"][d] for r in results) for d in range(depth)]
-    products = sum(r["products"] for r in results)
+    products = float(sum(r["products"]))
     out = {"inputs": n, "depth": depth, "chunk": chunk, "streams": S, "producer": "GPU enc_value (weights-only)",
+           "engine_call": "pvac_hip_ct_mul_chain (one caller thread; the engine's own worker streams)",
            "seconds": enc_s + chain_s, "enc_seconds": enc_s, "chain_seconds": chain_s,
+           "library_seconds": r["seconds"],
            "chains_per_s": n / (enc_s + chain_s), "ct_mul_per_s": n * depth / chain_s,
            "ct_mul_per_s_incl_enc": n * depth / (enc_s + chain_s),
+           "timing": "wall clock of the timed call alone (synchronised on both sides); no checks or read-backs "
+                     "inside it; the invariant and digests come from a second, untimed pass",
            "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
-           "edges_per_input_by_step": [e / n for e in step_edges],
-           "stream_ms_by_step": step_ms, "last_step_ms_by_chunk": [r["last_ms"] for r in results],
-           "peak_hbm_reserved_gb": torch.cuda.max_memory_reserved(dev) / 1e9}
-    gf, gp = sum(r["gsum_failed"] for r in results), sum(r["gsum_pairs"] for r in results)
+           "edges_per_input_by_step": [e / n for e in r["edges"]],
+           "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak}
+    gf, gp = rc["gsum_failed"], rc["gsum_pairs"]
     out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
-                                 "step, on the device (untimed)", "pair_steps": gp, "failed": gf,
-                        "invariant_ok": gf == 0 and gp == n * depth, "check_seconds": check_s}
+                                 "step, on the device (second, untimed pass with the same nonces)", "pair_steps": gp,
+                        "failed": gf, "invariant_ok": gf == 0 and gp == n * depth, "check_pass_seconds": check_s,
+                        "timed_pass_digests_equal": same,
+                        "edges_equal": rc["edges"] == r["edges"]}
     # Roofline of the products: per second against the matrix-core ceiling measured on this GPU
     # (k_ubench.hip k_probe_mfma8: back-to-back v_mfma_i32_32x32x32_i8, 64 dense-mode products
     # each); the round-2 column-accumulator (col26_mac) and round-1 fp_mul_fold1 VALU ceilings
@@ -954,12 +895,34 @@ def chain_bench(eng, args):
                            "col26_ceiling": eng.alu_ceiling(3), "fold1_ceiling": eng.alu_ceiling(1)}
     except Exception as ex:
         out["roofline"] = {"error": repr(ex)}
-    if errors:
-        out["errors"] = errors
+    if args.chain_compare_streams:
+        # the same call with S worker streams and with ONE on 4 chunks per worker of new inputs
+        try:
+            out["streams_compare"] = _chain_streams_compare(eng, args, min(n, 4 * S * chunk), depth, chunk, S, seed)
+        except Exception as ex:
+            out["streams_compare"] = {"error": repr(ex)}
     if n_chk and x_host is not None:
-        out.update(_chain_cpu(args, x_host, n_chk, depth, results[0].get("chk_digests"),
-                              results[0].get("chk_counts"), n * depth / chain_s))
+        out.update(_chain_cpu(args, x_host, n_chk, depth, r.get("digests"), r.get("counts"), n * depth / chain_s))
     return out
+
+
+def _chain_streams_compare(eng, args, k, depth, chunk, S, seed):
+    """ct_mul/s of the chain call on k fresh enc_value inputs with S worker streams and with 1."""
+    import torch
+    vals = torch.empty(k, dtype=torch.int64, device=eng.device)
+    rnd = torch.empty(k * ENC_STRIDE, dtype=torch.int64, device=eng.device)
+    eng.fill_random(vals, 0x5EED2004)
+    eng.fill_random(rnd, 0x5EED3004)
+    X, _ = eng.enc_value(vals, rnd)
+    res = {"inputs": k}
+    for s in (S, 1):
+        eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=s, chunk=chunk)   # warm
+        torch.cuda.synchronize(eng.device)
+        t = time.perf_counter()
+        eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=s, chunk=chunk)
+        torch.cuda.synchronize(eng.device)
+        res[f"streams_{s}_ct_mul_per_s"] = k * depth / (time.perf_counter() - t)
+    return res
 
 
 def _head(X, k):

@@ -187,6 +187,56 @@ int pvac_hip_ct_mul_status(pvac_hip_ctx* ctx, uint32_t* out, size_t n);
 int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, const pvac_ct_batch* C,
                             const uint64_t* nonces, uint32_t* status, uint64_t* n_bad);
 
+/* ---------------------------------------------------------------- depth chains
+ * c_0 = X[i], c_k = ct_mul(c_{k-1}, X[i]) for k = 1..depth, for every input i of X: the reference's
+ * chain workload (tests/test_main.cpp:289-295, c = ct_mul(pk, c, x) in a loop) over a batch of
+ * independent inputs. The library cuts X into chunks of `chunk` inputs and runs them on `streams`
+ * worker threads, each with its own HIP stream, scratch arena and output buffers (child contexts
+ * kept by ctx between calls), chunks handed out in input order. One chunk's host planning (the
+ * plan's shape read-back) and its short dependent launches overlap other chunks' kernels, so a
+ * single caller thread gets the concurrency. Synchronous: returns when every chunk is done.
+ * Each step is exactly pvac_hip_ct_mul_plan + pvac_hip_ct_mul_exec (weights only, reference hash
+ * order unless flags has PVAC_MUL_ORDER_CANONICAL; WITH_SIGMA is not accepted here).
+ * Nonces: fill_nonces(user, step, first_input, n_words, dev_words, stream) when given (called on
+ * the worker thread; fill n_words device words on `stream`, the 2-words-per-output-layer-slot
+ * array of pvac_hip_ct_mul_exec), else splitmix64 words: pvac_hip_fill_random with seed
+ * nonce_seed + 97 * first_input + step (step counted from 0).
+ * Outputs are streamed: on_chunk(user, first_input, C, stream) receives each chunk's final
+ * c_depth (device batch, capacity-padded CSR) valid until it returns; digest_out / count_out
+ * (DEVICE, nullable) receive pvac_hip_batch_digest and |E| of c_depth for inputs [0, digest_n).
+ * PVAC_CHAIN_CHECK_GSUM runs the reference's gsum invariant (pvac_hip_check_mul_gsum) on every pair
+ * of every step (needs pvac_hip_ctx_set_powg). A callback's nonzero return stops the chain with
+ * PVAC_EINVAL. */
+#define PVAC_CHAIN_CHECK_GSUM 0x100u
+#define PVAC_CHAIN_MAX_DEPTH 32
+typedef struct pvac_chain_opts {
+    uint32_t depth;        /* 1 .. PVAC_CHAIN_MAX_DEPTH */
+    uint32_t streams;      /* worker streams, 0 = 4 */
+    uint64_t chunk;        /* inputs per chunk, 0 = 1024 */
+    uint64_t nonce_seed;
+    uint32_t flags;        /* PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM */
+    uint32_t pad;
+    uint64_t digest_n;     /* leading inputs whose final digests / counts are written */
+    uint64_t* digest_out;  /* DEVICE [digest_n], nullable */
+    uint64_t* count_out;   /* DEVICE [digest_n], nullable */
+    int (*fill_nonces)(void* user, uint32_t step, uint64_t first_input, uint64_t n_words, uint64_t* dev_words,
+                       void* stream);
+    int (*on_chunk)(void* user, uint64_t first_input, const pvac_ct_batch* C, void* stream);
+    void* user;
+} pvac_chain_opts;
+typedef struct pvac_chain_stats {
+    uint64_t pair_steps;                        /* inputs x depth */
+    uint64_t edges[PVAC_CHAIN_MAX_DEPTH];       /* sum over inputs of |c_k.E|, step k = index + 1 */
+    uint64_t products[PVAC_CHAIN_MAX_DEPTH];    /* sum over inputs of |c_{k-1}.E| |x.E| */
+    uint64_t gsum_pairs;                        /* pair-steps checked (PVAC_CHAIN_CHECK_GSUM) */
+    uint64_t gsum_failed;                       /* pair-steps whose invariant failed */
+    uint64_t redo;                              /* pairs re-run on the general path (ct_mul_exec) */
+    uint64_t chunks;
+    double seconds;                             /* wall time of the call */
+} pvac_chain_stats;
+int pvac_hip_ct_mul_chain(pvac_hip_ctx* ctx, const pvac_ct_batch* X, const pvac_chain_opts* opts,
+                          pvac_chain_stats* stats);
+
 /* ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45; combine_ciphers ops/encrypt.hpp:260-279).
  * negate_b != 0 gives ct_sub (B's weights scaled by p-1). Dense CSR output: the plan writes
  * C->l_off/e_off as exclusive scans of |A.L|+|B.L| and |A.E|+|B.E|. Sigmas are carried when

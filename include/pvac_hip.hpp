@@ -334,21 +334,37 @@ public:
         vc.n = n;
         check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, nullptr, &vc, 0));
         if (with_sigma) {
-            // one salt per emitted edge, drawn after the weights are known (arithmetic.hpp:90-94);
-            // the second exec reproduces the same edges and consumes the salts in hash order
+            // one salt per emitted edge, drawn after the weights are known (arithmetic.hpp:90-94), in
+            // emit order. In the reference hash order (pair status 0) output position k of a pair IS
+            // its k-th emit, so sigma_from_H runs over the finished batch (pvac_hip_sigma_batch);
+            // a pair in the canonical order (guard_budget) takes its salts in hash order, which the
+            // second exec with PVAC_MUL_WITH_SIGMA maps (salt positions)
             std::vector<uint64_t> ecnt(n), eoff(n);
+            std::vector<uint32_t> status(n);
+            detail::dev_array<uint32_t> d_status(n);
+            check(pvac_hip_ct_mul_status(ctx_, d_status.p, n));
             c.d_e_cnt.download(ecnt.data(), n, stream_);
             c.d_e_off.download(eoff.data(), n, stream_);
+            d_status.download(status.data(), n, stream_);
             detail::hip_ok(hipStreamSynchronize(stream_), "sync");
             std::vector<uint64_t> salts(plan.total_edge_slots ? plan.total_edge_slots : 1, 0);
-            for (size_t i = 0; i < n; ++i)
+            bool hash_order = true;
+            for (size_t i = 0; i < n; ++i) {
+                hash_order &= status[i] != 1u;
                 for (uint64_t k = 0; k < ecnt[i]; ++k) salts[eoff[i] + k] = rnd();
+            }
             detail::dev_array<uint64_t> d_salts(salts.size());
             d_salts.upload(salts.data(), salts.size(), stream_);
-            check(pvac_hip_ct_mul_plan(ctx_, &va, &vb, &vc, &plan));
             vc = c.view(true);
             vc.n = n;
-            check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, d_salts.p, &vc, PVAC_MUL_WITH_SIGMA));
+            if (hash_order) {
+                check(pvac_hip_sigma_batch(ctx_, &vc, d_salts.p));
+            } else {
+                check(pvac_hip_ct_mul_plan(ctx_, &va, &vb, &vc, &plan));
+                vc = c.view(true);
+                vc.n = n;
+                check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, d_salts.p, &vc, PVAC_MUL_WITH_SIGMA));
+            }
             return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits,
                                                 true, stream_);
         }

@@ -26,6 +26,8 @@ LAYER_DT = np.dtype([("rule", "<u4"), ("pa", "<u4"), ("pb", "<u4"), ("pad", "<u4
 
 FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE, FP_INV = 0, 1, 2, 3, 4, 5
 MUL_WITH_SIGMA, MUL_ORDER_CANONICAL = 0x1, 0x2
+CHAIN_CHECK_GSUM = 0x100
+CHAIN_MAX_DEPTH = 32
 ENC_WITH_SIGMA = 0x1
 
 P = (1 << 127) - 1
@@ -74,6 +76,23 @@ class Plan(C.Structure):
                 ("kind", C.c_uint32), ("reserved", C.c_uint32 * 5)]
 
 
+FILL_NONCES_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p)
+ON_CHUNK_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.POINTER(CtBatch), C.c_void_p)
+
+
+class ChainOpts(C.Structure):
+    _fields_ = [("depth", C.c_uint32), ("streams", C.c_uint32), ("chunk", C.c_uint64), ("nonce_seed", C.c_uint64),
+                ("flags", C.c_uint32), ("pad", C.c_uint32), ("digest_n", C.c_uint64), ("digest_out", C.c_void_p),
+                ("count_out", C.c_void_p), ("fill_nonces", FILL_NONCES_CB), ("on_chunk", ON_CHUNK_CB),
+                ("user", C.c_void_p)]
+
+
+class ChainStats(C.Structure):
+    _fields_ = [("pair_steps", C.c_uint64), ("edges", C.c_uint64 * CHAIN_MAX_DEPTH),
+                ("products", C.c_uint64 * CHAIN_MAX_DEPTH), ("gsum_pairs", C.c_uint64), ("gsum_failed", C.c_uint64),
+                ("redo", C.c_uint64), ("chunks", C.c_uint64), ("seconds", C.c_double)]
+
+
 def load_library(path: str = _LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise PvacError(f"native engine not built: {path} missing (run __graft_entry__.build())")
@@ -99,6 +118,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
                                   C.POINTER(CtBatch), u32], i32),
         "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ct_mul_status": ([vp, vp, C.c_size_t], i32),
+        "pvac_hip_ct_mul_chain": ([vp, C.POINTER(CtBatch), C.POINTER(ChainOpts), C.POINTER(ChainStats)], i32),
         "pvac_hip_alu_ceiling": ([vp, i32, C.POINTER(C.c_double)], i32),
         "pvac_hip_check_mul_gsum": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
                                      C.POINTER(u64)], i32),
@@ -387,6 +407,33 @@ class Engine:
                                                   p(salts), C.byref(sc), flags))
         return C_
 
+    def ct_mul_chain(self, X: DeviceBatch, depth, nonce_seed=0x5EED0040, streams=4, chunk=1024, check_gsum=False,
+                     digest_n=0, canonical=False, fill_nonces=None, on_chunk=None):
+        """c_0 = x, c_k = ct_mul(c_{k-1}, x) to `depth` for every input x of X (tests/test_main.cpp:289-295)
+        on `streams` internal worker streams in chunks of `chunk` inputs (pvac_hip_ct_mul_chain).
+        Returns a dict of the call's statistics; with digest_n > 0 also the final digests / edge
+        counts of inputs [0, digest_n) (numpy u64). fill_nonces / on_chunk: optional ctypes callbacks
+        (FILL_NONCES_CB / ON_CHUNK_CB), called from the library's worker threads."""
+        torch = self.torch
+        dn = min(int(digest_n), X.n)
+        dig = torch.zeros(max(dn, 1), dtype=torch.int64, device=self.device)
+        cnt = torch.zeros(max(dn, 1), dtype=torch.int64, device=self.device)
+        o = ChainOpts(depth=depth, streams=streams, chunk=chunk, nonce_seed=nonce_seed,
+                      flags=(CHAIN_CHECK_GSUM if check_gsum else 0) | (MUL_ORDER_CANONICAL if canonical else 0),
+                      pad=0, digest_n=dn, digest_out=C.c_void_p(dig.data_ptr()) if dn else None,
+                      count_out=C.c_void_p(cnt.data_ptr()) if dn else None,
+                      fill_nonces=fill_nonces or FILL_NONCES_CB(), on_chunk=on_chunk or ON_CHUNK_CB(), user=None)
+        st = ChainStats()
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_ct_mul_chain(self.ctx, C.byref(sx), C.byref(o), C.byref(st)))
+        res = {"pair_steps": st.pair_steps, "edges": [st.edges[d] for d in range(depth)],
+               "products": [st.products[d] for d in range(depth)], "gsum_pairs": st.gsum_pairs,
+               "gsum_failed": st.gsum_failed, "redo": st.redo, "chunks": st.chunks, "seconds": st.seconds}
+        if dn:
+            res["digests"] = dig[:dn].cpu().numpy().view(np.uint64).copy()
+            res["counts"] = cnt[:dn].cpu().numpy().view(np.uint64).copy()
+        return res
+
     def ct_mul_redo_count(self):
         """Fresh-shape pairs re-run on the general path because a key sum was 0 mod p."""
         v = C.c_uint64(0)
@@ -513,4 +560,5 @@ class Engine:
 
 
 __all__ = ["Engine", "DeviceBatch", "HostCipher", "PvacError", "LAYER_DT", "load_library", "FP_ADD", "FP_SUB",
-           "FP_MUL", "FP_NEG", "FP_SCALE", "FP_INV", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL"]
+           "FP_MUL", "FP_NEG", "FP_SCALE", "FP_INV", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL", "CHAIN_CHECK_GSUM",
+           "ChainOpts", "ChainStats", "FILL_NONCES_CB", "ON_CHUNK_CB"]

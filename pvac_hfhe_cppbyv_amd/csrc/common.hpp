@@ -125,7 +125,6 @@ constexpr uint32_t kFreshKeysMax = 1536;    // |A.L||B.L|B key slots
 constexpr uint32_t kFreshProdMax = 4096;    // |A.E||B.E| products
 constexpr uint32_t kFreshEdgesMax = 256;    // |A.E|, |B.E|
 constexpr uint32_t kFreshLayersMax = 64;    // |C.L| before compaction
-constexpr uint32_t kFreshThreads = 512;     // workgroup of the fresh kernel (8 waves, two per CU)
 
 // One 64-byte header record per pair (written by k_mul_layers_fresh, read by k_ct_mul_fresh with
 // a single scalar load): every per-pair field the aggregation kernel needs, in one cache line.
@@ -254,6 +253,13 @@ struct large_desc {
     // (cnt[kCntIFail]) when a B layer is too big for the matrix-core mode or an A layer cannot be
     // staged as a dense table
     uint32_t iblk;
+    // 1: direct mode (an iblk pair whose scratch holds no per-key sums): k_large_count_la counts the
+    // emit positions from key PRESENCE before any multiply, k_large_scan_direct turns the counts into
+    // offsets, and k_large_products_la<DIRECT> writes C's edge records at their positions from the
+    // matrix-core epilogue. A pair that turns out to need more (shared buckets, the canonical order,
+    // a fallback, a key whose products cancel) is left to the host's redo on the full layout
+    uint32_t direct;
+    uint32_t pad_d;
     uint64_t nb_m;               // floor(2^32 / |B.E|): t / |B.E| by div_small (k_mul_large.hip)
     // static bucket groups (bucket_count >= 2 S): per-slot chain head / next of the slots sharing
     // a libstdc++ bucket, word offsets into mul_large_args::grp (kNoGrp: dynamic chains via link)
@@ -313,7 +319,12 @@ struct mul_large_args {
     uint32_t la_xcd;             // k_large_products_la: 1 = all workgroups of a pair on one XCD (grid y padded to 8)
     uint32_t any_dyn;            // some pair has dynamic bucket chains (k_large_link runs)
     uint32_t all_iblk;           // every pair is iblk (rank / order / write on reduced grids)
-    uint32_t pad2;
+    uint32_t any_direct;         // some pair is direct (large_desc::direct): the direct kernels run
+    uint32_t layers_direct;      // k_large_layers: 1 = the direct pairs' pass (before their products),
+                                 // 0 = every other pair (after the products)
+    uint32_t all_direct;         // every pair is direct: the per-key kernels are not launched
+    uint64_t* redo_ids;          // pairs the host re-runs on the full layout (shared with the fresh kernel)
+    unsigned int* redo_cnt;
     // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all
     // over all, max_la_wg = ceil(|A.L| / kLaPerWG) over the A-layer-major class)
     uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg, max_nA;
@@ -331,10 +342,15 @@ hipError_t launch_check_sizes(const pvac_ct_batch& A, const pvac_ct_batch& B, co
 hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C, const uint64_t* nonces,
                              const uint64_t* powg, uint32_t Bm, const unsigned int* mx_host, uint32_t* status,
                              unsigned long long* n_bad, int num_cus, hipStream_t st);
+// pvac_hip_ct_mul_chain statistics: out[0] += sum |C.E|, out[1] += sum |A.E| |X.E| (k_check.hip)
+hipError_t launch_chain_stats(const pvac_ct_batch& A, const pvac_ct_batch& X, const pvac_ct_batch& C,
+                              unsigned long long* out, hipStream_t st);
 constexpr uint64_t kNoGrp = ~0ull;
 constexpr uint32_t kCntWords = 16;    // large_desc::o_cnt words
 constexpr uint32_t kCntIFail = 8;     // cnt word: an iblk pair uses the block marks after all
 constexpr uint32_t kCntIShared = 9;   // cnt word: an iblk pair has keys sharing a bucket (order probes)
+constexpr uint32_t kCntDirect = 10;   // cnt word: a direct pair's positions are final (k_large_scan_direct)
+constexpr uint32_t kCntRedo = 11;     // cnt word: a direct pair was handed to the host's redo
 constexpr uint32_t kIblkMaxNB = 63;   // iblk: |B.E| <= 63 (a 64-bit mask per A edge, bit 63 a flag)
 // static bucket groups of key slots [0, S) for one bucket count: head[s] = 0 when s is alone in
 // its bucket, else the first slot + 1 of the bucket's chain; next[s] = the following slot + 1

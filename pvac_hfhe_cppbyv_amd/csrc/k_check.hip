@@ -17,6 +17,8 @@
 // reference's fp_add / fp_sub chains, which compute exact residues for canonical terms.
 // Status per pair: 0 holds, 1 violated, 2 an edge idx >= B (the reference reads past powg_B),
 // 3 too many edges (> 2^21 in one cipher: the limb sums could overflow; not checked).
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace pvhip {
@@ -215,6 +217,41 @@ hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, con
     uint64_t blocks = (uint64_t)num_cus * 8;
     if (blocks > A.n) blocks = A.n;
     hipLaunchKernelGGL(k_check_gsum, dim3((unsigned)blocks), dim3(kCB), L.total, st, g, L);
+    return hipGetLastError();
+}
+
+// Chain statistics (pvac_hip_ct_mul_chain): out[0] += sum of |C.E|, out[1] += sum of |A.E| |X.E| over the
+// pairs of one step (the products the step multiplied). One block-reduced atomic per block.
+namespace {
+__global__ __launch_bounds__(256) void k_chain_stats(const uint64_t* a_cnt, const uint64_t* x_cnt, const uint64_t* c_cnt,
+                                                     uint64_t n, unsigned long long* out) {
+    __shared__ unsigned long long part[2][4];
+    unsigned long long e = 0, p = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        e += c_cnt[i];
+        p += a_cnt[i] * x_cnt[i];
+    }
+    for (int o = 32; o; o >>= 1) {
+        e += __shfl_xor(e, o);
+        p += __shfl_xor(p, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = e;
+        part[1][threadIdx.x >> 6] = p;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(out, part[0][0] + part[0][1] + part[0][2] + part[0][3]);
+        atomicAdd(out + 1, part[1][0] + part[1][1] + part[1][2] + part[1][3]);
+    }
+}
+}  // namespace
+
+hipError_t launch_chain_stats(const pvac_ct_batch& A, const pvac_ct_batch& X, const pvac_ct_batch& C,
+                              unsigned long long* out, hipStream_t st) {
+    if (!A.n) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((A.n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_chain_stats, dim3(blocks), dim3(256), 0, st, A.e_cnt, X.e_cnt, C.e_cnt, A.n, out);
     return hipGetLastError();
 }
 

@@ -375,7 +375,7 @@ __device__ __forceinline__ void mx_stage_sparse(uint4* prec, uint4* pinf, uint32
     const uint32_t nks = (Sd.n + 1u) >> 1;
     if (k >= 2u * nks) return;
     uint4 mid = make_uint4(0, 0, 0, 0);
-    uint4 inf = make_uint4(Bm, Bm, kInf, 0);   // padding edge: zero digits, time never smaller
+    uint4 inf = make_uint4(Bm, Bm, kInf, 0);   // padding edge: zero digits, time never smaller, w = 0
     if (k < Sd.n) {
         const edge_rec x = load_edge(Sd, k);
         uint64_t dl, dh;
@@ -384,7 +384,7 @@ __device__ __forceinline__ void mx_stage_sparse(uint4* prec, uint4* pinf, uint32
         mid = make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
         const uint32_t sidx = meta_idx(x.meta), sch = meta_ch(x.meta);
         // dense slot of output row r: P (dense channel == sparse channel), M (the other)
-        inf = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, x.e * smul, 0);
+        inf = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, x.e * smul, 1);
     }
     prec[3u * k] = make_uint4(0, 0, 0, 0);
     prec[3u * k + 1u] = mid;
@@ -405,6 +405,16 @@ struct task_out {
     const uint32_t* bjt = nullptr;      // B edge j: idx | ch << 16
     uint32_t nB = 0;
     uint64_t nb_m = 0;
+    // direct mode (large_desc::direct): C's edge records at their emit positions
+    const uint32_t* off = nullptr;      // per A edge i: exclusive suffix offset of its key range
+    const ulonglong2* imask = nullptr;  // per A edge i: keys (bit j) with a P / an M edge
+    uint64_t* c_meta = nullptr;
+    uint64_t* c_lo = nullptr;
+    uint64_t* c_hi = nullptr;
+    uint32_t* salt_pos = nullptr;       // nullable: hash-order index of each output edge
+    uint64_t ceo = 0;                   // the pair's first output edge slot
+    uint32_t lid = 0;                   // the product layer's id after compact_layers
+    uint32_t* redo = nullptr;           // cnt[kCntRedo] of the pair: a key's sum was 0
 };
 constexpr uint32_t kRecKey = 1u << 21, kRecShared = 1u << 20;
 
@@ -414,7 +424,7 @@ constexpr uint32_t kRecKey = 1u << 21, kRecShared = 1u << 20;
 // NKS = k-steps of two sparse edges, a compile-time count: the k-step loop is straight-line code,
 // so every k-step's LDS reads can be issued ahead of the MFMAs (a runtime guard per k-step made
 // each one a basic block of its own: two dependent LDS round trips per k-step)
-template <int BS, int NKS>
+template <int BS, int NKS, bool DIRECT>
 __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* pinf, uint32_t Bm, uint64_t slot0,
                             const task_out& o) {
     const uint4* dig = (const uint4*)lds;
@@ -444,6 +454,7 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
         const uint32_t rr = live ? r : 0u;
         mx_v16 aP{}, aM{};
         uint32_t tmin = kInf;
+        uint32_t presP = 0, presM = 0;   // DIRECT: this half's sparse edges reach the row's P / M cell
         for (int rep_ = 0; rep_ < PVAC_EXP_MXREP; ++rep_) {   // experiment builds repeat the loop
             uint32_t rq = rr;
             asm volatile("" : "+v"(rq));
@@ -463,6 +474,10 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
                 aP = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dp.x, (int)dp.y, (int)dp.z, (int)dp.w}, aP, 0, 0, 0);
                 aM = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dm.x, (int)dm.y, (int)dm.z, (int)dm.w}, aM, 0, 0, 0);
                 tmin = min(tmin, min(__builtin_elementwise_add_sat(tp, in.z), __builtin_elementwise_add_sat(tm, in.z)));
+                if (DIRECT) {
+                    presP |= tp != kInf ? in.w : 0u;   // in.w = 1 for a real sparse edge, 0 for padding
+                    presM |= tm != kInf ? in.w : 0u;
+                }
             }
         }
         MXMARK(3);
@@ -478,6 +493,31 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
         const uint32_t nzo = (uint32_t)__shfl_xor((int)nz, 32);
         const uint32_t eb = h ? (nzo | nz << 1) : (nz | nzo << 1);
         tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, 32));
+        if (DIRECT) {
+            // the key's edges were counted from presence (k_large_count_la): P / M cells with a
+            // product emit. Position = its A edge range's offset + the edges of the range's keys
+            // with a larger B edge j (j DESC, P before M), as k_large_write_ranges orders them
+            presP |= (uint32_t)__shfl_xor((int)presP, 32);
+            presM |= (uint32_t)__shfl_xor((int)presM, 32);
+            const uint32_t mine = h ? presM : presP;
+            if (live && tmin != kInf) {
+                if (mine != nz) *o.redo = 1u;   // a present cell whose products cancel: redo the pair
+                if (mine) {
+                    uint32_t j;
+                    const uint32_t i = div_small(tmin, o.nB, o.nb_m, j);
+                    const ulonglong2 mk = o.imask[i];
+                    const unsigned long long above = (~0ull << (j + 1u)) & ~(1ull << 63);
+                    const uint32_t pos = o.off[i] + (uint32_t)__popcll(mk.x & above) + (uint32_t)__popcll(mk.y & above) +
+                                         (h ? presP : 0u);
+                    const uint64_t q = o.ceo + pos;
+                    o.c_meta[q] = make_meta(o.lid, r, h);
+                    o.c_lo[q] = v.lo;
+                    o.c_hi[q] = v.hi;
+                    if (o.salt_pos) o.salt_pos[q] = pos;
+                }
+            }
+            continue;
+        }
         if (live) {
             const uint64_t s = slot0 + r;
             if (h == 0) o.tkey[s] = tmin;
@@ -507,22 +547,22 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
     return any;
 }
 
-template <int BS>
+template <int BS, bool DIRECT = false>
 __device__ bool mx_blocks(const uint8_t* lds, const uint4* prec, const uint4* pinf, uint32_t ns, uint32_t Bm, uint64_t slot0,
                           const task_out& o) {
     static_assert(kMxKS == 10, "one instantiation per k-step count");
     switch ((ns + 1u) >> 1) {   // workgroup-uniform
     case 0: return false;       // no products: the slots keep their initial time
-    case 1: return mx_blocks_n<BS, 1>(lds, prec, pinf, Bm, slot0, o);
-    case 2: return mx_blocks_n<BS, 2>(lds, prec, pinf, Bm, slot0, o);
-    case 3: return mx_blocks_n<BS, 3>(lds, prec, pinf, Bm, slot0, o);
-    case 4: return mx_blocks_n<BS, 4>(lds, prec, pinf, Bm, slot0, o);
-    case 5: return mx_blocks_n<BS, 5>(lds, prec, pinf, Bm, slot0, o);
-    case 6: return mx_blocks_n<BS, 6>(lds, prec, pinf, Bm, slot0, o);
-    case 7: return mx_blocks_n<BS, 7>(lds, prec, pinf, Bm, slot0, o);
-    case 8: return mx_blocks_n<BS, 8>(lds, prec, pinf, Bm, slot0, o);
-    case 9: return mx_blocks_n<BS, 9>(lds, prec, pinf, Bm, slot0, o);
-    default: return mx_blocks_n<BS, 10>(lds, prec, pinf, Bm, slot0, o);
+    case 1: return mx_blocks_n<BS, 1, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 2: return mx_blocks_n<BS, 2, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 3: return mx_blocks_n<BS, 3, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 4: return mx_blocks_n<BS, 4, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 5: return mx_blocks_n<BS, 5, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 6: return mx_blocks_n<BS, 6, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 7: return mx_blocks_n<BS, 7, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 8: return mx_blocks_n<BS, 8, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 9: return mx_blocks_n<BS, 9, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    default: return mx_blocks_n<BS, 10, DIRECT>(lds, prec, pinf, Bm, slot0, o);
     }
 }
 
@@ -798,6 +838,225 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
     __syncthreads();   // the next A layer's staging overwrites M1 / M2, tt and recs
 }
 
+// ---- direct mode (large_desc::direct) ------------------------------------------------------
+// Which keys emit, and in which order, follows from key PRESENCE alone when no key's products cancel:
+// a P (M) cell emits iff some product lands in it (arithmetic.hpp:96-101 with sums assumed != 0).
+// So the per-A-edge counts and masks of iblk_layer can be built before any multiply, the counts
+// scanned into offsets, and the products kernel can write C's edge records at their positions from
+// its epilogue: no per-key sums, first-insert times or key records go through HBM, and the range
+// writer that gathered them is not needed. A key whose sum turns out to be 0 sends the pair to the
+// host's redo (exact path), as the fresh kernel does.
+
+// the dense side's first-insert shares only (no digits): tt[2][2B] at lds + 64 B as mx_stage_dense
+// lays them out (iblk_layer reads them there); false when the layer has duplicate (idx, ch) edges
+template <int BS>
+__device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t tmul) {
+    uint32_t* tt = (uint32_t*)(lds + 64u * Bm);
+    uint32_t* dup = (uint32_t*)(lds + 80u * Bm);
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < 4 * Bm; k += BS) tt[k] = kInf;
+    if (tid == 0) *dup = 0;
+    __syncthreads();
+    for (uint32_t k0 = tid; k0 < D.n; k0 += 4u * BS) {   // four edges per round, loads first
+        uint64_t m[4];
+        uint32_t e[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint32_t k = k0 + (uint32_t)v * BS;
+            e[v] = D.ids[k < D.n ? k : 0u];
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) m[v] = D.X->meta[D.eo + e[v]];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            if (k0 + (uint32_t)v * BS >= D.n) break;
+            const uint32_t sl = meta_ch(m[v]) * 2u * Bm + meta_idx(m[v]);
+            const uint32_t te = e[v] * tmul;
+            if (atomicCAS(&tt[sl], kInf, te) != kInf) *dup = 1;
+            else tt[sl + Bm] = te;
+        }
+    }
+    __syncthreads();
+    return *dup == 0;
+}
+
+// Pass 1 of a direct pair, one workgroup per (pair, la_per_wg A layers) like k_large_products_la:
+// per A layer, every key (r, B layer) gets its first-insert time and its P / M presence from the
+// dense shares and the B layers' edges, one record per key (the products kernel's iblk record),
+// then iblk_layer's counts and masks; product-layer used flags for compact_layers. A layer the
+// matrix-core mode cannot take (duplicate edges, fewer than kLargeDenseMin edges) fails the pair
+// (cnt[kCntIFail]): k_large_scan_direct sends it to the host's redo.
+template <int BS>
+__global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
+    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    if (!d.direct) return;
+    uint32_t* S = g.scratch;
+    uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2] || cnt[kCntIFail]) return;
+    const uint32_t neA = cnt[0], neB = min(cnt[1], kLaMaxLB);
+    const uint32_t i0 = blockIdx.x * g.la_per_wg;
+    if (i0 >= neA) return;
+    const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
+    const uint32_t tid = threadIdx.x;
+    // B layers: per edge (P slot offset, M slot offset, j) as mx_stage_sparse computes them
+    uint4* sp = (uint4*)(plds + g.lds_task);                          // [kLaMaxLB][kMxMaxSparse]
+    uint32_t* bjt = (uint32_t*)(sp + kLaMaxLB * kMxMaxSparse);        // [64] B edge j: idx | ch << 16
+    uint32_t* recs = bjt + 64;                                        // [kLaMaxLB][B]
+    uint32_t nbv[kLaMaxLB], lbv[kLaMaxLB];
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) {
+        nbv[k] = 0;
+        lbv[k] = 0;
+        if (k < neB) {
+            const uint32_t lb = S[d.o_neB + k];
+            const layer_src srcB = side_layer(&g.B, g.B.e_off[d.pair], S, d.o_lstB, LB, lb);
+            lbv[k] = lb;
+            nbv[k] = srcB.n;   // <= kIblkMaxSparse (k_large_lists failed the pair otherwise)
+            if (tid < srcB.n && srcB.n <= kMxMaxSparse) {
+                const uint32_t e = srcB.ids[tid];
+                const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + e];
+                const uint32_t sidx = meta_idx(mb), sch = meta_ch(mb);
+                sp[k * kMxMaxSparse + tid] = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, e, 0);
+            }
+        }
+    }
+    if (tid < nB) {   // published by stage_tt's barriers
+        const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + tid];
+        bjt[tid] = meta_idx(mb) | meta_ch(mb) << 16;
+    }
+    const uint32_t* ghead = group_heads(g, d);
+    const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
+    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t la = S[d.o_neA + i];
+        const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
+        bool ok = srcA.n >= kLargeDenseMin;
+#pragma unroll
+        for (uint32_t k = 0; k < kLaMaxLB; ++k) ok &= k >= neB || (nbv[k] <= kMxMaxSparse && nbv[k] <= srcA.n);
+        if (!ok) {   // workgroup-uniform: this A layer's tasks would not all run on the matrix cores
+            if (tid == 0) atomicExch(&cnt[kCntIFail], 1u);
+            return;
+        }
+        if (!stage_tt<BS>(plds, Bm, srcA, nB)) {
+            if (tid == 0) atomicExch(&cnt[kCntIFail], 1u);
+            return;
+        }
+        uint32_t usedm = 0;
+        for (uint32_t q = tid; q < neB * Bm; q += BS) {
+            const uint32_t k = q / Bm, r = q - k * Bm;
+            const uint4* e = sp + k * kMxMaxSparse;
+            uint32_t tmin = kInf, pp = 0, pm = 0;
+            for (uint32_t x = 0; x < nbv[k]; ++x) {
+                const uint4 in = e[x];
+                const uint32_t tp = tt[in.x + r], tm = tt[in.y + r];
+                pp |= tp != kInf ? 1u : 0u;
+                pm |= tm != kInf ? 1u : 0u;
+                tmin = min(tmin, min(__builtin_elementwise_add_sat(tp, in.z), __builtin_elementwise_add_sat(tm, in.z)));
+            }
+            uint32_t rv = 0;
+            if (tmin != kInf) {
+                const uint32_t eb = pp | pm << 1;
+                const uint64_t s = (uint64_t)(la * LB + lbv[k]) * Bm + r;
+                const bool shared = ghead && ghead[s] != 0u;
+                uint32_t j;
+                const uint32_t ia = div_small(tmin, nB, d.nb_m, j);
+                const uint32_t ij = bjt[j] & 0xFFFFu;
+                const uint32_t xx = r >= ij ? r - ij : r + Bm - ij;
+                const uint32_t dd = tt[xx] == ia * nB ? xx : Bm + xx;
+                rv = dd | j << 12 | eb << 18 | (shared ? kRecShared : 0u) | kRecKey;
+                usedm |= 1u << k;
+            }
+            recs[k * Bm + r] = rv;
+        }
+        // product layers with a key: compact_layers keeps them (benign race: every writer stores 1)
+#pragma unroll
+        for (uint32_t k = 0; k < kLaMaxLB; ++k)
+            if ((usedm >> k) & 1u) S[d.o_used + (LA + LB) + la * LB + lbv[k]] = 1;
+        __syncthreads();
+        iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, recs, S + d.o_icnt,
+                       (ulonglong2*)(S + d.o_imask));
+    }
+}
+
+// Pass 2 of a direct pair, one workgroup per pair: the total, the guard_budget decision, and the
+// per-A-edge counts turned into exclusive suffix offsets (as k_large_scan). A pair with shared
+// buckets, a fallback or the canonical order is not direct after all: it goes to the host's redo.
+__global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
+    __shared__ uint32_t part[kLBig / 64];
+    const large_desc& d = g.desc[blockIdx.x];
+    if (!d.direct) return;
+    uint32_t* S = g.scratch;
+    uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2]) return;
+    const int tid = threadIdx.x;
+    uint32_t* icnt = S + d.o_icnt;
+    const uint32_t nA = d.nA;
+    bool direct = !cnt[kCntIFail] && !cnt[kCntIShared];
+    uint32_t total = 0;
+    if (direct) {
+        for (uint32_t base = 0; base < nA; base += 4u * kLBig) {
+            uint32_t local = 0;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t r = base + 4u * (uint32_t)tid + (uint32_t)k;
+                local += r < nA ? icnt[r] : 0u;
+            }
+            uint32_t tot;
+            wg_exclusive_scan<kLBig>(local, part, tot);
+            total += tot;
+        }
+        direct = !((g.flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > g.edge_budget);
+    }
+    if (!direct) {
+        if (tid == 0) {
+            cnt[kCntRedo] = 1;
+            g.pair_status[d.pair] = kPairRedo;
+        }
+        return;
+    }
+    uint32_t run0 = 0;
+    for (uint32_t base = 0; base < nA; base += 4u * kLBig) {
+        const uint32_t r0 = base + 4u * (uint32_t)tid;
+        uint32_t v[4];
+        uint32_t local = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = r0 + (uint32_t)k;
+            v[k] = r < nA ? icnt[nA - 1 - r] : 0u;
+            local += v[k];
+        }
+        uint32_t tot;
+        uint32_t run = run0 + wg_exclusive_scan<kLBig>(local, part, tot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = r0 + (uint32_t)k;
+            if (r < nA) icnt[nA - 1 - r] = run;
+            run += v[k];
+        }
+        run0 += tot;
+    }
+    if (tid == 0) {
+        cnt[3] = total;
+        cnt[4] = 0;
+        cnt[kCntDirect] = 1;
+        g.C.e_cnt[d.pair] = total;
+        g.pair_status[d.pair] = 0;
+    }
+}
+
+// direct pairs handed to the redo (not direct after all, or a key whose products cancel): onto the
+// redo list the host re-runs on the full layout (ct_mul_exec's redo step)
+__global__ __launch_bounds__(64) void k_large_direct_redo(mul_large_args g) {
+    const uint32_t q = blockIdx.x * 64u + threadIdx.x;
+    if (q >= g.nl) return;
+    const large_desc& d = g.desc[q];
+    if (!d.direct) return;
+    const uint32_t* cnt = g.scratch + d.o_cnt;
+    if (cnt[2] || !cnt[kCntRedo]) return;
+    g.pair_status[d.pair] = kPairRedo;
+    g.redo_ids[atomicAdd(g.redo_cnt, 1u)] = d.pair;
+}
+
 // One workgroup per (pair, kLaPerWG A layers) for pairs with at most kLaMaxLB B layers (chain
 // steps): the B layers' sparse sides are staged once per workgroup and each A layer's dense table
 // once for all B layers, so a chain step reads every A edge once (a task per workgroup read it
@@ -821,6 +1080,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
         if (py >= g.n_la) return;
     }
     const large_desc& d = g.desc[g.sel[py]];
+    if (d.direct) return;   // k_large_products_direct
     uint32_t* S = g.scratch;
     const uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
@@ -919,12 +1179,76 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
     }
 }
 
+// Pass 3 of a direct pair (after k_large_scan_direct and the layers pass): k_large_products_la's
+// matrix-core products without any per-key scratch. Each row's folded P / M sums go straight to C's
+// edge records at their emit positions (mx_blocks_n<DIRECT>); a present cell whose sum is 0 flags
+// the pair for the host's redo.
+template <int BS>
+__global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_large_args g) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
+    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    if (!d.direct) return;
+    uint32_t* S = g.scratch;
+    uint32_t* cnt = S + d.o_cnt;
+    if (cnt[2] || !cnt[kCntDirect]) return;
+    const uint32_t neA = cnt[0], neB = min(cnt[1], kLaMaxLB);
+    const uint32_t i0 = blockIdx.x * g.la_per_wg;
+    if (i0 >= neA) return;
+    const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
+    uint8_t* sreg = plds + g.lds_task;   // per B layer: prec | pinf
+    uint32_t lbv[kLaMaxLB], nbv[kLaMaxLB];
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) {
+        lbv[k] = 0;
+        nbv[k] = 0;
+        if (k < neB) {
+            const uint32_t lb = S[d.o_neB + k];
+            const layer_src srcB = side_layer(&g.B, g.B.e_off[d.pair], S, d.o_lstB, LB, lb);
+            lbv[k] = lb;
+            nbv[k] = srcB.n;   // <= kMxMaxSparse: k_large_count_la checked
+            uint4* prec = (uint4*)(sreg + k * kMxSparseBytes);
+            mx_stage_sparse(prec, prec + 3u * kMxMaxSparse, Bm, srcB, 1u, threadIdx.x);
+        }
+    }
+    task_out o{};
+    o.nB = nB;
+    o.nb_m = d.nb_m;
+    o.off = S + d.o_icnt;
+    o.imask = (const ulonglong2*)(S + d.o_imask);
+    o.c_meta = g.C.meta;
+    o.c_lo = g.C.w_lo;
+    o.c_hi = g.C.w_hi;
+    o.salt_pos = g.salt_pos;
+    o.ceo = g.C.e_off[d.pair];
+    o.redo = &cnt[kCntRedo];
+    const uint32_t* remap = S + d.o_used;   // k_large_layers left the remap here
+    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t la = S[d.o_neA + i];
+        const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
+        if (!mx_stage_dense<BS>(plds, Bm, srcA, nB)) {   // cannot happen: k_large_count_la staged it
+            if (threadIdx.x == 0) cnt[kCntRedo] = 1;
+            return;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kLaMaxLB; ++k) {
+            if (k >= neB) continue;
+            const uint4* prec = (const uint4*)(sreg + k * kMxSparseBytes);
+            const uint32_t lp = la * LB + lbv[k];
+            o.lid = remap[LA + LB + lp];
+            mx_blocks<BS, true>(plds, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, (uint64_t)lp * Bm, o);
+        }
+        __syncthreads();   // the next A layer's staging overwrites the dense tables
+    }
+}
+
 // the column-mode tasks k_large_products_la deferred: kDeferWG workgroups per pair walk its list
 constexpr uint32_t kDeferWG = 4;
 template <int BS>
 __global__ __launch_bounds__(BS) void k_large_products_defer(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
     const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    if (d.direct) return;
     uint32_t* S = g.scratch;
     const uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
@@ -960,6 +1284,8 @@ __global__ __launch_bounds__(kLBig) void k_large_layers(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.x];
     uint32_t* S = g.scratch;
     if (S[d.o_cnt + 2]) return;
+    // direct pairs: their own pass before their products (redone pairs: none); the others after
+    if (g.layers_direct ? !(d.direct && S[d.o_cnt + kCntDirect]) : d.direct != 0) return;
     const uint64_t pr = d.pair;
     const uint32_t LA = d.LA, LB = d.LB, Lc = (uint32_t)d.Lc, base = LA + LB;
     const uint64_t alo = g.A.l_off[pr], blo = g.B.l_off[pr], clo = g.C.l_off[pr];
@@ -1027,6 +1353,7 @@ __global__ __launch_bounds__(kLBig) void k_large_layers(mul_large_args g) {
 // ---------------------------------------------------------------- bucket chains
 __global__ __launch_bounds__(kLB) void k_large_link(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.y];
+    if (d.direct) return;
     uint32_t* S = g.scratch;
     if (S[d.o_cnt + 2]) return;
     const uint32_t Bm = g.Bm;
@@ -1055,6 +1382,7 @@ __global__ __launch_bounds__(kLB) void k_large_link(mul_large_args g) {
 
 __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.y];
+    if (d.direct) return;
     uint32_t* S = g.scratch;
     if (S[d.o_cnt + 2]) return;
     const uint32_t* tkey = S + d.o_tkey;
@@ -1140,6 +1468,7 @@ __global__ __launch_bounds__(kLB) void k_large_rank(mul_large_args g) {
 __global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
     __shared__ uint32_t part[kLBig / 64];
     const large_desc& d = g.desc[blockIdx.x];
+    if (d.direct) return;   // k_large_scan_direct
     uint32_t* S = g.scratch;
     uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
@@ -1218,6 +1547,7 @@ __global__ __launch_bounds__(kLBig) void k_large_scan(mul_large_args g) {
 
 __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.y];
+    if (d.direct) return;
     uint32_t* S = g.scratch;
     const uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
@@ -1327,6 +1657,7 @@ __global__ __launch_bounds__(kLB) void k_large_order(mul_large_args g) {
 
 __global__ __launch_bounds__(kLB) void k_large_write(mul_large_args g) {
     const large_desc& d = g.desc[blockIdx.y];
+    if (d.direct) return;
     uint32_t* S = g.scratch;
     const uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
@@ -1361,6 +1692,7 @@ __global__ __launch_bounds__(kLB) void k_large_write(mul_large_args g) {
 __global__ __launch_bounds__(kLB) void k_large_write_ranges(mul_large_args g) {
     __shared__ uint32_t bjt[64];   // B edge j: idx | layer << 16
     const large_desc& d = g.desc[blockIdx.y];
+    if (d.direct) return;
     uint32_t* S = g.scratch;
     const uint32_t* cnt = S + d.o_cnt;
     if (cnt[2] || !d.iblk || cnt[kCntIFail] || cnt[4] || cnt[kCntIShared]) return;
@@ -1507,18 +1839,34 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     hipLaunchKernelGGL(k_large_init, dim3(grid_x(a.max_zero > a.max_S ? a.max_zero : a.max_S, kLB * 4, 4096), nl),
                        dim3(kLB), 0, st, a);
     hipLaunchKernelGGL(k_large_lists, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
+#ifndef PVAC_LARGE_PRODUCTS_COL26
+    if (a.any_direct && a.n_la && a.max_la_wg) {
+        // direct pairs: presence counts, offsets, compact_layers, then products straight to C
+        mul_large_args b = a;
+        b.lds_task = mx_lds_bytes(a.Bm);
+        const dim3 grid((unsigned)a.max_la_wg, a.n_la);
+        hipLaunchKernelGGL((k_large_count_la<kLPX>), grid, dim3(kLPX),
+                           (size_t)b.lds_task + kLaMaxLB * kMxMaxSparse * 16u + kIblkBjtBytes + kLaMaxLB * 4u * a.Bm, st, b);
+        hipLaunchKernelGGL(k_large_scan_direct, dim3(nl), dim3(kLBig), 0, st, b);
+        b.layers_direct = 1;
+        hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, b);
+        hipLaunchKernelGGL((k_large_products_direct<kLPX>), grid, dim3(kLPX), (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes,
+                           st, b);
+        hipLaunchKernelGGL(k_large_direct_redo, dim3((nl + 63) / 64), dim3(64), 0, st, b);
+        if (a.all_direct) return hipGetLastError();
+    }
+#endif
     // products: the matrix-core dense mode in 4-wave workgroups (A-layer-major for pairs with few B
-    // layers, one task per workgroup for the rest) unless PVAC_LARGE_PRODUCTS=col26 selects the
-    // column-accumulator kernel of round 2 for every pair (A/B runs)
-    static const bool col26_only = [] {
-        const char* e = std::getenv("PVAC_LARGE_PRODUCTS");
-        return e && std::strcmp(e, "col26") == 0;
-    }();
-    if (col26_only) {
+    // layers, one task per workgroup for the rest). A/B builds with -DPVAC_LARGE_PRODUCTS_COL26 run
+    // the column-accumulator kernel of round 2 for every pair instead (never the shipped library).
+#ifdef PVAC_LARGE_PRODUCTS_COL26
+    {
         mul_large_args b = a;
         b.n_la = 0;
         hipLaunchKernelGGL((k_large_products<kLP, false>), dim3((unsigned)a.max_tasks_all, nl), dim3(kLP), plds, st, b);
-    } else {
+    }
+#else
+    {
         const size_t lx = std::max<size_t>(plds, mx_lds_bytes(a.Bm) + kMxSparseBytes);
         if (nl > a.n_la && a.max_tasks)
             hipLaunchKernelGGL((k_large_products<kLPX, true>), dim3((unsigned)a.max_tasks, nl - a.n_la), dim3(kLPX), lx, st, a);
@@ -1531,6 +1879,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
             hipLaunchKernelGGL((k_large_products_defer<kLPX>), dim3(kDeferWG, a.n_la), dim3(kLPX), plds, st, a);
         }
     }
+#endif
     hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, a);
     const unsigned gs = grid_x(a.max_S, kLB * 2, 4096);
     // a batch of iblk pairs runs rank / order / write only for the few that share buckets, need the

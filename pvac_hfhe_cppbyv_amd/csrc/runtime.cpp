@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cmath>
@@ -12,7 +13,9 @@
 #include <cstring>
 #include <map>
 #include <new>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -30,6 +33,21 @@ struct timer_rec {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     double ms = 0;
     uint64_t launches = 0;
+};
+
+// one output batch of a chain worker (pvac_hip_ct_mul_chain): stream-ordered allocations that grow
+struct chain_set {
+    uint64_t* l_off = nullptr;
+    uint64_t* l_cnt = nullptr;
+    uint64_t* e_off = nullptr;
+    uint64_t* e_cnt = nullptr;
+    size_t n_cap = 0;
+    pvac_layer* layers = nullptr;
+    size_t l_cap = 0;
+    uint64_t* meta = nullptr;
+    uint64_t* w_lo = nullptr;
+    uint64_t* w_hi = nullptr;
+    size_t e_cap = 0;
 };
 
 }  // namespace
@@ -107,6 +125,15 @@ struct pvac_hip_ctx {
     // timing
     bool timing = false;
     std::map<std::string, timer_rec> timers;
+    // general-path scratch cap in words (0 = half the free HBM): chain workers share the device
+    uint64_t arena_cap_words = 0;
+    bool large_no_direct = false;   // the redo run: every pair on the full (per-key sums) layout
+    // pvac_hip_ct_mul_chain: worker contexts (own stream / arena), and a worker's own buffers
+    std::vector<pvac_hip_ctx*> chain_kids;
+    chain_set chain_bufs[2];
+    uint64_t* chain_nonces = nullptr;
+    size_t chain_nonce_cap = 0;
+    unsigned long long* chain_stats = nullptr;   // [2 * PVAC_CHAIN_MAX_DEPTH]
 };
 
 namespace {
@@ -223,23 +250,31 @@ uint32_t ceil_log2(uint64_t x) {
     return b;
 }
 
-// Per-A-edge emit order for eligible pairs (large_desc::iblk). PVAC_LARGE_IBLK=0 keeps the n/16
-// block marks for every pair (A/B runs); so does PVAC_LARGE_PRODUCTS=col26, whose per-task products
-// kernel does not see an A layer's keys in one workgroup.
-bool large_iblk_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("PVAC_LARGE_IBLK");
-        const char* p = std::getenv("PVAC_LARGE_PRODUCTS");
-        return !(e && e[0] == '0') && !(p && std::strcmp(p, "col26") == 0);
-    }();
-    return on;
+// Per-A-edge emit order for eligible pairs (large_desc::iblk). A/B builds only (make variant-f, never
+// the shipped library): -DPVAC_LARGE_IBLK=0 keeps the n/16 block marks for every pair, and so does
+// -DPVAC_LARGE_PRODUCTS_COL26, whose per-task products kernel does not see an A layer's keys in one
+// workgroup.
+#ifndef PVAC_LARGE_IBLK
+#define PVAC_LARGE_IBLK 1
+#endif
+constexpr bool large_iblk_enabled() {
+#ifdef PVAC_LARGE_PRODUCTS_COL26
+    return false;
+#else
+    return PVAC_LARGE_IBLK != 0;
+#endif
 }
+// Direct mode for iblk pairs (large_desc::direct): A/B builds with -DPVAC_LARGE_DIRECT=0 keep every
+// iblk pair on the per-key-sums layout
+#ifndef PVAC_LARGE_DIRECT
+#define PVAC_LARGE_DIRECT 1
+#endif
 
 // Scratch layout of one general-path pair (k_mul_large.hip), offsets relative to 0; the
 // executor rebases them into the arena. 64-bit arrays on even words, 16-byte arrays on
 // multiples of four.
 int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uint64_t nA, uint64_t nB, uint32_t Bm,
-                     std::string& why, bool static_grp = false) {
+                     std::string& why, bool static_grp = false, bool allow_direct = false) {
     d = large_desc{};
     d.pair = pair;
     d.n = nA * nB;
@@ -265,10 +300,36 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.nbm = make_fastmod64(bucket_count_after_reserve(d.n));
     d.hbits = std::max<uint32_t>(1, ceil_log2(2 * std::max<uint64_t>(keys, 1)));
     d.g_head = d.g_next = kNoGrp;
-    const uint64_t hcap = static_grp ? 0 : 1ull << d.hbits;   // static groups: no bucket table / chains
+    // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
+    d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
+    d.direct = d.iblk && allow_direct && PVAC_LARGE_DIRECT ? 1u : 0u;
+    d.nb_m = nB ? (1ull << 32) / nB : 0;
     uint64_t o = 0;
     auto even = [&]() { o = (o + 1) & ~1ull; };
     auto quad = [&]() { o = (o + 3) & ~3ull; };
+    if (d.direct) {
+        // no per-key scratch: cnt | used, the edge lists, per-A-edge counts and masks
+        quad();
+        d.o_zero = d.o_cnt = o;
+        o += kCntWords;
+        d.o_hkey = d.o_hhead = d.o_bmask = o;
+        d.o_bcnt = d.o_used = o;
+        o += d.Lc;
+        d.zero_words = o - d.o_zero;
+        d.o_tkey = o;
+        d.o_lstA = o; o += 2 * LA + nA;
+        d.o_lstB = o; o += 2 * LB + nB;
+        d.o_neA = o; o += LA;
+        d.o_neB = o; o += LB;
+        d.o_defer = d.o_info = d.o_sums = d.o_nxt = d.o_tb = d.o_within = d.o_etot = d.o_cpos = d.o_order = d.o_hpos = o;
+        d.o_icnt = o; o += nA;
+        quad();
+        d.o_imask = o; o += 4 * nA;
+        quad();
+        d.words = o;
+        return PVAC_OK;
+    }
+    const uint64_t hcap = static_grp ? 0 : 1ull << d.hbits;   // static groups: no bucket table / chains
     quad();
     d.o_zero = o;
     d.o_cnt = o; o += kCntWords;
@@ -295,12 +356,9 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.o_cpos = o; o += d.S;
     d.o_order = o; o += d.capE;
     d.o_hpos = o; o += d.capE;
-    // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
-    d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
     d.o_icnt = o; o += d.iblk ? nA : 0;
     quad();
     d.o_imask = o; o += d.iblk ? 4 * nA : 0;
-    d.nb_m = nB ? (1ull << 32) / nB : 0;
     quad();
     d.words = o;
     return PVAC_OK;
@@ -357,8 +415,17 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
 int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     if (!c) return PVAC_OK;
     hipSetDevice(c->device);
+    for (pvac_hip_ctx* k : c->chain_kids) pvac_hip_ctx_destroy(k);
+    c->chain_kids.clear();
     if (c->stream) hipStreamSynchronize(c->stream);
     flush_timers(c);
+    for (chain_set& b : c->chain_bufs)
+        for (void* q : {(void*)b.l_off, (void*)b.l_cnt, (void*)b.e_off, (void*)b.e_cnt, (void*)b.layers, (void*)b.meta,
+                        (void*)b.w_lo, (void*)b.w_hi})
+            if (q) hipFreeAsync(q, c->stream);
+    if (c->chain_nonces) hipFreeAsync(c->chain_nonces, c->stream);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    hipFree(c->chain_stats);
     hipFree(c->nb_table);
     hipFree(c->nb_magic);
     hipFree(c->pair_class);
@@ -512,7 +579,7 @@ int plan_static_groups(pvac_hip_ctx* c) {
         if (it == off.end() || d.nbm.d < 2 * d.S || !d.S) continue;
         std::string why;
         large_desc x;
-        rc = build_large_desc(x, d.pair, d.LA, d.LB, d.nA, d.nB, c->prm.B, why, true);
+        rc = build_large_desc(x, d.pair, d.LA, d.LB, d.nA, d.nB, c->prm.B, why, true, !c->large_no_direct);
         if (rc) return fail(c, rc, why);
         x.g_head = it->second;
         x.g_next = it->second + cfg[d.nbm.d];
@@ -605,38 +672,44 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
     if (!rc) rc = ensure_dev(c, c->sel_dev, c->sel_cap, nl, "alloc large descriptor order");
     if (rc) return rc;
     c->sel_host.resize(nl);
-    // A/B knobs of k_large_products_la (environment, read once)
-    static const uint32_t la_per_wg = [] {
-        const char* e = std::getenv("PVAC_LA_PER_WG");
-        const int v = e ? std::atoi(e) : 0;
-        return v >= 1 && v <= 64 ? (uint32_t)v : kLaPerWG;
-    }();
-    static const uint32_t la_xcd = [] {
-        const char* e = std::getenv("PVAC_LA_XCD");
-        return e && e[0] == '1' ? 1u : 0u;
-    }();
+    // A-layers per workgroup and the XCD-aware grid of k_large_products_la: compile-time A/B knobs
+#ifndef PVAC_LA_PER_WG
+#define PVAC_LA_PER_WG kLaPerWG
+#endif
+#ifndef PVAC_LA_XCD
+#define PVAC_LA_XCD 0
+#endif
+    constexpr uint32_t la_per_wg = PVAC_LA_PER_WG, la_xcd = PVAC_LA_XCD;
+    static_assert(la_per_wg >= 1 && la_per_wg <= 64, "A layers per products workgroup");
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
     uint64_t budget = std::max<uint64_t>((uint64_t)(free_b / 2) / 4 + c->arena_words, 1ull << 24);
     budget = std::min<uint64_t>(budget, 16ull << 30);   // <= 64 GiB of scratch per sub-batch
+    // a worker of pvac_hip_ct_mul_chain shares the device with the other workers: its share
+    if (c->arena_cap_words) budget = std::min<uint64_t>(budget, std::max<uint64_t>(c->arena_cap_words, c->arena_words));
     c->large_exec = c->large_host;
     size_t i = 0;
     while (i < nl) {
         uint64_t words = 0;
         size_t j = i;
         uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0, mA = 0;
-        bool dyn = false, all_ib = true;
+        bool dyn = false, all_ib = true, any_dir = false, all_dir = true;
         while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
             large_desc& d = c->large_exec[j];
             const uint64_t w = d.words;
             rebase_desc(d, words);
             words += w;
-            mS = std::max(mS, d.S);
+            // direct pairs have no per-key scratch: the slot- and edge-sized grids are the others'
+            if (!d.direct) {
+                mS = std::max(mS, d.S);
+                mE = std::max(mE, d.capE);
+                mA = std::max<uint64_t>(mA, d.iblk ? d.nA : 0);
+            }
             mZ = std::max(mZ, d.zero_words);
-            mE = std::max(mE, d.capE);
-            mA = std::max<uint64_t>(mA, d.iblk ? d.nA : 0);
             dyn |= d.g_head == kNoGrp;
             all_ib &= d.iblk != 0;
+            any_dir |= d.direct != 0;
+            all_dir &= d.direct != 0;
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
         }
@@ -658,13 +731,25 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         if (words > c->arena_words) {
             // grow with 1/8 headroom (within the budget): batches of similar pairs differ by a few
             // words, and a free + re-malloc of tens of GB stalls for seconds
-            const uint64_t grown = std::max<uint64_t>(words, std::min<uint64_t>(words + words / 8, budget));
+            uint64_t grown = std::max<uint64_t>(words, std::min<uint64_t>(words + words / 8, budget));
             hipStreamSynchronize(c->stream);
             const auto t0 = std::chrono::steady_clock::now();
             hipFree(c->arena);
             c->arena = nullptr;
             c->arena_words = 0;
             hipError_t e = hipMalloc(&c->arena, grown * 4);
+            if (e == hipErrorOutOfMemory && grown > words) {   // without the headroom
+                (void)hipGetLastError();
+                grown = words;
+                e = hipMalloc(&c->arena, grown * 4);
+            }
+            if (e == hipErrorOutOfMemory && j - i > 1) {
+                // other contexts hold the HBM the budget counted on: split this sub-batch and retry
+                (void)hipGetLastError();
+                for (size_t k = i; k < j; ++k) c->large_exec[k] = c->large_host[k];
+                budget = std::max<uint64_t>(words / 2, 1);
+                continue;
+            }
             if (e != hipSuccess) return hip_fail(c, e, "alloc ct_mul scratch arena");
             c->arena_words = grown;
             if (std::getenv("PVAC_DEBUG_ARENA"))
@@ -697,6 +782,10 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.max_tasks_all = mTa; a.max_la_wg = mLa; a.max_nA = mA;
         a.any_dyn = dyn ? 1u : 0u;
         a.all_iblk = all_ib ? 1u : 0u;
+        a.any_direct = any_dir ? 1u : 0u;
+        a.all_direct = all_dir ? 1u : 0u;
+        a.redo_ids = c->redo_ids;
+        a.redo_cnt = c->redo_cnt;
         a.la_per_wg = la_per_wg;
         a.la_xcd = la_xcd;
         e = launch_ct_mul_large(a, c->stream);
@@ -706,9 +795,11 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
     return PVAC_OK;
 }
 
-// The fresh kernel emits every key cell that received a product; a cell whose sum is 0 mod p
-// (cancelling products or a zero weight, arithmetic.hpp:98-99) makes it flag the pair instead.
-// Those pairs are re-run here on the general path, which folds every sum before it orders keys.
+// The fresh kernel and the general path's direct mode emit every key cell that received a
+// product; a cell whose sum is 0 mod p (cancelling products or a zero weight, arithmetic.hpp:98-99)
+// makes them flag the pair instead, and a direct pair that needs the canonical order or shares
+// buckets is flagged too. Those pairs are re-run here on the general path's full layout, which
+// folds every sum before it orders keys.
 int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, const uint64_t* nonces,
                      pvac_ct_batch* C, uint32_t flags, uint32_t* salt_pos) {
     unsigned int cnt = 0;
@@ -733,9 +824,11 @@ int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batc
     std::vector<large_desc> plan_set;
     plan_set.swap(c->large_host);
     c->large_host.swap(redo);
+    c->large_no_direct = true;   // the exact path: per-key sums, no presence-based positions
     int rc = plan_static_groups(c);
     if (!rc) rc = run_large(c, A, B, nonces, C, flags, salt_pos);
     if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = hip_fail(c, hipErrorUnknown, "ct_mul_exec (redo)");
+    c->large_no_direct = false;
     c->large_host.swap(plan_set);
     if (!rc) {
         c->redo_total += cnt;
@@ -768,6 +861,10 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         int rc = ensure_dev(c, c->salt_pos, c->salt_cap, plan->total_edge_slots, "alloc salt positions");
         if (rc) return rc;
         salt_pos = c->salt_pos;
+    }
+    {
+        const hipError_t e = hipMemsetAsync(c->redo_cnt, 0, sizeof(unsigned int), c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "reset redo count");
     }
     if (plan->n_small) {
         mul_fresh_args a{};
@@ -803,7 +900,6 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         // stream-ordered copy from the ctx's host mirror (kept alive until the next exec)
         c->fresh_args_host = a;
         hipError_t e = hipMemcpyAsync(c->fresh_args, &c->fresh_args_host, sizeof a, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess) e = hipMemsetAsync(c->redo_cnt, 0, sizeof(unsigned int), c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "upload fresh args");
         scoped_timer t(c, "ct_mul_fresh");
         e = launch_ct_mul_fresh(a, c->fresh_args, c->num_cus, c->stream);
@@ -814,7 +910,7 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         int rc = run_large(c, A, B, nonces, C, flags, salt_pos);
         if (rc) return rc;
     }
-    if (plan->n_small) {
+    {
         int rc = redo_fresh_pairs(c, A, B, nonces, C, flags, salt_pos);
         if (rc) return rc;
     }
@@ -1317,6 +1413,250 @@ uint64_t pvac_hip_bucket_count(uint64_t n) { return bucket_count_after_reserve(n
 int pvac_hip_batch_digest(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* out) {
     if (!c || !batch_ok(X) || (X->n && !out)) return PVAC_EINVAL;
     return hip_fail(c, launch_batch_digest(*X, out, c->stream), "batch_digest");
+}
+
+// ---------------------------------------------------------------- depth chains
+}  // extern "C"
+
+namespace {
+
+// grows a stream-ordered device array to at least `need` elements (1/8 headroom); contents are lost
+template <typename T>
+hipError_t grow_async(T*& p, size_t& cap, size_t need, hipStream_t st) {
+    if (need <= cap && p) return hipSuccess;
+    if (p) hipFreeAsync(p, st);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(need + need / 8, 64);
+    hipError_t e = hipMallocAsync((void**)&p, want * sizeof(T), st);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        e = hipMallocAsync((void**)&p, std::max<size_t>(need, 64) * sizeof(T), st);
+        if (e == hipSuccess) cap = std::max<size_t>(need, 64);
+    } else if (e == hipSuccess) {
+        cap = want;
+    }
+    return e;
+}
+
+struct chain_shared {
+    const pvac_ct_batch* X = nullptr;
+    const pvac_chain_opts* o = nullptr;
+    uint64_t chunk = 0;
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> stop{0};
+    std::mutex mu;
+    int rc = PVAC_OK;
+    std::string err;
+    void failed(int code, const std::string& msg) {
+        std::lock_guard<std::mutex> g(mu);
+        if (rc == PVAC_OK) {
+            rc = code;
+            err = msg;
+        }
+        stop.store(1);
+    }
+};
+
+struct chain_wstats {
+    uint64_t gsum_pairs = 0, gsum_failed = 0, chunks = 0;
+};
+
+pvac_ct_batch chain_view(const pvac_ct_batch& X, uint64_t c0, uint64_t k) {
+    pvac_ct_batch v = X;
+    v.n = k;
+    v.l_off = X.l_off + c0;
+    v.l_cnt = X.l_cnt + c0;
+    v.e_off = X.e_off + c0;
+    v.e_cnt = X.e_cnt + c0;
+    v.sigma = nullptr;
+    v.sigma_words = 0;
+    return v;
+}
+
+// one worker: chunks in input order from the shared counter, depth steps of plan + exec each on
+// this context's stream, the final c_depth to the digests / on_chunk
+void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
+    if (hipSetDevice(k->device) != hipSuccess) {
+        sh->failed(PVAC_EDEVICE, "ct_mul_chain: hipSetDevice");
+        return;
+    }
+    const pvac_chain_opts& o = *sh->o;
+    const pvac_ct_batch& X = *sh->X;
+    const uint32_t mflags = o.flags & PVAC_MUL_ORDER_CANONICAL;
+    const bool check = (o.flags & PVAC_CHAIN_CHECK_GSUM) != 0;
+    auto hipchk = [&](hipError_t e, const char* where) {
+        if (e == hipSuccess) return true;
+        sh->failed(e == hipErrorOutOfMemory ? PVAC_ENOMEM : PVAC_EDEVICE,
+                   std::string("ct_mul_chain: ") + where + ": " + hipGetErrorString(e));
+        return false;
+    };
+    auto rcchk = [&](int rc, const char* where) {
+        if (rc == PVAC_OK) return true;
+        sh->failed(rc, std::string("ct_mul_chain: ") + where + ": " + k->err);
+        return false;
+    };
+    for (;;) {
+        if (sh->stop.load()) return;
+        const uint64_t c0 = sh->next.fetch_add(1) * sh->chunk;
+        if (c0 >= X.n) return;
+        const uint64_t kk = std::min<uint64_t>(sh->chunk, X.n - c0);
+        const pvac_ct_batch Xv = chain_view(X, c0, kk);
+        pvac_ct_batch A = Xv;
+        int cur = 0;
+        for (uint32_t d = 0; d < o.depth; ++d) {
+            if (sh->stop.load()) return;
+            chain_set& S = k->chain_bufs[cur];
+            if (kk > S.n_cap) {
+                size_t c1 = S.n_cap, c2 = S.n_cap, c3 = S.n_cap, c4 = S.n_cap;
+                if (!hipchk(grow_async(S.l_off, c1, kk, k->stream), "alloc offsets") ||
+                    !hipchk(grow_async(S.l_cnt, c2, kk, k->stream), "alloc counts") ||
+                    !hipchk(grow_async(S.e_off, c3, kk, k->stream), "alloc offsets") ||
+                    !hipchk(grow_async(S.e_cnt, c4, kk, k->stream), "alloc counts"))
+                    return;
+                S.n_cap = std::min(std::min(c1, c2), std::min(c3, c4));
+            }
+            pvac_ct_batch C{};
+            C.n = kk;
+            C.l_off = S.l_off;
+            C.l_cnt = S.l_cnt;
+            C.e_off = S.e_off;
+            C.e_cnt = S.e_cnt;
+            pvac_hip_plan plan{};
+            if (!rcchk(pvac_hip_ct_mul_plan(k, &A, &Xv, &C, &plan), "plan")) return;
+            if (plan.total_layer_slots > S.l_cap &&
+                !hipchk(grow_async(S.layers, S.l_cap, plan.total_layer_slots, k->stream), "alloc layers"))
+                return;
+            if (plan.total_edge_slots > S.e_cap) {
+                size_t c1 = S.e_cap, c2 = S.e_cap, c3 = S.e_cap;
+                if (!hipchk(grow_async(S.meta, c1, plan.total_edge_slots, k->stream), "alloc edges") ||
+                    !hipchk(grow_async(S.w_lo, c2, plan.total_edge_slots, k->stream), "alloc edges") ||
+                    !hipchk(grow_async(S.w_hi, c3, plan.total_edge_slots, k->stream), "alloc edges"))
+                    return;
+                S.e_cap = std::min(c1, std::min(c2, c3));
+            }
+            const size_t nw = 2 * std::max<uint64_t>(plan.total_layer_slots, 1);
+            if (!hipchk(grow_async(k->chain_nonces, k->chain_nonce_cap, nw, k->stream), "alloc nonces")) return;
+            C.layers = S.layers;
+            C.meta = S.meta;
+            C.w_lo = S.w_lo;
+            C.w_hi = S.w_hi;
+            if (o.fill_nonces) {
+                if (o.fill_nonces(o.user, d, c0, nw, k->chain_nonces, (void*)k->stream) != 0) {
+                    sh->failed(PVAC_EINVAL, "ct_mul_chain: fill_nonces callback failed");
+                    return;
+                }
+            } else if (!hipchk(launch_fill_random(o.nonce_seed + 97ull * c0 + d, k->chain_nonces, nw, k->stream),
+                               "fill nonces")) {
+                return;
+            }
+            if (!rcchk(pvac_hip_ct_mul_exec(k, &plan, &A, &Xv, k->chain_nonces, nullptr, &C, mflags), "exec")) return;
+            if (!hipchk(launch_chain_stats(A, Xv, C, k->chain_stats + 2 * d, k->stream), "stats")) return;
+            if (check) {
+                uint64_t bad = 0;
+                if (!rcchk(pvac_hip_check_mul_gsum(k, &A, &Xv, &C, k->chain_nonces, nullptr, &bad), "gsum check"))
+                    return;
+                ws->gsum_pairs += kk;
+                ws->gsum_failed += bad;
+            }
+            A = C;
+            cur ^= 1;
+        }
+        if (o.digest_n > c0 && (o.digest_out || o.count_out)) {
+            pvac_ct_batch H = A;
+            H.n = std::min<uint64_t>(kk, o.digest_n - c0);
+            if (o.digest_out && !hipchk(launch_batch_digest(H, o.digest_out + c0, k->stream), "digest")) return;
+            if (o.count_out &&
+                !hipchk(hipMemcpyAsync(o.count_out + c0, H.e_cnt, H.n * 8, hipMemcpyDeviceToDevice, k->stream), "counts"))
+                return;
+        }
+        if (o.on_chunk && o.on_chunk(o.user, c0, &A, (void*)k->stream) != 0) {
+            sh->failed(PVAC_EINVAL, "ct_mul_chain: on_chunk callback failed");
+            return;
+        }
+        ++ws->chunks;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_chain_opts* o, pvac_chain_stats* st) {
+    if (!c || !o || !st || !batch_ok(X)) return fail(c, PVAC_EINVAL, "ct_mul_chain: bad arguments");
+    if (o->depth < 1 || o->depth > PVAC_CHAIN_MAX_DEPTH) return fail(c, PVAC_EINVAL, "ct_mul_chain: depth");
+    if (o->flags & ~(PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM))
+        return fail(c, PVAC_EINVAL, "ct_mul_chain: flags (WITH_SIGMA is not supported on chains)");
+    if ((o->flags & PVAC_CHAIN_CHECK_GSUM) && !c->powg)
+        return fail(c, PVAC_EINVAL, "ct_mul_chain: CHECK_GSUM needs pvac_hip_ctx_set_powg");
+    if (X->n && (!X->layers || !X->meta || !X->w_lo || !X->w_hi)) return fail(c, PVAC_EINVAL, "ct_mul_chain: input arrays");
+    std::memset(st, 0, sizeof *st);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!X->n) return PVAC_OK;
+    const uint32_t S = o->streams ? std::min<uint32_t>(o->streams, 64) : 4u;
+    const uint64_t chunk = o->chunk ? o->chunk : 1024;
+    // inputs already enqueued on the caller's stream must be complete before other streams read them
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain (caller stream)");
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
+    // each worker's general-path scratch: its share of half the HBM free now (the other half holds
+    // the workers' ping-pong outputs and the caller's data)
+    const uint64_t cap_words = std::max<uint64_t>((uint64_t)(free_b / 2) / S / 4, 1ull << 24);
+    while (c->chain_kids.size() < S) {
+        pvac_hip_ctx* k = nullptr;
+        const int rc = pvac_hip_ctx_create(c->device, &c->prm, &k);
+        if (rc) return fail(c, rc, "ct_mul_chain: worker context");
+        c->chain_kids.push_back(k);
+        e = hipMalloc(&k->chain_stats, 2 * PVAC_CHAIN_MAX_DEPTH * sizeof(unsigned long long));
+        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain: worker statistics");
+    }
+    for (uint32_t w = 0; w < S; ++w) {
+        pvac_hip_ctx* k = c->chain_kids[w];
+        k->arena_cap_words = cap_words;
+        k->prm = c->prm;
+        if (c->powg && (k->powg_n != c->powg_n || !k->powg)) {
+            hipFree(k->powg);
+            k->powg = nullptr;
+            e = hipMalloc(&k->powg, (size_t)c->powg_n * 16);
+            if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain: worker powg");
+            k->powg_n = c->powg_n;
+        }
+        if (c->powg) e = hipMemcpy(k->powg, c->powg, (size_t)c->powg_n * 16, hipMemcpyDeviceToDevice);
+        if (e == hipSuccess) e = hipMemsetAsync(k->chain_stats, 0, 2 * PVAC_CHAIN_MAX_DEPTH * 8, k->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(k->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain: worker setup");
+    }
+    chain_shared sh;
+    sh.X = X;
+    sh.o = o;
+    sh.chunk = chunk;
+    std::vector<chain_wstats> ws(S);
+    std::vector<uint64_t> redo0(S);
+    for (uint32_t w = 0; w < S; ++w) redo0[w] = c->chain_kids[w]->redo_total;
+    std::vector<std::thread> th;
+    th.reserve(S);
+    for (uint32_t w = 0; w < S; ++w) th.emplace_back(chain_worker, c->chain_kids[w], &sh, &ws[w]);
+    for (std::thread& t : th) t.join();
+    for (uint32_t w = 0; w < S; ++w) {
+        pvac_hip_ctx* k = c->chain_kids[w];
+        e = hipStreamSynchronize(k->stream);
+        if (e != hipSuccess && sh.rc == PVAC_OK) sh.failed(PVAC_EDEVICE, std::string("ct_mul_chain: ") + hipGetErrorString(e));
+        unsigned long long v[2 * PVAC_CHAIN_MAX_DEPTH];
+        if (hipMemcpy(v, k->chain_stats, sizeof v, hipMemcpyDeviceToHost) == hipSuccess)
+            for (uint32_t d = 0; d < o->depth; ++d) {
+                st->edges[d] += v[2 * d];
+                st->products[d] += v[2 * d + 1];
+            }
+        st->gsum_pairs += ws[w].gsum_pairs;
+        st->gsum_failed += ws[w].gsum_failed;
+        st->chunks += ws[w].chunks;
+        st->redo += k->redo_total - redo0[w];
+    }
+    st->pair_steps = X->n * o->depth;
+    st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (sh.rc != PVAC_OK) return fail(c, sh.rc, sh.err);
+    return PVAC_OK;
 }
 
 }  // extern "C"

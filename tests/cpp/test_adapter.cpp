@@ -5,6 +5,7 @@
 //   test_adapter <golden_dir> <canon_tag> <H_digest_hex>
 // Exit 0 = every check passed; failures abort with a message (like the reference's must()).
 //   test_adapter --time <pairs>   end-to-end (host ciphers in and out) ct_mul rate, JSON
+#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cinttypes>
@@ -246,8 +247,78 @@ static int time_host_roundtrip(size_t n) {
     return 0;
 }
 
+// --time-single <calls>: latency of ONE by-value drop-in call pvac_hip::ct_mul(pk, A, B) WITH sigma
+// (the reference's full ct_mul, ops/arithmetic.hpp:47-106, as tests/test_main.cpp:178-188 and the
+// chain at :291-292 call it: one pair at a time, host ciphers in and out, getrandom nonces and
+// salts), on fresh x fresh and on chain step 3 x fresh (c_3 = ((x x) x) x). Prints one JSON line
+// with p50 / p99 / mean per call in ms.
+static int time_single(size_t calls) {
+    uint64_t st = 0x5EED0007;
+    auto rnd = [&]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto fresh = [&]() {
+        Cipher c;
+        c.L.resize(2);
+        for (auto& l : c.L) { l.rule = mirror::RRule::BASE; l.seed.ztag = rnd(); l.seed.nonce = {rnd(), rnd()}; l.pa = l.pb = 0; }
+        for (uint32_t la = 0; la < 2; ++la) {
+            std::vector<uint32_t> used;
+            while (used.size() < 20) {
+                const uint32_t k = (uint32_t)(rnd() % (2 * 337));
+                bool dup = false;
+                for (uint32_t u : used) dup |= u == k;
+                if (dup) continue;
+                used.push_back(k);
+                mirror::Edge e{};
+                e.layer_id = la; e.idx = (uint16_t)(k >> 1); e.ch = (uint8_t)(k & 1);
+                e.w = mirror::Fp{rnd(), rnd() & 0x7FFFFFFFFFFFFFFFull};
+                e.s.nbits = 8192;
+                e.s.w.assign(128, rnd());
+                c.E.push_back(e);
+            }
+        }
+        return c;
+    };
+    mirror::PubKey pk;   // empty pk.H: regenerated on the device from canon_tag (pvac_hip_ctx_gen_H)
+    pk.canon_tag = 0x5EED0007;
+    auto src = [&]() { return rnd(); };
+    auto pct = [](std::vector<double> v, double q) {
+        std::sort(v.begin(), v.end());
+        return v[std::min(v.size() - 1, (size_t)(q * (v.size() - 1) + 0.5))];
+    };
+    auto run = [&](const Cipher& a, const Cipher& b, size_t k, size_t& edges) {
+        std::vector<double> ms;
+        (void)pvac_hip::ct_mul(pk, a, b, src);   // warm-up: H, code objects, allocations
+        for (size_t i = 0; i < k; ++i) {
+            const auto t0 = std::chrono::steady_clock::now();
+            const Cipher c = pvac_hip::ct_mul(pk, a, b, src);
+            ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            edges = c.E.size();
+            MUST(!c.E.empty() && c.E[0].s.w.size() == 128, "sigma missing");
+        }
+        double mean = 0;
+        for (double x : ms) mean += x;
+        return std::array<double, 3>{pct(ms, 0.5), pct(ms, 0.99), mean / ms.size()};
+    };
+    const Cipher x = fresh(), y = fresh();
+    size_t e1 = 0, e2 = 0;
+    const auto f = run(x, y, calls, e1);
+    Cipher c = x;   // chain c_k = c_{k-1} * x (tests/test_main.cpp:291-292)
+    for (int k = 0; k < 3; ++k) c = pvac_hip::ct_mul(pk, c, x, src);
+    const auto g = run(c, x, std::max<size_t>(calls / 5, 5), e2);
+    std::printf("{\"fresh_x_fresh\": {\"calls\": %zu, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"mean_ms\": %.4f, "
+                "\"output_edges\": %zu}, \"chain3_x_fresh\": {\"calls\": %zu, \"input_edges\": %zu, \"p50_ms\": %.4f, "
+                "\"p99_ms\": %.4f, \"mean_ms\": %.4f, \"output_edges\": %zu}}\n",
+                calls, f[0], f[1], f[2], e1, std::max<size_t>(calls / 5, 5), c.E.size(), g[0], g[1], g[2], e2);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc == 3 && std::string(argv[1]) == "--time") return time_host_roundtrip(std::strtoull(argv[2], nullptr, 10));
+    if (argc == 3 && std::string(argv[1]) == "--time-single") return time_single(std::strtoull(argv[2], nullptr, 10));
     if (argc < 5) {
         std::fprintf(stderr, "usage: %s <golden_dir> <canon_tag> <H_digest_hex> <v0,v1,...>\n", argv[0]);
         return 2;

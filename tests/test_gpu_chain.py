@@ -1,0 +1,135 @@
+"""pvac_hip_ct_mul_chain (include/pvac_hip.h): the reference's chain workload c_k = ct_mul(c_{k-1}, x)
+(tests/test_main.cpp:289-295) over a batch of inputs, run by the library on internal worker streams.
+Every chain's final c_depth must equal the same chain driven step by step through ct_mul_plan /
+ct_mul_exec on one stream, and the pinned CPU port's chain (orc_ct_mul_chain_timed)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import Cipher, default_params, fixture_secret, pack_device_batch, read_u64
+
+pytestmark = pytest.mark.gpu
+
+
+def _stepwise(eng, X, depth, seed, chunk):
+    """The same chains step by step on the caller's stream, chunk by chunk with the library's nonce
+    seeds (nonce_seed + 97 * first_input + step): final digests, counts and per-step edge sums."""
+    import torch
+    from pvac_hfhe_cppbyv_amd import DeviceBatch
+    dig, cnt, edges = [], [], [0] * depth
+    for c0 in range(0, X.n, chunk):
+        k = min(chunk, X.n - c0)
+        Xv = DeviceBatch(k, X.l_off[c0:c0 + k], X.l_cnt[c0:c0 + k], X.layers, X.e_off[c0:c0 + k],
+                         X.e_cnt[c0:c0 + k], X.meta, X.w_lo, X.w_hi)
+        cur = Xv
+        for d in range(depth):
+            Cb, plan = eng.ct_mul_plan(cur, Xv)
+            nonces = torch.empty(2 * max(plan.total_layer_slots, 1), dtype=torch.int64, device=eng.device)
+            eng.fill_random(nonces, seed + 97 * c0 + d)
+            cur = eng.ct_mul(cur, Xv, nonces=nonces, C_=Cb, plan=plan)
+            edges[d] += int(cur.e_cnt[:k].sum().item())
+        dig.append(eng.digest(cur).cpu().numpy().view(np.uint64).copy())
+        cnt.append(cur.e_cnt[:k].cpu().numpy().view(np.uint64).copy())
+    return np.concatenate(dig), np.concatenate(cnt), edges
+
+
+def test_chain_api_equals_stepwise_and_oracle(oracle):
+    """enc_value inputs (the cfg-4 producer), depth 5, 3 worker streams over chunks of 7 (a ragged
+    last chunk): digests and edge counts of every chain equal the step-by-step engine run and the
+    CPU port; the gsum invariant holds on every pair-step; the statistics add up."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    sk, man, em = fixture_secret()
+    eng = Engine(device=0, canon_tag=man["canon_tag"])
+    assert eng.gen_H().hex() == man["H_digest"]
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    eng.set_powg(read_u64("powg_B.u64"))
+    rng = np.random.default_rng(0xC4A5)
+    n, depth, chunk, seed = 40, 5, 7, 0x7E57
+    X, st = eng.enc_value(rng.integers(0, 2**64, n, dtype=np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    r = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=3, chunk=chunk, check_gsum=True, digest_n=n)
+    assert r["chunks"] == (n + chunk - 1) // chunk and r["pair_steps"] == n * depth
+    assert r["gsum_pairs"] == n * depth and r["gsum_failed"] == 0 and r["redo"] == 0
+    dig, cnt, edges = _stepwise(eng, X, depth, seed, chunk)
+    assert np.array_equal(r["digests"], dig) and np.array_equal(r["counts"], cnt)
+    assert r["edges"] == edges and r["edges"][-1] == int(cnt.sum())
+    xe = X.e_cnt[:n].cpu().numpy().astype(np.int64)
+    assert r["products"][0] == int((xe * xe).sum())
+    # the CPU port's chains on the same inputs
+    px = pack_device_batch(X, n)
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
+    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(man["canon_tag"])), n, *(P_(a) for a in px), depth, 8,
+                                      P_(ocnt), P_(odig), P_(se))
+    assert np.array_equal(ocnt, cnt) and np.array_equal(odig, dig)
+    # a second call reuses the worker contexts and buffers: same result
+    r2 = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=3, chunk=chunk, digest_n=n)
+    assert np.array_equal(r2["digests"], dig) and r2["gsum_pairs"] == 0
+
+
+def test_chain_api_callbacks_and_errors():
+    """fill_nonces / on_chunk callbacks from the worker threads: every chunk arrives once with its
+    first input and size, the nonces come from the callback (different nonces, same edges: a digest
+    covers (meta, w) only, and layer ztags change), and a failing callback stops the chain with
+    PVAC_EINVAL. Bad options are refused."""
+    import threading
+    import torch
+    from pvac_hfhe_cppbyv_amd import FILL_NONCES_CB, ON_CHUNK_CB, Engine, PvacError
+    eng = Engine(device=0, canon_tag=0xCA11)
+    n, depth, chunk = 24, 3, 5
+    X = eng.gen_fresh(n, 0xCA12, 20)
+    base = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n)
+    lock = threading.Lock()
+    seen, fills = [], []
+    fill_lib = eng.lib
+
+    def fill(user, step, first, nwords, dev, stream):
+        # splitmix words through a context of this thread's own (one thread per context)
+        with lock:
+            fills.append((step, first, nwords))
+        return 0 if fill_lib.pvac_hip_fill_random(ctxs[threading.get_ident()], 0xF111 + step, dev, nwords) == 0 else 1
+
+    def chunk_cb(user, first, cb, stream):
+        b = cb.contents
+        with lock:
+            seen.append((first, b.n))
+        return 0
+
+    # per-thread helper contexts for the fill callback (created lazily on the worker threads)
+    ctxs = {}
+    from pvac_hfhe_cppbyv_amd import Params
+
+    def fill_wrap(user, step, first, nwords, dev, stream):
+        tid = threading.get_ident()
+        if tid not in ctxs:
+            c = C.c_void_p()
+            prm = Params(B=337, m_bits=8192, n_bits=16384, h_col_wt=192, x_col_wt=128, err_wt=128,
+                         edge_budget=1200000, canon_tag=0xCA11)
+            assert eng.lib.pvac_hip_ctx_create(0, C.byref(prm), C.byref(c)) == 0
+            assert eng.lib.pvac_hip_ctx_set_stream(c, C.c_void_p(stream)) == 0
+            ctxs[tid] = c
+        return fill(user, step, first, nwords, dev, stream)
+
+    fcb, ccb = FILL_NONCES_CB(fill_wrap), ON_CHUNK_CB(chunk_cb)
+    r = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n, fill_nonces=fcb, on_chunk=ccb)
+    for c in ctxs.values():
+        eng.lib.pvac_hip_ctx_destroy(c)
+    assert sorted(seen) == [(c0, min(chunk, n - c0)) for c0 in range(0, n, chunk)]
+    assert len(fills) == depth * len(seen) and all(w >= 2 for _, _, w in fills)
+    assert np.array_equal(r["digests"], base["digests"])
+
+    def bad_chunk(user, first, cb, stream):
+        return 1
+
+    with pytest.raises(PvacError):
+        eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, on_chunk=ON_CHUNK_CB(bad_chunk))
+    with pytest.raises(PvacError):
+        eng.ct_mul_chain(X, 0)
+    with pytest.raises(PvacError):   # no powg on this context
+        eng.ct_mul_chain(X, 2, check_gsum=True)
+    # the context is still usable after the errors
+    r3 = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n)
+    assert np.array_equal(r3["digests"], base["digests"])
+    torch.cuda.synchronize()

@@ -530,3 +530,43 @@ def test_enc_value_chains_depth8_digests_vs_oracle(oracle):
     assert np.array_equal(cnt, gcnt)
     assert np.array_equal(dig, gdig)
     assert int(se[-1]) == int(gcnt.sum()) and gcnt.min() > 300000
+
+
+def test_direct_cancelling_key_redo_vs_oracle(oracle):
+    """Chain-step pairs take the direct mode (large_desc::direct: emit positions counted from key
+    presence, C's records written from the products' epilogue). A P cell whose products cancel
+    (sum 0 mod p, arithmetic.hpp:96-101 drops its edge) breaks the presence assumption: the pair
+    must be handed to the redo on the exact path and come out bit-exact. Here one A weight is
+    solved so that the P sum of key (0, 0, r) is 0; the other pairs of the batch stay direct."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    B = 337
+    rng = np.random.default_rng(0xCA2C)
+    xs = [_mk_layers(rng, [674, 674]) for _ in range(4)]
+    ys = [_mk_layers(rng, [20, 20]) for _ in range(4)]
+    x, y = xs[1], ys[1]
+    lid = lambda m: int(m & 0xFFFFFFFF)
+    idx = lambda m: int((m >> 32) & 0xFFFF)
+    ch = lambda m: int((m >> 48) & 0xFF)
+    w = lambda c, k: (int(c.w_lo[k]) | (int(c.w_hi[k]) << 64)) % ((1 << 127) - 1)
+    P_ = (1 << 127) - 1
+    r = 5
+    a_at = {(idx(m), ch(m)): k for k, m in enumerate(x.meta) if lid(m) == 0}
+    terms = []   # (A edge, B edge) of every product in key (0, 0, r)'s P cell
+    for j, m in enumerate(y.meta):
+        if lid(m) == 0:
+            terms.append((a_at[((r - idx(m)) % B, ch(m))], j))
+    assert len(terms) == 20
+    (k0, j0), rest = terms[0], terms[1:]
+    s = sum(w(x, k) * w(y, j) for k, j in rest) % P_
+    v = (-s * pow(w(y, j0), P_ - 2, P_)) % P_
+    x.w_lo[k0], x.w_hi[k0] = np.uint64(v & ((1 << 64) - 1)), np.uint64(v >> 64)
+    assert (sum(w(x, k) * w(y, j) for k, j in terms)) % P_ == 0
+    eng = Engine(device=0, canon_tag=0xCA2D)
+    r0 = eng.ct_mul_redo_count()
+    out, plan, per = _run_mul(eng, xs, ys, seed=0xCA2E)
+    assert plan.n_large == 4
+    assert eng.ct_mul_redo_count() - r0 == 1   # only the cancelling pair left the direct mode
+    for p in range(4):
+        ref = oracle.ct_mul(xs[p], ys[p], per[p], canon_tag=0xCA2D)
+        _same(out[p], ref, view=False)
+    assert out[0].nE == 4 * 337 * 2 and out[1].nE == 4 * 337 * 2 - 1   # saturated: every cell emits but one

@@ -14,16 +14,10 @@ import torch  # noqa: E402
 
 from pvac_hfhe_cppbyv_amd import Engine, load_library  # noqa: E402
 
-PHASES_V1 = ["prologue", "S1 products", "S2a fold+bucket (after compact)", "S2b link", "S2c walk+closure", "S3 scan",
-             "S4 positions", "clear", "S5 writer", "end barrier", "S1 next header + prefetch issue",
-             "  S1 work (before barrier)", "  S2a reads", "  S2a fold", "  S2a zero+or", "  S2c walks (before closure)",
-             "  S4 prefetch wait", "  S4 stage"]
 # k_ct_mul_fresh3 (default kernel): work phases end with an lgkmcnt(0) stamp, then the barrier wait
 PHASES = ["loop top (header, rebuild)", "P1 key times", "  B1 wait", "P2 order", "  B2 wait", "P3 closure (wave 0)",
           "  B3 wait (scan)", "P4 positions", "  B4 wait", "P5 products", "  B5 wait", "P6 writer", "P6 reset+stage",
           "  B6 wait", "-", "-", "-", "-"]
-if os.environ.get("PVAC_FRESH_KERNEL") == "1":
-    PHASES = PHASES_V1
 
 
 def main():
