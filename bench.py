@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--chain-streams", type=int, default=4,
                     help="cfg 4: worker streams of the engine's chain call (pvac_hip_ct_mul_chain): one chunk's "
                          "host planning and dependent launches overlap the other chunks' kernels")
+    ap.add_argument("--chain-no-check", action="store_true",
+                    help="cfg 4: skip the checked second pass and the CPU sample (kernel-trace profiling)")
     ap.add_argument("--chain-compare-streams", action="store_true",
                     help="cfg 4: also time the chain call with 1 worker stream on a subset (side field)")
     ap.add_argument("--enc-values", type=int, default=1 << 14, help="enc_value batch (f2)")
@@ -849,12 +851,21 @@ def chain_bench(eng, args):
     # output buffers (a first allocation of tens of GB waits for the driver to clear the VRAM)
     eng.ct_mul_chain(view(0, min(n, S * chunk)), depth, nonce_seed=seed ^ 0xFFFF, streams=S, chunk=chunk)
     torch.cuda.synchronize(dev)
-    # timed pass: the chains and nothing else
+    # timed pass: the chains and nothing else (the monotonic-clock window lets a kernel trace of the
+    # same command pick out this pass's dispatches: tools/chain_window.py)
+    w0 = time.monotonic_ns()
     t1 = time.perf_counter()
     r = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, digest_n=n_chk)
     torch.cuda.synchronize(dev)
     chain_s = time.perf_counter() - t1
+    w1 = time.monotonic_ns()
     peak = torch.cuda.max_memory_reserved(dev) / 1e9
+    if args.chain_no_check:   # profiling runs: the warm-up and the timed pass only
+        del X_all, vals
+        return {"inputs": n, "depth": depth, "chunk": chunk, "streams": S, "chain_seconds": chain_s,
+                "ct_mul_per_s": n * depth / chain_s, "timed_window_monotonic_ns": [w0, w1],
+                "edges_per_input_by_step": [e / n for e in r["edges"]], "products": float(sum(r["products"])),
+                "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak}
     # check pass (untimed): same nonces, gsum invariant on every pair-step, every final digest
     t2 = time.perf_counter()
     rc = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, check_gsum=True, digest_n=n)
@@ -875,7 +886,7 @@ def chain_bench(eng, args):
            "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
            "edges_per_input_by_step": [e / n for e in r["edges"]],
-           "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak}
+           "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak, "timed_window_monotonic_ns": [w0, w1]}
     gf, gp = rc["gsum_failed"], rc["gsum_pairs"]
     out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
                                  "step, on the device (second, untimed pass with the same nonces)", "pair_steps": gp,

@@ -209,8 +209,17 @@ struct sig_args {
 // 6 blocks per CU (6 waves per SIMD): the compiler keeps the pass loop within 80 VGPRs without
 // spills instead of hoisting the whole SHA-256 message schedule (149 VGPRs, 3 waves per SIMD)
 constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compression per lane covers
+#ifdef PVAC_SIG_ICOPY
+// A/B build: the delta path flips into four bank-interleaved copies of the image (word W of copy k
+// at dword 4 W + k of the 1024 words sigma | bmX | bmN), copy k = lane & 3, so the 8 lanes of a
+// 32-lane write group that share a copy meet on 8 banks instead of 32 lanes on 32 (expected worst
+// bank 2.3 instead of 3.5 addresses per ds_xor); the noise rows wait in 64 words after the columns
+constexpr uint32_t kNoiseWords = 64;
+#else
+constexpr uint32_t kNoiseWords = 0;
+#endif
 __host__ __device__ constexpr uint32_t sigma_wave_words(uint32_t m_bits, uint32_t n_bits, uint32_t x_col_wt) {
-    return ((m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2 + 3) & ~3u) + kMidBatch * 2 * 8;
+    return ((m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2 + kNoiseWords + 3) & ~3u) + kMidBatch * 2 * 8;
 }
 
 // Fast column expansion (default Params: m_bits 8192, n_bits 16384, x_col_wt <= 128, full
@@ -267,7 +276,13 @@ constexpr uint32_t kDeltaBytes = 208;   // 13 chunks of 16 increments; <= 8 brid
 template <int WV>
 __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0, uint32_t c1) {
     constexpr uint32_t img = WV * kFastWaveWords * 4u;   // byte address of wave WV's image
+#ifdef PVAC_SIG_ICOPY
+    uint32_t two = 4u, one = 1u;   // word W of copy k at byte 16 W + 4 k
+    const uint32_t kofs = (threadIdx.x & 3u) << 2;
+#else
     uint32_t two = 2u, one = 1u;
+    constexpr uint32_t kofs = 0;
+#endif
     asm volatile("" : "+v"(two), "+v"(one));   // VGPR operands for the SDWA shifts
     auto word4 = [&](uint32_t& R, uint32_t w) {
 #pragma unroll
@@ -279,7 +294,8 @@ __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0,
                 : "=v"(off) : "v"(two), "v"(R));
             asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
                 : "=v"(bit) : "v"(R), "v"(one));
-            __builtin_assume(off < 1024u);
+            off |= kofs;
+            __builtin_assume(off < 4096u);
             lds_xor(img + off, bit);
         }
     };
@@ -329,7 +345,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t slds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t sw32 = a.m_bits / 32, bx32 = a.n_bits / 32, bn32 = a.m_bits / 32;
-    const uint32_t per_wave = sw32 + bx32 + bn32 + (a.x_col_wt + 1) / 2;
+    const uint32_t per_wave = sw32 + bx32 + bn32 + (a.x_col_wt + 1) / 2 + kNoiseWords;
     uint32_t* sig = slds + (size_t)wave * sigma_wave_words(a.m_bits, a.n_bits, a.x_col_wt);
     uint32_t* bmX = sig + sw32;
     uint32_t* bmN = bmX + bx32;
@@ -345,6 +361,10 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     const uint64_t words_per_sigma = a.X.sigma_words;
     const uint32_t sub = blockIdx.y * 4 + wave, nsub = a.sub_blocks * 4;
     const bool lds_at0 = (uint32_t)(size_t)(lds_u32*)slds == 0u;   // flip_cols_fast's absolute addresses
+#ifdef PVAC_SIG_ICOPY
+    const bool icopy = a.rows_delta && lds_at0;
+    uint16_t* nrows = cols + a.x_col_wt;   // kNoiseWords: err_wt <= 128 rows (host-checked)
+#endif
 
     // the salt-independent words of an edge (salt last: it is the only word in both blocks)
     auto edge_words = [&](uint64_t eo, uint64_t lo, uint64_t nl, uint64_t e, uint64_t (&words)[7]) {
@@ -452,6 +472,9 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                 for (int q = 0; q < 4; ++q) {
                     if (rank[q] >= 0) {
                         if (isX) cols[rank[q]] = (uint16_t)val[q];
+#ifdef PVAC_SIG_ICOPY
+                        else if (icopy) nrows[rank[q]] = (uint16_t)val[q];   // flipped with the columns
+#endif
                         else atomicXor(&sig[val[q] >> 5], 1u << (val[q] & 31));   // noise bit
                     }
                 }
@@ -487,6 +510,31 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                     case 2: flip_cols_delta<2>(a.rows_delta, c0, c1); break;
                     default: flip_cols_delta<3>(a.rows_delta, c0, c1); break;
                 }
+#ifdef PVAC_SIG_ICOPY
+                {   // the noise rows, into the lane's copy like the columns
+                    const uint32_t kofs = ((uint32_t)lane & 3u) << 2;
+                    for (uint32_t q = (uint32_t)lane; q < a.err_wt; q += 64) {
+                        const uint32_t r = nrows[q];
+                        atomicXor((uint32_t*)((uint8_t*)sig + (((r >> 5) << 4) | kofs)), 1u << (r & 31u));
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t* out = a.X.sigma + e * words_per_sigma;
+                {
+                    // output words 4 lane .. 4 lane + 3: each the XOR of its four copies (one b128 read)
+                    uint4* s4 = (uint4*)sig + 4 * lane;
+                    uint32_t o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint4 v = s4[q];
+                        o[q] = v.x ^ v.y ^ v.z ^ v.w;
+                    }
+                    ((ulonglong2*)out)[lane] = make_ulonglong2((uint64_t)o[0] | ((uint64_t)o[1] << 32),
+                                                               (uint64_t)o[2] | ((uint64_t)o[3] << 32));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) s4[q] = make_uint4(0, 0, 0, 0);
+                }
+#else
                 __builtin_amdgcn_wave_barrier();
                 uint64_t* out = a.X.sigma + e * words_per_sigma;
                 {
@@ -496,6 +544,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                                                                (uint64_t)v.z | ((uint64_t)v.w << 32));
                     *s4 = make_uint4(0, 0, 0, 0);
                 }
+#endif
                 __builtin_amdgcn_s_setprio(0);
                 continue;
             }
@@ -896,7 +945,8 @@ hipError_t launch_sigma(const sigma_tables& T, const pvac_hip_params& prm, const
     path = 1;
 #endif
     const bool fast_ok = prm.m_bits == 8192 && prm.x_col_wt == 128 && T.full &&
-                         sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords;
+                         sigma_wave_words(prm.m_bits, prm.n_bits, prm.x_col_wt) == kFastWaveWords &&
+                         (kNoiseWords == 0 || prm.err_wt <= 2 * kNoiseWords);
     a.rows_fast = (fast_ok && path <= 1) ? T.rows_fast : nullptr;
     a.rows_delta = (a.rows_fast && path == 0) ? T.rows_delta : nullptr;
     a.counts = T.counts;

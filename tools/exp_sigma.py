@@ -22,7 +22,8 @@ def main():
         eng = Engine(device=0, canon_tag=0x5EED0003, lib=load_library(path))
         r = bench.sigma_bench(eng, args, False)
         res[os.path.basename(path)] = round(r["sigma_kernel_ms"], 3)
-        print(os.path.basename(path), res[os.path.basename(path)], flush=True)
+        res[os.path.basename(path) + ":checks"] = r.get("checks")
+        print(os.path.basename(path), res[os.path.basename(path)], r.get("checks"), flush=True)
         del eng
         torch.cuda.empty_cache()
     print(json.dumps(res))

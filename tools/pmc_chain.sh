@@ -1,16 +1,17 @@
 #!/bin/bash
-# PMC passes over the cfg-4 chain's general-path kernels (GPU box): one counter group per
-# rocprofv3 run (FETCH_SIZE and WRITE_SIZE cannot share a pass), then per-kernel TOTALS over every
-# dispatch of the chain (tools/pmc_chain_summary.py). Output: gpurun_out/pmc_chain/
+# PMC passes over the cfg-4 chain's kernels (GPU box): one counter group per rocprofv3 run
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass), then per-kernel TOTALS over the dispatches of the
+# TIMED chain only (the bench line's monotonic window; tools/pmc_chain_summary.py). The bench runs
+# without its checked second pass (--chain-no-check). Output: gpurun_out/pmc_chain/
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 export TMPDIR=/tmp
 OUT="$ROOT/gpurun_out/pmc_chain"
 mkdir -p "$OUT"
-KRE="${KRE:-k_large_}"
-BENCH=(python3 "$ROOT/bench.py" --only chain --chain-inputs "${CHAIN_INPUTS:-4096}" --chain-chunk "${CHAIN_CHUNK:-4096}"
-       --chain-check 0 --chain-ref 0)
+KRE="${KRE:-k_}"
+BENCH=(python3 "$ROOT/bench.py" --only chain --chain-inputs "${CHAIN_INPUTS:-4096}" --chain-chunk "${CHAIN_CHUNK:-1024}"
+       --chain-check 0 --chain-ref 0 --chain-no-check)
 passes=(
   "FETCH_SIZE"
   "WRITE_SIZE"
