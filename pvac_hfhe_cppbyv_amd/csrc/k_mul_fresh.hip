@@ -809,12 +809,8 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
             auto offset = [&](uint32_t tb) {
                 const bool has = tb != kT16;
                 const uint32_t so = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((has ? tb >> 8 : 0u) << 2), (int)segsuf);
-#ifdef PVAC_F3_OFFSET_NB   // A/B: the time word read unconditionally (no exec-masked branch per bin slot)
-                const uint32_t tv = tkey[has ? tb : 0u];
+                const uint32_t tv = tkey[has ? tb : 0u];   // unconditional: no exec-masked branch
                 return has ? (tv >> 16) + so : 0u;
-#else
-                return has ? (tkey[tb] >> 16) + so : 0u;
-#endif
             };
 #pragma unroll
             for (int k = 0; k < KR; ++k) {
@@ -948,12 +944,12 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
             uint64_t* chh = gq->C.w_hi + ceo;
             uint32_t* sp = gq->salt_pos ? gq->salt_pos + ceo : nullptr;
             uint32_t zero = canonical || misc[F3_BIGOVF] ? 1u : 0u;
-#ifdef PVAC_F3_BUFSTORE   // A/B: buffer stores, one 32-bit offset for the three arrays (SGPR bases)
+            // buffer stores: one 32-bit offset for the three arrays (SGPR bases) instead of three
+            // 64-bit address computations per position (round 4: -1.7%, A/B)
             typedef unsigned int u2v __attribute__((ext_vector_type(2)));
             const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(cm, 0, 0x7FFFFFF8, 0x00020000);
             const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(cl, 0, 0x7FFFFFF8, 0x00020000);
             const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(chh, 0, 0x7FFFFFF8, 0x00020000);
-#endif
             for (uint32_t p = tid; p < total && wave != NW - 1; p += BS - 64) {
                 unsigned long long* q = lim + 3u * p;
                 const uint64_t l0 = q[0], l1 = q[1], l2c = q[2];
@@ -968,17 +964,11 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 const uint32_t r = s - lp * Bm;
                 const uint32_t lid = ident ? base + lp : remap[base + lp];
                 // streaming stores: the output is not read again by this kernel (-1%, A/B)
-#ifdef PVAC_F3_BUFSTORE
                 const uint64_t mv = make_meta(lid, r, cell & 1u);
                 const uint32_t bo = p * 8u;   // < 2^31: a pair has <= 2 x 4096 edges
                 __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rm, bo, 0, 2);
                 __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.lo, (uint32_t)(w.lo >> 32)}, rl, bo, 0, 2);
                 __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.hi, (uint32_t)(w.hi >> 32)}, rh, bo, 0, 2);
-#else
-                __builtin_nontemporal_store((unsigned long long)make_meta(lid, r, cell & 1u), (unsigned long long*)cm + p);
-                __builtin_nontemporal_store((unsigned long long)w.lo, (unsigned long long*)cl + p);
-                __builtin_nontemporal_store((unsigned long long)w.hi, (unsigned long long*)chh + p);
-#endif
                 if (sp) sp[p] = p;   // hash order == emit order here
             }
             if (zero) misc[F3_ZERO] = 1u;

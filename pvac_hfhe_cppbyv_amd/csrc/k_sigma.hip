@@ -205,19 +205,17 @@ struct sig_args {
 };
 
 // per-wave LDS: sigma [m_bits/32] | bmX [n_bits/32] | bmN [m_bits/32] | cols [x_col_wt] u16 |
-// midstates [32 edges][2 streams][8] u32
+// noise rows [2 kNoiseWords] u16 | midstates [32 edges][2 streams][8] u32
 // 6 blocks per CU (6 waves per SIMD): the compiler keeps the pass loop within 80 VGPRs without
 // spills instead of hoisting the whole SHA-256 message schedule (149 VGPRs, 3 waves per SIMD)
 constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compression per lane covers
-#ifdef PVAC_SIG_ICOPY
-// A/B build: the delta path flips into four bank-interleaved copies of the image (word W of copy k
-// at dword 4 W + k of the 1024 words sigma | bmX | bmN), copy k = lane & 3, so the 8 lanes of a
-// 32-lane write group that share a copy meet on 8 banks instead of 32 lanes on 32 (expected worst
-// bank 2.3 instead of 3.5 addresses per ds_xor); the noise rows wait in 64 words after the columns
+// The delta path flips into four bank-interleaved copies of the image (word W of copy k at dword
+// 4 W + k of the 1024 words sigma | bmX | bmN, dead after the selection), copy k = lane & 3: the 8
+// lanes of a 32-lane ds_xor group that share a copy meet on 8 banks, instead of 32 lanes on 32
+// (expected busiest bank 2.3 instead of 3.5 addresses per instruction), for one more VALU per flip
+// (round 4: 35.2 -> 30.5 ms per 5.05 M edges, A/B in one process). The noise rows wait in
+// kNoiseWords after the columns and are flipped with them; the output word is the XOR of its copies.
 constexpr uint32_t kNoiseWords = 64;
-#else
-constexpr uint32_t kNoiseWords = 0;
-#endif
 __host__ __device__ constexpr uint32_t sigma_wave_words(uint32_t m_bits, uint32_t n_bits, uint32_t x_col_wt) {
     return ((m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2 + kNoiseWords + 3) & ~3u) + kMidBatch * 2 * 8;
 }
@@ -276,13 +274,8 @@ constexpr uint32_t kDeltaBytes = 208;   // 13 chunks of 16 increments; <= 8 brid
 template <int WV>
 __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0, uint32_t c1) {
     constexpr uint32_t img = WV * kFastWaveWords * 4u;   // byte address of wave WV's image
-#ifdef PVAC_SIG_ICOPY
     uint32_t two = 4u, one = 1u;   // word W of copy k at byte 16 W + 4 k
     const uint32_t kofs = (threadIdx.x & 3u) << 2;
-#else
-    uint32_t two = 2u, one = 1u;
-    constexpr uint32_t kofs = 0;
-#endif
     asm volatile("" : "+v"(two), "+v"(one));   // VGPR operands for the SDWA shifts
     auto word4 = [&](uint32_t& R, uint32_t w) {
 #pragma unroll
@@ -361,10 +354,8 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     const uint64_t words_per_sigma = a.X.sigma_words;
     const uint32_t sub = blockIdx.y * 4 + wave, nsub = a.sub_blocks * 4;
     const bool lds_at0 = (uint32_t)(size_t)(lds_u32*)slds == 0u;   // flip_cols_fast's absolute addresses
-#ifdef PVAC_SIG_ICOPY
     const bool icopy = a.rows_delta && lds_at0;
     uint16_t* nrows = cols + a.x_col_wt;   // kNoiseWords: err_wt <= 128 rows (host-checked)
-#endif
 
     // the salt-independent words of an edge (salt last: it is the only word in both blocks)
     auto edge_words = [&](uint64_t eo, uint64_t lo, uint64_t nl, uint64_t e, uint64_t (&words)[7]) {
@@ -472,9 +463,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                 for (int q = 0; q < 4; ++q) {
                     if (rank[q] >= 0) {
                         if (isX) cols[rank[q]] = (uint16_t)val[q];
-#ifdef PVAC_SIG_ICOPY
                         else if (icopy) nrows[rank[q]] = (uint16_t)val[q];   // flipped with the columns
-#endif
                         else atomicXor(&sig[val[q] >> 5], 1u << (val[q] & 31));   // noise bit
                     }
                 }
@@ -510,7 +499,6 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                     case 2: flip_cols_delta<2>(a.rows_delta, c0, c1); break;
                     default: flip_cols_delta<3>(a.rows_delta, c0, c1); break;
                 }
-#ifdef PVAC_SIG_ICOPY
                 {   // the noise rows, into the lane's copy like the columns
                     const uint32_t kofs = ((uint32_t)lane & 3u) << 2;
                     for (uint32_t q = (uint32_t)lane; q < a.err_wt; q += 64) {
@@ -534,17 +522,6 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) s4[q] = make_uint4(0, 0, 0, 0);
                 }
-#else
-                __builtin_amdgcn_wave_barrier();
-                uint64_t* out = a.X.sigma + e * words_per_sigma;
-                {
-                    uint4* s4 = (uint4*)sig + lane;   // 256 words: one 16-byte store per lane
-                    const uint4 v = *s4;
-                    ((ulonglong2*)out)[lane] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
-                                                               (uint64_t)v.z | ((uint64_t)v.w << 32));
-                    *s4 = make_uint4(0, 0, 0, 0);
-                }
-#endif
                 __builtin_amdgcn_s_setprio(0);
                 continue;
             }

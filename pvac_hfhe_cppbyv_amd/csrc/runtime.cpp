@@ -535,6 +535,37 @@ int pvac_hip_fp_binop(pvac_hip_ctx* c, int op, const uint64_t* a_lo, const uint6
 // ---------------------------------------------------------------- ct_mul
 namespace {
 
+// Whether two key slots of [0, S) share a libstdc++ bucket among nb buckets (std::hash<u64> times the
+// reference's 0x9E3779B97F4A7C15, arithmetic.hpp:72-77). A pair whose slots can share a bucket is not
+// taken in the direct mode (its emit order then needs bucket leaders across A layers): chain step 2
+// (|A.L| = 8, bucket counts near 49 K) has hundreds of such buckets, deeper steps none (the structured
+// keys (lp << 32) | r spread perfectly there). Memoised per (nb, S): chunks of one step repeat them.
+bool slots_share_bucket(uint64_t nb, uint64_t S, uint32_t Bm) {
+    static std::mutex mu;
+    static std::map<std::pair<uint64_t, uint64_t>, bool> memo;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = memo.find({nb, S});
+        if (it != memo.end()) return it->second;
+    }
+    bool shared = false;
+    if (S > nb) {
+        shared = true;
+    } else {
+        std::vector<uint64_t> seen((nb + 63) / 64, 0);
+        for (uint64_t s = 0; s < S && !shared; ++s) {
+            const uint64_t key = ((s / Bm) << 32) | (s % Bm);
+            const uint64_t b = (key * kGolden) % nb;
+            const uint64_t m = 1ull << (b & 63);
+            shared = (seen[b >> 6] & m) != 0;
+            seen[b >> 6] |= m;
+        }
+    }
+    std::lock_guard<std::mutex> g(mu);
+    memo[{nb, S}] = shared;
+    return shared;
+}
+
 // Pairs whose bucket count is at least twice their key-slot space (dense chain steps: reserve(|A.E||B.E|)
 // buckets for |A.L||B.L|B slots) share their bucket groups with every pair of the same bucket count:
 // the group of a slot depends only on (slot, B, bucket count). One static table per distinct bucket
@@ -579,7 +610,8 @@ int plan_static_groups(pvac_hip_ctx* c) {
         if (it == off.end() || d.nbm.d < 2 * d.S || !d.S) continue;
         std::string why;
         large_desc x;
-        rc = build_large_desc(x, d.pair, d.LA, d.LB, d.nA, d.nB, c->prm.B, why, true, !c->large_no_direct);
+        rc = build_large_desc(x, d.pair, d.LA, d.LB, d.nA, d.nB, c->prm.B, why, true,
+                              !c->large_no_direct && !slots_share_bucket(d.nbm.d, d.S, c->prm.B));
         if (rc) return fail(c, rc, why);
         x.g_head = it->second;
         x.g_next = it->second + cfg[d.nbm.d];

@@ -541,7 +541,7 @@ def test_direct_cancelling_key_redo_vs_oracle(oracle):
     from pvac_hfhe_cppbyv_amd import Engine
     B = 337
     rng = np.random.default_rng(0xCA2C)
-    xs = [_mk_layers(rng, [674, 674]) for _ in range(4)]
+    xs = [_mk_layers(rng, [674] * 4) for _ in range(4)]   # 4 A layers: no two key slots share a bucket
     ys = [_mk_layers(rng, [20, 20]) for _ in range(4)]
     x, y = xs[1], ys[1]
     lid = lambda m: int(m & 0xFFFFFFFF)
@@ -569,4 +569,4 @@ def test_direct_cancelling_key_redo_vs_oracle(oracle):
     for p in range(4):
         ref = oracle.ct_mul(xs[p], ys[p], per[p], canon_tag=0xCA2D)
         _same(out[p], ref, view=False)
-    assert out[0].nE == 4 * 337 * 2 and out[1].nE == 4 * 337 * 2 - 1   # saturated: every cell emits but one
+    assert out[0].nE == 8 * 337 * 2 and out[1].nE == 8 * 337 * 2 - 1   # saturated: every cell emits but one
