@@ -202,8 +202,10 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * array of pvac_hip_ct_mul_exec), else splitmix64 words: pvac_hip_fill_random with seed
  * nonce_seed + 97 * first_input + step (step counted from 0).
  * Outputs are streamed: on_chunk(user, first_input, C, stream) receives each chunk's final
- * c_depth (device batch, capacity-padded CSR) valid until it returns; digest_out / count_out
- * (DEVICE, nullable) receive pvac_hip_batch_digest and |E| of c_depth for inputs [0, digest_n).
+ * c_depth (device batch, capacity-padded CSR) valid until it returns; digest_out (DEVICE, nullable)
+ * receives pvac_hip_batch_digest of c_depth for inputs [0, digest_n) (FNV-1a: serial over a cipher's
+ * edges, ~0.2 s for a chunk of depth-8 chains), count_out (DEVICE, nullable) |E| of c_depth for
+ * inputs [0, count_n).
  * PVAC_CHAIN_CHECK_GSUM runs the reference's gsum invariant (pvac_hip_check_mul_gsum) on every pair
  * of every step (needs pvac_hip_ctx_set_powg). A callback's nonzero return stops the chain with
  * PVAC_EINVAL. */
@@ -216,9 +218,10 @@ typedef struct pvac_chain_opts {
     uint64_t nonce_seed;
     uint32_t flags;        /* PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM */
     uint32_t pad;
-    uint64_t digest_n;     /* leading inputs whose final digests / counts are written */
+    uint64_t digest_n;     /* leading inputs whose final digests are written */
     uint64_t* digest_out;  /* DEVICE [digest_n], nullable */
-    uint64_t* count_out;   /* DEVICE [digest_n], nullable */
+    uint64_t count_n;      /* leading inputs whose final edge counts are written */
+    uint64_t* count_out;   /* DEVICE [count_n], nullable */
     int (*fill_nonces)(void* user, uint32_t step, uint64_t first_input, uint64_t n_words, uint64_t* dev_words,
                        void* stream);
     int (*on_chunk)(void* user, uint64_t first_input, const pvac_ct_batch* C, void* stream);

@@ -83,7 +83,8 @@ ON_CHUNK_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.POINTER(CtBatch), C
 class ChainOpts(C.Structure):
     _fields_ = [("depth", C.c_uint32), ("streams", C.c_uint32), ("chunk", C.c_uint64), ("nonce_seed", C.c_uint64),
                 ("flags", C.c_uint32), ("pad", C.c_uint32), ("digest_n", C.c_uint64), ("digest_out", C.c_void_p),
-                ("count_out", C.c_void_p), ("fill_nonces", FILL_NONCES_CB), ("on_chunk", ON_CHUNK_CB),
+                ("count_n", C.c_uint64), ("count_out", C.c_void_p), ("fill_nonces", FILL_NONCES_CB),
+                ("on_chunk", ON_CHUNK_CB),
                 ("user", C.c_void_p)]
 
 
@@ -408,20 +409,23 @@ class Engine:
         return C_
 
     def ct_mul_chain(self, X: DeviceBatch, depth, nonce_seed=0x5EED0040, streams=4, chunk=1024, check_gsum=False,
-                     digest_n=0, canonical=False, fill_nonces=None, on_chunk=None):
+                     digest_n=0, canonical=False, fill_nonces=None, on_chunk=None, count_n=None):
         """c_0 = x, c_k = ct_mul(c_{k-1}, x) to `depth` for every input x of X (tests/test_main.cpp:289-295)
         on `streams` internal worker streams in chunks of `chunk` inputs (pvac_hip_ct_mul_chain).
         Returns a dict of the call's statistics; with digest_n > 0 also the final digests / edge
         counts of inputs [0, digest_n) (numpy u64). fill_nonces / on_chunk: optional ctypes callbacks
-        (FILL_NONCES_CB / ON_CHUNK_CB), called from the library's worker threads."""
+        (FILL_NONCES_CB / ON_CHUNK_CB), called from the library's worker threads. count_n: inputs whose
+        final edge counts are returned (default digest_n; the FNV-1a digest walks a cipher's edges
+        serially, a count is a copy)."""
         torch = self.torch
         dn = min(int(digest_n), X.n)
+        cn = dn if count_n is None else min(int(count_n), X.n)
         dig = torch.zeros(max(dn, 1), dtype=torch.int64, device=self.device)
-        cnt = torch.zeros(max(dn, 1), dtype=torch.int64, device=self.device)
+        cnt = torch.zeros(max(cn, 1), dtype=torch.int64, device=self.device)
         o = ChainOpts(depth=depth, streams=streams, chunk=chunk, nonce_seed=nonce_seed,
                       flags=(CHAIN_CHECK_GSUM if check_gsum else 0) | (MUL_ORDER_CANONICAL if canonical else 0),
                       pad=0, digest_n=dn, digest_out=C.c_void_p(dig.data_ptr()) if dn else None,
-                      count_out=C.c_void_p(cnt.data_ptr()) if dn else None,
+                      count_n=cn, count_out=C.c_void_p(cnt.data_ptr()) if cn else None,
                       fill_nonces=fill_nonces or FILL_NONCES_CB(), on_chunk=on_chunk or ON_CHUNK_CB(), user=None)
         st = ChainStats()
         sx = X.struct()
@@ -431,7 +435,8 @@ class Engine:
                "gsum_failed": st.gsum_failed, "redo": st.redo, "chunks": st.chunks, "seconds": st.seconds}
         if dn:
             res["digests"] = dig[:dn].cpu().numpy().view(np.uint64).copy()
-            res["counts"] = cnt[:dn].cpu().numpy().view(np.uint64).copy()
+        if cn:
+            res["counts"] = cnt[:cn].cpu().numpy().view(np.uint64).copy()
         return res
 
     def ct_mul_redo_count(self):

@@ -323,6 +323,8 @@ struct mul_large_args {
     uint32_t layers_direct;      // k_large_layers: 1 = the direct pairs' pass (before their products),
                                  // 0 = every other pair (after the products)
     uint32_t all_direct;         // every pair is direct: the per-key kernels are not launched
+    uint32_t dir_lb;             // k_large_products_direct: B layers its LDS holds (max |B.L| of the direct pairs)
+    uint32_t pad4;
     uint64_t* redo_ids;          // pairs the host re-runs on the full layout (shared with the fresh kernel)
     unsigned int* redo_cnt;
     // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all

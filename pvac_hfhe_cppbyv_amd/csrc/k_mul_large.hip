@@ -1179,10 +1179,129 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
     }
 }
 
-// Pass 3 of a direct pair (after k_large_scan_direct and the layers pass): k_large_products_la's
-// matrix-core products without any per-key scratch. Each row's folded P / M sums go straight to C's
-// edge records at their emit positions (mx_blocks_n<DIRECT>); a present cell whose sum is 0 flags
-// the pair for the host's redo.
+// Pass 3 of a direct pair (after k_large_scan_direct and the layers pass), one workgroup per
+// (pair, la_per_wg A layers) like k_large_products_la. Per A layer: the matrix-core products of every
+// B layer with each row's folded P / M sums staged in LDS by key slot (no first-insert times: the
+// order is already in the counts and masks of k_large_count_la), then a range writer: the A layer's
+// ranges (its A edges with keys, positions [off(i), off(i) + cnt(i)) of the output) are walked like
+// k_large_write_ranges walks all of them, each position resolved to its key (j DESC, P before M) and
+// its value read from LDS, so C's records are stored range by range, coalesced, with no per-key
+// scratch in HBM. A staged value of 0 at a present cell (products that cancel) flags the pair for
+// the host's redo.
+//
+// LDS: dig1 [2][B] uint4 (one copy per channel: slot (r - idx) mod B with a wrap, 32 B per index) |
+// per B layer: prec | pinf (kMxSparseBytes) | bjt [64] | stg [neB][B][2] (16 B per cell)
+__host__ __device__ inline uint32_t dir_lds_bytes(uint32_t Bm, uint32_t nbl) {
+    return al16(32u * Bm) + nbl * kMxSparseBytes + kIblkBjtBytes + nbl * 32u * Bm;
+}
+
+// the dense side (an A layer) as digits, one copy per channel (k_large_count_la checked for
+// duplicate cells). Barriers inside; every thread calls it.
+template <int BS>
+__device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < 2 * Bm; k += BS) dig[k] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (uint32_t k0 = tid; k0 < D.n; k0 += 2u * BS) {   // two edges per round, loads first
+        edge_rec x[2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const uint32_t k = k0 + (uint32_t)v * BS;
+            x[v] = load_edge(D, k < D.n ? k : 0u);
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            if (k0 + (uint32_t)v * BS >= D.n) break;
+            uint64_t dl, dh;
+            fp_digits8(fp_canon(x[v].lo, x[v].hi), dl, dh);
+            dig[meta_ch(x[v].meta) * Bm + meta_idx(x[v].meta)] =
+                make_uint4((uint32_t)dl, (uint32_t)(dl >> 32), (uint32_t)dh, (uint32_t)(dh >> 32));
+        }
+    }
+    __syncthreads();
+}
+
+// a B layer as the MFMA sparse side (prec as mx_stage_sparse) with pinf = (B - idx, P table base,
+// M table base) for the one-copy dense table; no first-insert shares. Thread k writes edge k.
+__device__ __forceinline__ void dir_stage_sparse(uint4* prec, uint4* pinf, uint32_t Bm, const layer_src& Sd, uint32_t k) {
+    const uint32_t nks = (Sd.n + 1u) >> 1;
+    if (k >= 2u * nks) return;
+    uint4 mid = make_uint4(0, 0, 0, 0);
+    uint4 inf = make_uint4(0, 0, Bm, 0);   // padding edge: zero digits
+    if (k < Sd.n) {
+        const edge_rec x = load_edge(Sd, k);
+        uint64_t dl, dh;
+        fp_digits8(fp_canon(x.lo, x.hi), dl, dh);
+        const uint64_t rl = __builtin_bswap64(dh), rh = __builtin_bswap64(dl);   // digit 15 - x at byte x
+        mid = make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
+        const uint32_t sidx = meta_idx(x.meta), sch = meta_ch(x.meta);
+        inf = make_uint4(Bm - sidx, sch * Bm, (sch ^ 1u) * Bm, 1);
+    }
+    prec[3u * k] = make_uint4(0, 0, 0, 0);
+    prec[3u * k + 1u] = mid;
+    prec[3u * k + 2u] = make_uint4(0, 0, 0, 0);
+    pinf[k] = inf;
+}
+
+// one task's products, each row's P (half 0) / M (half 1) sum into stg[(r) 2 + h]
+template <int BS, int NKS>
+__device__ void dir_rows_n(const uint4* dig, const uint4* prec, const uint4* pinf, uint32_t Bm, ulonglong2* stg) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t h = lane >> 5, n = lane & 31u;
+    mx_v4 frag[NKS];
+    {
+        const uint32_t y0 = 31u - n, sh = y0 & 3u;
+        const uint32_t* pw = (const uint32_t*)prec + (y0 >> 2) + 12u * h;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const uint32_t* q = pw + 24u * (uint32_t)s;
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+            frag[s] = mx_v4{(int)__builtin_amdgcn_alignbyte(w1, w0, sh), (int)__builtin_amdgcn_alignbyte(w2, w1, sh),
+                            (int)__builtin_amdgcn_alignbyte(w3, w2, sh), (int)__builtin_amdgcn_alignbyte(w4, w3, sh)};
+        }
+    }
+    const uint32_t nblk = (Bm + 31u) >> 5;
+    for (uint32_t blk = wave; blk < nblk; blk += BS / 64) {
+        const uint32_t r = blk * 32u + n;
+        const bool live = r < Bm;
+        const uint32_t rr = live ? r : 0u;
+        mx_v16 aP{}, aM{};
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const uint4 in = pinf[2u * (uint32_t)s + h];
+            uint32_t x = rr + in.x;   // (r - idx) mod B
+            x = min(x, x - Bm);
+            const uint4 dp = dig[in.y + x], dm = dig[in.z + x];
+            aP = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dp.x, (int)dp.y, (int)dp.z, (int)dp.w}, aP, 0, 0, 0);
+            aM = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dm.x, (int)dm.y, (int)dm.z, (int)dm.w}, aM, 0, 0, 0);
+        }
+        int64_t paw, pbw, maw, mbw;
+        mx_groups(aP, paw, pbw);
+        mx_groups(aM, maw, mbw);
+        const int64_t ra = shfl_xor64(h ? paw : maw, 32), rb = shfl_xor64(h ? pbw : mbw, 32);
+        const fp v = mx_fold(h ? ra : paw, h ? maw : ra, h ? rb : pbw, h ? mbw : rb);
+        if (live) stg[2u * r + h] = make_ulonglong2(v.lo, v.hi);
+    }
+}
+
+template <int BS>
+__device__ void dir_rows(const uint4* dig, const uint4* prec, const uint4* pinf, uint32_t ns, uint32_t Bm, ulonglong2* stg) {
+    static_assert(kMxKS == 10, "one instantiation per k-step count");
+    switch ((ns + 1u) >> 1) {   // workgroup-uniform
+    case 0: return;
+    case 1: dir_rows_n<BS, 1>(dig, prec, pinf, Bm, stg); return;
+    case 2: dir_rows_n<BS, 2>(dig, prec, pinf, Bm, stg); return;
+    case 3: dir_rows_n<BS, 3>(dig, prec, pinf, Bm, stg); return;
+    case 4: dir_rows_n<BS, 4>(dig, prec, pinf, Bm, stg); return;
+    case 5: dir_rows_n<BS, 5>(dig, prec, pinf, Bm, stg); return;
+    case 6: dir_rows_n<BS, 6>(dig, prec, pinf, Bm, stg); return;
+    case 7: dir_rows_n<BS, 7>(dig, prec, pinf, Bm, stg); return;
+    case 8: dir_rows_n<BS, 8>(dig, prec, pinf, Bm, stg); return;
+    case 9: dir_rows_n<BS, 9>(dig, prec, pinf, Bm, stg); return;
+    default: dir_rows_n<BS, 10>(dig, prec, pinf, Bm, stg); return;
+    }
+}
+
 template <int BS>
 __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
@@ -1191,11 +1310,15 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     uint32_t* S = g.scratch;
     uint32_t* cnt = S + d.o_cnt;
     if (cnt[2] || !cnt[kCntDirect]) return;
-    const uint32_t neA = cnt[0], neB = min(cnt[1], kLaMaxLB);
+    const uint32_t neA = cnt[0], neB = min(cnt[1], g.dir_lb);   // the host sized the LDS for dir_lb B layers
     const uint32_t i0 = blockIdx.x * g.la_per_wg;
     if (i0 >= neA) return;
     const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
-    uint8_t* sreg = plds + g.lds_task;   // per B layer: prec | pinf
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    uint4* dig = (uint4*)plds;
+    uint8_t* sreg = plds + al16(32u * Bm);                             // per B layer: prec | pinf
+    uint32_t* bjt = (uint32_t*)(sreg + g.dir_lb * kMxSparseBytes);     // B edge j: idx | k << 12 | lb << 16
+    ulonglong2* stg = (ulonglong2*)(bjt + 64);                         // [k][B][2]
     uint32_t lbv[kLaMaxLB], nbv[kLaMaxLB];
 #pragma unroll
     for (uint32_t k = 0; k < kLaMaxLB; ++k) {
@@ -1207,38 +1330,89 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
             lbv[k] = lb;
             nbv[k] = srcB.n;   // <= kMxMaxSparse: k_large_count_la checked
             uint4* prec = (uint4*)(sreg + k * kMxSparseBytes);
-            mx_stage_sparse(prec, prec + 3u * kMxMaxSparse, Bm, srcB, 1u, threadIdx.x);
+            dir_stage_sparse(prec, prec + 3u * kMxMaxSparse, Bm, srcB, tid);
         }
     }
-    task_out o{};
-    o.nB = nB;
-    o.nb_m = d.nb_m;
-    o.off = S + d.o_icnt;
-    o.imask = (const ulonglong2*)(S + d.o_imask);
-    o.c_meta = g.C.meta;
-    o.c_lo = g.C.w_lo;
-    o.c_hi = g.C.w_hi;
-    o.salt_pos = g.salt_pos;
-    o.ceo = g.C.e_off[d.pair];
-    o.redo = &cnt[kCntRedo];
-    const uint32_t* remap = S + d.o_used;   // k_large_layers left the remap here
-    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
-    for (uint32_t i = i0; i < i1; ++i) {
-        const uint32_t la = S[d.o_neA + i];
-        const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
-        if (!mx_stage_dense<BS>(plds, Bm, srcA, nB)) {   // cannot happen: k_large_count_la staged it
-            if (threadIdx.x == 0) cnt[kCntRedo] = 1;
-            return;
-        }
+    const uint64_t beo = g.B.e_off[d.pair], aeo = g.A.e_off[d.pair], ceo = g.C.e_off[d.pair];
+    if (tid < nB) {   // published by the dense staging's barriers
+        const uint32_t lb = meta_layer(g.B.meta[beo + tid]);
+        uint32_t kk = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < kLaMaxLB; ++k) {
-            if (k >= neB) continue;
+        for (uint32_t k = 0; k < kLaMaxLB; ++k)
+            if (k < neB && lbv[k] == lb) kk = k;
+        bjt[tid] = meta_idx(g.B.meta[beo + tid]) | kk << 12 | lb << 16;
+    }
+    const uint32_t* off = S + d.o_icnt;   // exclusive suffix offsets (k_large_scan_direct)
+    const ulonglong2* imask = (const ulonglong2*)(S + d.o_imask);
+    const uint32_t* remap = S + d.o_used;  // k_large_layers left the remap here
+    const uint32_t total = cnt[3];
+    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+    for (uint32_t ia = i0; ia < i1; ++ia) {
+        const uint32_t la = S[d.o_neA + ia];
+        const layer_src srcA = side_layer(&g.A, aeo, S, d.o_lstA, LA, la);
+        dir_stage_dense<BS>(dig, Bm, srcA);   // barriers inside (they also publish the B staging)
+        for (uint32_t k = 0; k < neB; ++k) {
             const uint4* prec = (const uint4*)(sreg + k * kMxSparseBytes);
-            const uint32_t lp = la * LB + lbv[k];
-            o.lid = remap[LA + LB + lp];
-            mx_blocks<BS, true>(plds, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, (uint64_t)lp * Bm, o);
+            dir_rows<BS>(dig, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, stg + 2u * Bm * k);
         }
-        __syncthreads();   // the next A layer's staging overwrites the dense tables
+        __syncthreads();
+        // range writer over this A layer's A edges (k_large_write_ranges' resolution)
+        uint32_t lid[kLaMaxLB];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaMaxLB; ++k) lid[k] = k < neB ? remap[LA + LB + la * LB + lbv[k]] : 0u;
+        for (uint32_t b0 = 0; b0 < srcA.n; b0 += BS) {   // workgroup-uniform
+            const uint32_t kq = b0 + tid;
+            const bool lv = kq < srcA.n;
+            const uint32_t e = lv ? srcA.ids[kq] : 0u;
+            const uint32_t oi = lv ? off[e] : 0u;
+            const uint32_t E = lv ? (e ? off[e - 1] : total) - oi : 0u;
+            const ulonglong2 mk = E ? imask[e] : make_ulonglong2(0ull, 0ull);
+            const uint32_t ai = E ? meta_idx(g.A.meta[aeo + e]) : 0u;
+            const uint32_t incl = wave_incl_scan_u32(E);
+            const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+            for (uint32_t q0 = 0; q0 < T; q0 += 64u) {   // wave-uniform
+                const uint32_t q = min(q0 + lane, T - 1u);
+                uint32_t l = 0;
+#pragma unroll
+                for (uint32_t bb = 32; bb; bb >>= 1) {
+                    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l + bb - 1u) << 2), (int)incl);
+                    if (v <= q) l += bb;
+                }
+                l = min(l, 63u);
+                const int bl = (int)(l << 2);
+                const uint32_t il = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)incl) -
+                                    (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)E);
+                const uint64_t mp = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.x) |
+                                    (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.x >> 32)) << 32;
+                const uint64_t mm = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.y) |
+                                    (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.y >> 32)) << 32;
+                const uint32_t aiL = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)ai);
+                const uint32_t oL = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)oi);
+                const uint32_t kk = q - il;   // edge kk of the range
+                uint32_t j = 0;
+#pragma unroll
+                for (uint32_t bb = 32; bb; bb >>= 1) {
+                    const uint32_t y = j + bb;
+                    if ((uint32_t)__popcll(mp >> y) + (uint32_t)__popcll(mm >> y) > kk) j = y;
+                }
+                const uint32_t fa = j == 63u ? 0u : (uint32_t)__popcll(mp >> (j + 1u)) + (uint32_t)__popcll(mm >> (j + 1u));
+                const uint32_t ch = (kk - fa == 0u && ((mp >> j) & 1u)) ? 0u : 1u;   // a key emits P before M
+                const uint32_t bj = bjt[j];
+                const uint32_t kb = (bj >> 12) & 15u;
+                const uint32_t r = mod_small(aiL + (bj & 0xFFFu), Bm);
+                const ulonglong2 w = stg[(kb * Bm + r) * 2u + ch];
+                if (q0 + lane < T) {
+                    if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
+                    const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
+                    const uint64_t pq = ceo + oL + kk;
+                    g.C.meta[pq] = make_meta(lidk, r, ch);
+                    g.C.w_lo[pq] = w.x;
+                    g.C.w_hi[pq] = w.y;
+                    if (g.salt_pos) g.salt_pos[pq] = oL + kk;
+                }
+            }
+        }
+        __syncthreads();   // the next A layer's staging overwrites dig and stg
     }
 }
 
@@ -1850,8 +2024,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
         hipLaunchKernelGGL(k_large_scan_direct, dim3(nl), dim3(kLBig), 0, st, b);
         b.layers_direct = 1;
         hipLaunchKernelGGL(k_large_layers, dim3(nl), dim3(kLBig), (size_t)a.max_lay * 4, st, b);
-        hipLaunchKernelGGL((k_large_products_direct<kLPX>), grid, dim3(kLPX), (size_t)b.lds_task + kLaMaxLB * kMxSparseBytes,
-                           st, b);
+        hipLaunchKernelGGL((k_large_products_direct<kLPX>), grid, dim3(kLPX), (size_t)dir_lds_bytes(a.Bm, a.dir_lb), st, b);
         hipLaunchKernelGGL(k_large_direct_redo, dim3((nl + 63) / 64), dim3(64), 0, st, b);
         if (a.all_direct) return hipGetLastError();
     }

@@ -726,6 +726,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         size_t j = i;
         uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0, mA = 0;
         bool dyn = false, all_ib = true, any_dir = false, all_dir = true;
+        uint32_t mLBd = 0;
         while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
             large_desc& d = c->large_exec[j];
             const uint64_t w = d.words;
@@ -742,6 +743,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             all_ib &= d.iblk != 0;
             any_dir |= d.direct != 0;
             all_dir &= d.direct != 0;
+            if (d.direct) mLBd = std::max<uint32_t>(mLBd, d.LB);
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
         }
@@ -816,6 +818,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.all_iblk = all_ib ? 1u : 0u;
         a.any_direct = any_dir ? 1u : 0u;
         a.all_direct = all_dir ? 1u : 0u;
+        a.dir_lb = std::max<uint32_t>(mLBd, 1u);
         a.redo_ids = c->redo_ids;
         a.redo_cnt = c->redo_cnt;
         a.la_per_wg = la_per_wg;
@@ -1594,12 +1597,14 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
             A = C;
             cur ^= 1;
         }
-        if (o.digest_n > c0 && (o.digest_out || o.count_out)) {
+        if (o.digest_n > c0 && o.digest_out) {
             pvac_ct_batch H = A;
             H.n = std::min<uint64_t>(kk, o.digest_n - c0);
-            if (o.digest_out && !hipchk(launch_batch_digest(H, o.digest_out + c0, k->stream), "digest")) return;
-            if (o.count_out &&
-                !hipchk(hipMemcpyAsync(o.count_out + c0, H.e_cnt, H.n * 8, hipMemcpyDeviceToDevice, k->stream), "counts"))
+            if (!hipchk(launch_batch_digest(H, o.digest_out + c0, k->stream), "digest")) return;
+        }
+        if (o.count_n > c0 && o.count_out) {
+            const uint64_t m = std::min<uint64_t>(kk, o.count_n - c0);
+            if (!hipchk(hipMemcpyAsync(o.count_out + c0, A.e_cnt, m * 8, hipMemcpyDeviceToDevice, k->stream), "counts"))
                 return;
         }
         if (o.on_chunk && o.on_chunk(o.user, c0, &A, (void*)k->stream) != 0) {

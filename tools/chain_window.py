@@ -23,7 +23,8 @@ def main():
             s, e = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
             if s < w0 or s > w1:
                 continue
-            k = row["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+            k = row["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+            k = k.split("(")[0].split("<")[0].split("::")[-1].strip()
             tot[k] += e - s
             cnt[k] += 1
             first = s if first is None else min(first, s)
