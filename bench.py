@@ -552,7 +552,27 @@ def extras(eng, args, with_cpu):
     res["cfg4_chain"] = chain_bench(eng, args)
     res["enc_value"] = enc_bench(eng, args, with_cpu)
     res["ct_mul_host_roundtrip"] = _host_roundtrip()
+    res["ct_mul_single"] = _single_call()
     return res
+
+
+def _single_call(calls=100):
+    """Latency of ONE by-value drop-in call, as the reference's callers make them
+    (tests/test_main.cpp:178-188, :291-292): pvac_hip::ct_mul(pk, A, B) with sigma, host Cipher in
+    and out, on fresh x fresh and on chain-step-3 x fresh (tests/cpp/test_adapter --time-single).
+    Reported next to the reference binary's 108.6 ms per ct_mul; never the headline."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "test_adapter")
+    if not os.path.exists(exe):
+        return None
+    try:
+        outp = subprocess.run([exe, "--time-single", str(calls)], capture_output=True, text=True, timeout=300)
+        r = json.loads([l for l in outp.stdout.splitlines() if l.startswith("{")][-1])
+        r["path"] = "pvac_hip::ct_mul(pk, A, B) with sigma, one call at a time, tests/cpp/test_adapter --time-single"
+        r["reference_ms_per_call"] = 108.6   # BASELINE.md, fresh x fresh with sigma, 1 core
+        return r
+    except Exception as ex:
+        return {"error": repr(ex)}
 
 
 def _host_roundtrip(pairs=1 << 15):

@@ -255,9 +255,10 @@ struct large_desc {
     uint32_t iblk;
     // 1: direct mode (an iblk pair whose scratch holds no per-key sums): k_large_count_la counts the
     // emit positions from key PRESENCE before any multiply, k_large_scan_direct turns the counts into
-    // offsets, and k_large_products_la<DIRECT> writes C's edge records at their positions from the
-    // matrix-core epilogue. A pair that turns out to need more (shared buckets, the canonical order,
-    // a fallback, a key whose products cancel) is left to the host's redo on the full layout
+    // offsets, and k_large_products_direct writes C's edge records at their positions from the
+    // matrix-core sums staged in LDS. A pair that turns out to need more (shared buckets, the
+    // canonical order, a fallback, a key whose products cancel) is left to the host's redo on the
+    // full layout. Its A ids carry the dense cell (k_large_lists)
     uint32_t direct;
     uint32_t pad_d;
     uint64_t nb_m;               // floor(2^32 / |B.E|): t / |B.E| by div_small (k_mul_large.hip)
@@ -294,7 +295,10 @@ struct large_desc {
     uint64_t o_icnt;             // [nA] iblk: edges whose emit time lies in A edge i's product range
                                  // [i |B.E|, (i + 1) |B.E|), then their exclusive suffix offset
     uint64_t o_imask;            // [nA] x 2 u64 iblk: the range's keys with a P edge / an M edge (bit j
-                                 // = B edge j), read by k_large_write_ranges
+                                 // = B edge j), read by k_large_write_ranges; direct pairs: per A layer
+                                 // (slice o_lstA's ids offset) the masks of its writer list
+    uint64_t o_wle;              // direct pairs: [nA] writer lists, A edge | idx << 21 (k_large_count_la)
+    uint64_t o_wln;              // direct pairs: [LA] writer list length per A layer
     uint64_t words;              // end of this pair's scratch (absolute)
 };
 

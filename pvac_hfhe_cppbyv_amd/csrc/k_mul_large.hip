@@ -38,6 +38,28 @@
 #include <cstdlib>
 #include <cstring>
 
+#ifdef PVAC_DIR_STAMPS   // diagnostic build only: k_large_products_direct's wave 0 s_memtime per phase
+__device__ unsigned long long g_dir_stamps[16];
+extern "C" int pvac_hip_diag_dir_stamps(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dir_stamps), sizeof(g_dir_stamps)) != hipSuccess) return -5;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_dir_stamps), z, sizeof(z)) != hipSuccess) return -5;
+    }
+    return 0;
+}
+__device__ __forceinline__ unsigned long long dir_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define DSTAMP(ph) do { const unsigned long long t_ = dir_stamp(); st_acc[ph] += t_ - t_prev; t_prev = t_; } while (0)
+#else
+#define DSTAMP(ph) do {} while (0)
+#endif
+
 namespace pvhip {
 
 namespace {
@@ -162,18 +184,24 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     __syncthreads();
     uint32_t* idsA = S + d.o_lstA + 2 * LA;
     uint32_t* idsB = S + d.o_lstB + 2 * LB;
+    if (d.direct)   // k_large_count_la stores the counts of the A edges whose ranges hold keys only
+        for (uint32_t i = tid; i < nA; i += kLBig) S[d.o_icnt + i] = 0;
+    // direct pairs: an A id carries its dense cell, i | (ch B + idx) << 21 (the host checked
+    // |A.E| < 2^21, B <= 1024), so their passes need no per-edge meta gather
+    const uint32_t dsh = d.direct ? 21u : 32u;
     for (uint32_t i0 = tid; i0 < nA; i0 += 4u * kLBig) {
-        uint32_t la[4];
+        uint64_t m[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = i0 + (uint32_t)u * kLBig;
-            la[u] = i < nA ? meta_layer(g.A.meta[aeo + i]) : 0u;
+            m[u] = i < nA ? g.A.meta[aeo + i] : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = i0 + (uint32_t)u * kLBig;
             if (i >= nA) break;
-            idsA[atomicAdd(&hist[la[u]], 1u)] = i;
+            const uint64_t cell = (uint64_t)(meta_ch(m[u]) * Bm + meta_idx(m[u]));
+            idsA[atomicAdd(&hist[meta_layer(m[u])], 1u)] = i | (uint32_t)((cell << dsh) & 0xFFFFFFFFull);
         }
     }
     for (uint32_t j = tid; j < nB; j += kLBig) {
@@ -255,6 +283,13 @@ constexpr uint64_t kDigC = 0x8080808080808080ull;  // 128 in every byte
 #define PVAC_EXP_MXREP 1
 #endif
 
+// a loaded value kept in a VGPR until here: a uniform load is otherwise moved to an SGPR right
+// after it is issued, and that readfirstlane waits for every load in flight
+__device__ __forceinline__ uint32_t late(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // t = i D + j for D <= 63: m = floor(2^32 / D), i = (t m) >> 32 is i or i - 1
 __device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t D, uint64_t m, uint32_t& j) {
     uint32_t i = (uint32_t)(((uint64_t)t * m) >> 32);
@@ -325,6 +360,10 @@ __device__ __forceinline__ int64_t shfl_xor64(int64_t v, int mask) {
 // digits reversed, 16 zero bytes: W_e's row m is the 16-byte window at 31 - m) and
 // pinf[kMxMaxSparse] (uint4: P and M slot offsets relative to row r, the sparse side's share of t)
 __host__ __device__ inline uint32_t mx_lds_bytes(uint32_t Bm) { return al16(80u * Bm + 4u); }
+// k_large_count_la (no digit tables): M1 / M2 [0, 32 B) | tt [32 B, 48 B) | dup | list length, then
+// the B layers' staging at cnt_lds_bytes (6 workgroups per CU where mx_lds_bytes allowed 4)
+constexpr uint32_t kCntTtOff = 32u;
+__host__ __device__ inline uint32_t cnt_lds_bytes(uint32_t Bm) { return al16((kCntTtOff + 16u) * Bm + 8u); }
 constexpr uint32_t kMxSparseBytes = 64u * kMxMaxSparse;
 constexpr uint32_t kIblkBjtBytes = 4u * 64u;       // k_large_products_la: B edge table of iblk pairs
 
@@ -384,7 +423,7 @@ __device__ __forceinline__ void mx_stage_sparse(uint4* prec, uint4* pinf, uint32
         mid = make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
         const uint32_t sidx = meta_idx(x.meta), sch = meta_ch(x.meta);
         // dense slot of output row r: P (dense channel == sparse channel), M (the other)
-        inf = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, x.e * smul, 1);
+        inf = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, x.e * smul, 0);
     }
     prec[3u * k] = make_uint4(0, 0, 0, 0);
     prec[3u * k + 1u] = mid;
@@ -405,16 +444,6 @@ struct task_out {
     const uint32_t* bjt = nullptr;      // B edge j: idx | ch << 16
     uint32_t nB = 0;
     uint64_t nb_m = 0;
-    // direct mode (large_desc::direct): C's edge records at their emit positions
-    const uint32_t* off = nullptr;      // per A edge i: exclusive suffix offset of its key range
-    const ulonglong2* imask = nullptr;  // per A edge i: keys (bit j) with a P / an M edge
-    uint64_t* c_meta = nullptr;
-    uint64_t* c_lo = nullptr;
-    uint64_t* c_hi = nullptr;
-    uint32_t* salt_pos = nullptr;       // nullable: hash-order index of each output edge
-    uint64_t ceo = 0;                   // the pair's first output edge slot
-    uint32_t lid = 0;                   // the product layer's id after compact_layers
-    uint32_t* redo = nullptr;           // cnt[kCntRedo] of the pair: a key's sum was 0
 };
 constexpr uint32_t kRecKey = 1u << 21, kRecShared = 1u << 20;
 
@@ -424,7 +453,7 @@ constexpr uint32_t kRecKey = 1u << 21, kRecShared = 1u << 20;
 // NKS = k-steps of two sparse edges, a compile-time count: the k-step loop is straight-line code,
 // so every k-step's LDS reads can be issued ahead of the MFMAs (a runtime guard per k-step made
 // each one a basic block of its own: two dependent LDS round trips per k-step)
-template <int BS, int NKS, bool DIRECT>
+template <int BS, int NKS>
 __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* pinf, uint32_t Bm, uint64_t slot0,
                             const task_out& o) {
     const uint4* dig = (const uint4*)lds;
@@ -454,7 +483,6 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
         const uint32_t rr = live ? r : 0u;
         mx_v16 aP{}, aM{};
         uint32_t tmin = kInf;
-        uint32_t presP = 0, presM = 0;   // DIRECT: this half's sparse edges reach the row's P / M cell
         for (int rep_ = 0; rep_ < PVAC_EXP_MXREP; ++rep_) {   // experiment builds repeat the loop
             uint32_t rq = rr;
             asm volatile("" : "+v"(rq));
@@ -474,10 +502,6 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
                 aP = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dp.x, (int)dp.y, (int)dp.z, (int)dp.w}, aP, 0, 0, 0);
                 aM = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dm.x, (int)dm.y, (int)dm.z, (int)dm.w}, aM, 0, 0, 0);
                 tmin = min(tmin, min(__builtin_elementwise_add_sat(tp, in.z), __builtin_elementwise_add_sat(tm, in.z)));
-                if (DIRECT) {
-                    presP |= tp != kInf ? in.w : 0u;   // in.w = 1 for a real sparse edge, 0 for padding
-                    presM |= tm != kInf ? in.w : 0u;
-                }
             }
         }
         MXMARK(3);
@@ -493,31 +517,6 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
         const uint32_t nzo = (uint32_t)__shfl_xor((int)nz, 32);
         const uint32_t eb = h ? (nzo | nz << 1) : (nz | nzo << 1);
         tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, 32));
-        if (DIRECT) {
-            // the key's edges were counted from presence (k_large_count_la): P / M cells with a
-            // product emit. Position = its A edge range's offset + the edges of the range's keys
-            // with a larger B edge j (j DESC, P before M), as k_large_write_ranges orders them
-            presP |= (uint32_t)__shfl_xor((int)presP, 32);
-            presM |= (uint32_t)__shfl_xor((int)presM, 32);
-            const uint32_t mine = h ? presM : presP;
-            if (live && tmin != kInf) {
-                if (mine != nz) *o.redo = 1u;   // a present cell whose products cancel: redo the pair
-                if (mine) {
-                    uint32_t j;
-                    const uint32_t i = div_small(tmin, o.nB, o.nb_m, j);
-                    const ulonglong2 mk = o.imask[i];
-                    const unsigned long long above = (~0ull << (j + 1u)) & ~(1ull << 63);
-                    const uint32_t pos = o.off[i] + (uint32_t)__popcll(mk.x & above) + (uint32_t)__popcll(mk.y & above) +
-                                         (h ? presP : 0u);
-                    const uint64_t q = o.ceo + pos;
-                    o.c_meta[q] = make_meta(o.lid, r, h);
-                    o.c_lo[q] = v.lo;
-                    o.c_hi[q] = v.hi;
-                    if (o.salt_pos) o.salt_pos[q] = pos;
-                }
-            }
-            continue;
-        }
         if (live) {
             const uint64_t s = slot0 + r;
             if (h == 0) o.tkey[s] = tmin;
@@ -547,22 +546,22 @@ __device__ bool mx_blocks_n(const uint8_t* lds, const uint4* prec, const uint4* 
     return any;
 }
 
-template <int BS, bool DIRECT = false>
+template <int BS>
 __device__ bool mx_blocks(const uint8_t* lds, const uint4* prec, const uint4* pinf, uint32_t ns, uint32_t Bm, uint64_t slot0,
                           const task_out& o) {
     static_assert(kMxKS == 10, "one instantiation per k-step count");
     switch ((ns + 1u) >> 1) {   // workgroup-uniform
     case 0: return false;       // no products: the slots keep their initial time
-    case 1: return mx_blocks_n<BS, 1, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 2: return mx_blocks_n<BS, 2, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 3: return mx_blocks_n<BS, 3, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 4: return mx_blocks_n<BS, 4, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 5: return mx_blocks_n<BS, 5, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 6: return mx_blocks_n<BS, 6, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 7: return mx_blocks_n<BS, 7, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 8: return mx_blocks_n<BS, 8, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    case 9: return mx_blocks_n<BS, 9, DIRECT>(lds, prec, pinf, Bm, slot0, o);
-    default: return mx_blocks_n<BS, 10, DIRECT>(lds, prec, pinf, Bm, slot0, o);
+    case 1: return mx_blocks_n<BS, 1>(lds, prec, pinf, Bm, slot0, o);
+    case 2: return mx_blocks_n<BS, 2>(lds, prec, pinf, Bm, slot0, o);
+    case 3: return mx_blocks_n<BS, 3>(lds, prec, pinf, Bm, slot0, o);
+    case 4: return mx_blocks_n<BS, 4>(lds, prec, pinf, Bm, slot0, o);
+    case 5: return mx_blocks_n<BS, 5>(lds, prec, pinf, Bm, slot0, o);
+    case 6: return mx_blocks_n<BS, 6>(lds, prec, pinf, Bm, slot0, o);
+    case 7: return mx_blocks_n<BS, 7>(lds, prec, pinf, Bm, slot0, o);
+    case 8: return mx_blocks_n<BS, 8>(lds, prec, pinf, Bm, slot0, o);
+    case 9: return mx_blocks_n<BS, 9>(lds, prec, pinf, Bm, slot0, o);
+    default: return mx_blocks_n<BS, 10>(lds, prec, pinf, Bm, slot0, o);
     }
 }
 
@@ -797,17 +796,23 @@ __global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
 // bit 63 of M1 = a key of a shared bucket lies in the range (`order` probes it); then icnt[i] and,
 // for ranges with keys, imask[i] = (M1, M2). M1 / M2 use the dense digit table's LDS (dead now), tt
 // maps dense slot d back to its A edge. Barriers inside; every thread calls it.
-template <int BS>
+// LIST (direct pairs, k_large_count_la): the ranges with keys go instead to the A layer's writer list,
+// wl[k] = A edge i | its idx << 21 and imask[k] = (M1, M2) in any order, its length to *wln, so that
+// k_large_products_direct reads one contiguous list per A layer rather than gathering per A edge.
+template <int BS, bool LIST = false>
 __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_desc& d, uint32_t la, uint4 lbq,
-                           uint32_t neB, const uint32_t* recs, uint32_t* icnt, ulonglong2* imask) {
+                           uint32_t neB, const uint32_t* recs, uint32_t* icnt, ulonglong2* imask,
+                           uint32_t* wl = nullptr, uint32_t* wln = nullptr) {
     const uint32_t Bm = g.Bm, nB = d.nB;
     uint32_t* S = g.scratch;
     unsigned long long* M1 = (unsigned long long*)plds;
     unsigned long long* M2 = M1 + 2u * Bm;
-    const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
+    const uint32_t* tt = (const uint32_t*)(plds + (LIST ? kCntTtOff : 64u) * Bm);
     const uint64_t m = d.nb_m;
     const uint32_t tid = threadIdx.x, nk = neB * Bm;
+    uint32_t* wn = (uint32_t*)(plds + (kCntTtOff + 16u) * Bm) + 1;   // LIST: the layer's list length (after dup)
     for (uint32_t k = tid; k < 4u * Bm; k += BS) M1[k] = 0ull;
+    if (LIST && tid == 0) *wn = 0;
     __syncthreads();
     bool shared = false;
     for (uint32_t q = tid; q < nk; q += BS) {
@@ -830,12 +835,23 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         uint32_t j;
         const uint32_t i = div_small(te, nB, m, j);
         const unsigned long long x1 = M1[dd], x2 = M2[dd];
-        icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
+        // (LIST: k_large_lists zeroed the counts, so only ranges with keys store theirs)
+        if (!LIST) icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
         // only ranges that hold keys are read back (write_ranges, order): most A edges of a deep
         // chain step hold none (their keys were all inserted by earlier A edges)
-        if (x1 | x2) imask[i] = make_ulonglong2(x1, x2);
+        if (x1 | x2) {
+            if (LIST) {   // direct pairs: the A layer's writer list (any order), A edge | its idx << 21
+                icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
+                const uint32_t k = atomicAdd(wn, 1u);
+                wl[k] = i | (dd - ch * Bm) << 21;
+                imask[k] = make_ulonglong2(x1, x2);
+            } else {
+                imask[i] = make_ulonglong2(x1, x2);
+            }
+        }
     }
     __syncthreads();   // the next A layer's staging overwrites M1 / M2, tt and recs
+    if (LIST && tid == 0) *wln = *wn;
 }
 
 // ---- direct mode (large_desc::direct) ------------------------------------------------------
@@ -847,31 +863,30 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
 // writer that gathered them is not needed. A key whose sum turns out to be 0 sends the pair to the
 // host's redo (exact path), as the fresh kernel does.
 
-// the dense side's first-insert shares only (no digits): tt[2][2B] at lds + 64 B as mx_stage_dense
-// lays them out (iblk_layer reads them there); false when the layer has duplicate (idx, ch) edges
+// the dense side's first-insert shares only (no digits): tt[2][2B] as mx_stage_dense lays them out,
+// at kCntTtOff (iblk_layer<LIST> reads them there), from the cells in the direct pair's A ids; false
+// when the layer has duplicate (idx, ch) edges
 template <int BS>
 __device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t tmul) {
-    uint32_t* tt = (uint32_t*)(lds + 64u * Bm);
-    uint32_t* dup = (uint32_t*)(lds + 80u * Bm);
+    uint32_t* tt = (uint32_t*)(lds + kCntTtOff * Bm);
+    uint32_t* dup = (uint32_t*)(lds + (kCntTtOff + 16u) * Bm);
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = tid; k < 4 * Bm; k += BS) tt[k] = kInf;
     if (tid == 0) *dup = 0;
     __syncthreads();
     for (uint32_t k0 = tid; k0 < D.n; k0 += 4u * BS) {   // four edges per round, loads first
-        uint64_t m[4];
         uint32_t e[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint32_t k = k0 + (uint32_t)v * BS;
-            e[v] = D.ids[k < D.n ? k : 0u];
+            e[v] = D.ids[k < D.n ? k : 0u];   // direct pairs: A edge | dense cell << 21 (k_large_lists)
         }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) m[v] = D.X->meta[D.eo + e[v]];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             if (k0 + (uint32_t)v * BS >= D.n) break;
-            const uint32_t sl = meta_ch(m[v]) * 2u * Bm + meta_idx(m[v]);
-            const uint32_t te = e[v] * tmul;
+            const uint32_t cell = e[v] >> 21, ch = cell >= Bm ? 1u : 0u;
+            const uint32_t sl = cell + ch * Bm;   // slot ch 2B + idx
+            const uint32_t te = (e[v] & 0x1FFFFFu) * tmul;
             if (atomicCAS(&tt[sl], kInf, te) != kInf) *dup = 1;
             else tt[sl + Bm] = te;
         }
@@ -889,7 +904,7 @@ __device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t
 template <int BS>
 __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
-    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    const large_desc d = g.desc[g.sel[blockIdx.y]];   // registers (the kernel's stores could alias it)
     if (!d.direct) return;
     uint32_t* S = g.scratch;
     uint32_t* cnt = S + d.o_cnt;
@@ -926,11 +941,18 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
         bjt[tid] = meta_idx(mb) | meta_ch(mb) << 16;
     }
     const uint32_t* ghead = group_heads(g, d);
-    const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
+    const uint32_t* tt = (const uint32_t*)(plds + kCntTtOff * Bm);
     const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+#ifdef PVAC_DIR_STAMPS
+    unsigned long long st_acc[4] = {0, 0, 0, 0}, t_prev = dir_stamp();
+#endif
+    const uint64_t aeo = g.A.e_off[d.pair];
+    uint32_t la_nx = S[d.o_neA + i0];   // layer ids one layer ahead
     for (uint32_t i = i0; i < i1; ++i) {
-        const uint32_t la = S[d.o_neA + i];
-        const layer_src srcA = side_layer(&g.A, g.A.e_off[d.pair], S, d.o_lstA, LA, la);
+        DSTAMP(0);
+        const uint32_t la = late(la_nx);
+        const layer_src srcA = side_layer(&g.A, aeo, S, d.o_lstA, LA, la);
+        if (i + 1u < i1) la_nx = S[d.o_neA + i + 1u];
         bool ok = srcA.n >= kLargeDenseMin;
 #pragma unroll
         for (uint32_t k = 0; k < kLaMaxLB; ++k) ok &= k >= neB || (nbv[k] <= kMxMaxSparse && nbv[k] <= srcA.n);
@@ -942,6 +964,7 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             if (tid == 0) atomicExch(&cnt[kCntIFail], 1u);
             return;
         }
+        DSTAMP(1);
         uint32_t usedm = 0;
         for (uint32_t q = tid; q < neB * Bm; q += BS) {
             const uint32_t k = q / Bm, r = q - k * Bm;
@@ -974,9 +997,21 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
         for (uint32_t k = 0; k < kLaMaxLB; ++k)
             if ((usedm >> k) & 1u) S[d.o_used + (LA + LB) + la * LB + lbv[k]] = 1;
         __syncthreads();
-        iblk_layer<BS>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, recs, S + d.o_icnt,
-                       (ulonglong2*)(S + d.o_imask));
+        DSTAMP(2);
+        const uint32_t lbase = S[d.o_lstA + la];   // the layer's list slice: as its edge ids
+        iblk_layer<BS, true>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, recs, S + d.o_icnt,
+                             (ulonglong2*)(S + d.o_imask) + lbase, S + d.o_wle + lbase, S + d.o_wln + la);
+        DSTAMP(3);
+#ifdef PVAC_DIR_STAMPS
+        if (tid == 0) atomicAdd(&g_dir_stamps[13], (unsigned long long)S[d.o_wln + la]);
+#endif
     }
+#ifdef PVAC_DIR_STAMPS
+    if (tid == 0) {
+        for (int p = 0; p < 4; ++p) atomicAdd(&g_dir_stamps[8 + p], st_acc[p]);
+        atomicAdd(&g_dir_stamps[12], (unsigned long long)(i1 - i0));
+    }
+#endif
 }
 
 // Pass 2 of a direct pair, one workgroup per pair: the total, the guard_budget decision, and the
@@ -1191,32 +1226,47 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
 //
 // LDS: dig1 [2][B] uint4 (one copy per channel: slot (r - idx) mod B with a wrap, 32 B per index) |
 // per B layer: prec | pinf (kMxSparseBytes) | bjt [64] | stg [neB][B][2] (16 B per cell)
+__host__ __device__ inline uint32_t dir_lds_base(uint32_t Bm) {   // the digit table, reused by the writer
+    return al16(max(32u * Bm, 16u * Bm + 8u * 256u + 64u));   // okey [8 B] u16 | obase, oidx [256] | part
+}
 __host__ __device__ inline uint32_t dir_lds_bytes(uint32_t Bm, uint32_t nbl) {
-    return al16(32u * Bm) + nbl * kMxSparseBytes + kIblkBjtBytes + nbl * 32u * Bm;
+    return dir_lds_base(Bm) + nbl * kMxSparseBytes + kIblkBjtBytes + nbl * 32u * Bm;
 }
 
 // the dense side (an A layer) as digits, one copy per channel (k_large_count_la checked for
 // duplicate cells). Barriers inside; every thread calls it.
 template <int BS>
 __device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D) {
+    constexpr uint32_t kV = 3;   // a dense A layer (<= 2 B = 674 edges) in one round of loads
     const uint32_t tid = threadIdx.x;
+    uint32_t c[kV];
+    uint64_t lo[kV], hi[kV];
+    auto load = [&](uint32_t k0) {   // direct pairs' A ids: A edge | dense cell << 21 (k_large_lists)
+#pragma unroll
+        for (uint32_t v = 0; v < kV; ++v) {
+            const uint32_t k = k0 + v * BS;
+            const uint32_t id = D.ids[k < D.n ? k : 0u];   // D.n >= kLargeDenseMin
+            c[v] = id >> 21;
+            lo[v] = D.X->w_lo[D.eo + (id & 0x1FFFFFu)];
+            hi[v] = D.X->w_hi[D.eo + (id & 0x1FFFFFu)];
+        }
+    };
+    auto put = [&](uint32_t k0) {
+#pragma unroll
+        for (uint32_t v = 0; v < kV; ++v) {
+            if (k0 + v * BS >= D.n) break;
+            uint64_t dl, dh;
+            fp_digits8(fp_canon(lo[v], hi[v]), dl, dh);
+            dig[c[v]] = make_uint4((uint32_t)dl, (uint32_t)(dl >> 32), (uint32_t)dh, (uint32_t)(dh >> 32));
+        }
+    };
+    load(tid);   // in flight across the zero fill and its barrier
     for (uint32_t k = tid; k < 2 * Bm; k += BS) dig[k] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    for (uint32_t k0 = tid; k0 < D.n; k0 += 2u * BS) {   // two edges per round, loads first
-        edge_rec x[2];
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            const uint32_t k = k0 + (uint32_t)v * BS;
-            x[v] = load_edge(D, k < D.n ? k : 0u);
-        }
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            if (k0 + (uint32_t)v * BS >= D.n) break;
-            uint64_t dl, dh;
-            fp_digits8(fp_canon(x[v].lo, x[v].hi), dl, dh);
-            dig[meta_ch(x[v].meta) * Bm + meta_idx(x[v].meta)] =
-                make_uint4((uint32_t)dl, (uint32_t)(dl >> 32), (uint32_t)dh, (uint32_t)(dh >> 32));
-        }
+    put(tid);
+    for (uint32_t k0 = tid + kV * BS; k0 < D.n; k0 += kV * BS) {
+        load(k0);
+        put(k0);
     }
     __syncthreads();
 }
@@ -1235,7 +1285,7 @@ __device__ __forceinline__ void dir_stage_sparse(uint4* prec, uint4* pinf, uint3
         const uint64_t rl = __builtin_bswap64(dh), rh = __builtin_bswap64(dl);   // digit 15 - x at byte x
         mid = make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
         const uint32_t sidx = meta_idx(x.meta), sch = meta_ch(x.meta);
-        inf = make_uint4(Bm - sidx, sch * Bm, (sch ^ 1u) * Bm, 1);
+        inf = make_uint4(Bm - sidx, sch * Bm, (sch ^ 1u) * Bm, 0);
     }
     prec[3u * k] = make_uint4(0, 0, 0, 0);
     prec[3u * k + 1u] = mid;
@@ -1305,7 +1355,9 @@ __device__ void dir_rows(const uint4* dig, const uint4* prec, const uint4* pinf,
 template <int BS>
 __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
-    const large_desc& d = g.desc[g.sel[blockIdx.y]];
+    // a register copy of the descriptor: C's stores could alias it, so field reads through the
+    // reference were reloaded from memory (a dependent round trip each) after every store
+    const large_desc d = g.desc[g.sel[blockIdx.y]];
     if (!d.direct) return;
     uint32_t* S = g.scratch;
     uint32_t* cnt = S + d.o_cnt;
@@ -1314,9 +1366,13 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     const uint32_t i0 = blockIdx.x * g.la_per_wg;
     if (i0 >= neA) return;
     const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    static_assert(BS <= 256, "dir_lds_base holds the writer's per-entry words for 256 entries");
+    const uint32_t tid = threadIdx.x;
+#ifdef PVAC_DIR_STAMPS
+    unsigned long long st_acc[4] = {0, 0, 0, 0}, t_prev = dir_stamp();
+#endif
     uint4* dig = (uint4*)plds;
-    uint8_t* sreg = plds + al16(32u * Bm);                             // per B layer: prec | pinf
+    uint8_t* sreg = plds + dir_lds_base(Bm);                           // per B layer: prec | pinf
     uint32_t* bjt = (uint32_t*)(sreg + g.dir_lb * kMxSparseBytes);     // B edge j: idx | k << 12 | lb << 16
     ulonglong2* stg = (ulonglong2*)(bjt + 64);                         // [k][B][2]
     uint32_t lbv[kLaMaxLB], nbv[kLaMaxLB];
@@ -1343,77 +1399,105 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
         bjt[tid] = meta_idx(g.B.meta[beo + tid]) | kk << 12 | lb << 16;
     }
     const uint32_t* off = S + d.o_icnt;   // exclusive suffix offsets (k_large_scan_direct)
-    const ulonglong2* imask = (const ulonglong2*)(S + d.o_imask);
-    const uint32_t* remap = S + d.o_used;  // k_large_layers left the remap here
-    const uint32_t total = cnt[3];
+    const ulonglong2* wlm = (const ulonglong2*)(S + d.o_imask);   // writer lists (k_large_count_la)
+    const uint32_t* wle = S + d.o_wle;
+    const uint32_t* remap = S + d.o_used;  // k_large_layers left the remap here (k_large_layers ran before)
     const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+    // layer headers one layer ahead: the next layer's id loads during this layer's staging, its
+    // list range and writer-list length during this layer's writer
+    uint32_t la = S[d.o_neA + i0];
+    uint32_t a_start = S[d.o_lstA + la], a_n = S[d.o_lstA + LA + la], a_nw = S[d.o_wln + la];
     for (uint32_t ia = i0; ia < i1; ++ia) {
-        const uint32_t la = S[d.o_neA + ia];
-        const layer_src srcA = side_layer(&g.A, aeo, S, d.o_lstA, LA, la);
+        const layer_src srcA{&g.A, aeo, S + d.o_lstA + 2u * LA + a_start, a_n};
+        uint32_t lid[kLaMaxLB];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaMaxLB; ++k) lid[k] = k < neB ? remap[LA + LB + la * LB + lbv[k]] : 0u;
+        const uint32_t la_nx = ia + 1u < i1 ? S[d.o_neA + ia + 1u] : 0u;
+        DSTAMP(0);
         dir_stage_dense<BS>(dig, Bm, srcA);   // barriers inside (they also publish the B staging)
+        DSTAMP(1);
         for (uint32_t k = 0; k < neB; ++k) {
             const uint4* prec = (const uint4*)(sreg + k * kMxSparseBytes);
             dir_rows<BS>(dig, prec, prec + 3u * kMxMaxSparse, nbv[k], Bm, stg + 2u * Bm * k);
         }
         __syncthreads();
-        // range writer over this A layer's A edges (k_large_write_ranges' resolution)
-        uint32_t lid[kLaMaxLB];
-#pragma unroll
-        for (uint32_t k = 0; k < kLaMaxLB; ++k) lid[k] = k < neB ? remap[LA + LB + la * LB + lbv[k]] : 0u;
-        for (uint32_t b0 = 0; b0 < srcA.n; b0 += BS) {   // workgroup-uniform
+        DSTAMP(2);
+        // writer: the A layer's list (its A edges with keys, contiguous; one offset gather each), a
+        // round of up to BS list entries at a time. Each entry's thread expands its range's keys in
+        // emit order (j DESC, P before M at one j) into okey[excl + kk] (the dead digit table), then
+        // every thread takes output slots q = tid, tid + BS, ... of the round: balanced across the
+        // waves, stores coalesced within each range, no search.
+        const uint32_t lx = late(la_nx);
+        uint32_t st_nx = 0, n_nx = 0, nw_nx = 0;
+        if (ia + 1u < i1) {   // workgroup-uniform
+            st_nx = S[d.o_lstA + lx];
+            n_nx = S[d.o_lstA + LA + lx];
+            nw_nx = S[d.o_wln + lx];
+        }
+        const uint32_t lbase = a_start, nw = a_nw;
+        uint16_t* okey = (uint16_t*)dig;                       // [<= 8 B] j | ch << 6 | entry << 7
+        uint32_t* obase = (uint32_t*)(plds + 16u * Bm);        // [BS] position base: off(i) - excl
+        uint32_t* oidx = obase + BS;                           // [BS] the entry's A idx
+        uint32_t* part = oidx + BS;                            // [BS / 64] scan partials
+        for (uint32_t b0 = 0; b0 < nw; b0 += BS) {   // workgroup-uniform
             const uint32_t kq = b0 + tid;
-            const bool lv = kq < srcA.n;
-            const uint32_t e = lv ? srcA.ids[kq] : 0u;
+            const bool lv = kq < nw;
+            const uint32_t we = lv ? wle[lbase + kq] : 0u;
+            const ulonglong2 mk = lv ? wlm[lbase + kq] : make_ulonglong2(0ull, 0ull);
+            const uint32_t e = we & 0x1FFFFFu;
             const uint32_t oi = lv ? off[e] : 0u;
-            const uint32_t E = lv ? (e ? off[e - 1] : total) - oi : 0u;
-            const ulonglong2 mk = E ? imask[e] : make_ulonglong2(0ull, 0ull);
-            const uint32_t ai = E ? meta_idx(g.A.meta[aeo + e]) : 0u;
-            const uint32_t incl = wave_incl_scan_u32(E);
-            const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-            for (uint32_t q0 = 0; q0 < T; q0 += 64u) {   // wave-uniform
-                const uint32_t q = min(q0 + lane, T - 1u);
-                uint32_t l = 0;
-#pragma unroll
-                for (uint32_t bb = 32; bb; bb >>= 1) {
-                    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l + bb - 1u) << 2), (int)incl);
-                    if (v <= q) l += bb;
+            uint64_t mp = mk.x & ~(1ull << 63), mm = mk.y;   // bit 63: a shared bucket (such pairs are redone)
+            uint32_t T;
+            const uint32_t excl = wg_exclusive_scan<BS>((uint32_t)__popcll(mp) + (uint32_t)__popcll(mm), part, T);
+            obase[tid] = oi - excl;
+            oidx[tid] = we >> 21;
+            uint32_t o = excl;
+            while (mp | mm) {
+                const uint32_t jp = mp ? 63u - (uint32_t)__clzll(mp) : 0u, jm = mm ? 63u - (uint32_t)__clzll(mm) : 0u;
+                const uint32_t jj = mp ? (mm ? max(jp, jm) : jp) : jm;
+                const uint64_t bit = 1ull << jj;
+                if (mp & bit) {
+                    okey[o++] = (uint16_t)(jj | tid << 7);
+                    mp ^= bit;
                 }
-                l = min(l, 63u);
-                const int bl = (int)(l << 2);
-                const uint32_t il = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)incl) -
-                                    (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)E);
-                const uint64_t mp = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.x) |
-                                    (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.x >> 32)) << 32;
-                const uint64_t mm = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)mk.y) |
-                                    (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)(uint32_t)(mk.y >> 32)) << 32;
-                const uint32_t aiL = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)ai);
-                const uint32_t oL = (uint32_t)__builtin_amdgcn_ds_bpermute(bl, (int)oi);
-                const uint32_t kk = q - il;   // edge kk of the range
-                uint32_t j = 0;
-#pragma unroll
-                for (uint32_t bb = 32; bb; bb >>= 1) {
-                    const uint32_t y = j + bb;
-                    if ((uint32_t)__popcll(mp >> y) + (uint32_t)__popcll(mm >> y) > kk) j = y;
-                }
-                const uint32_t fa = j == 63u ? 0u : (uint32_t)__popcll(mp >> (j + 1u)) + (uint32_t)__popcll(mm >> (j + 1u));
-                const uint32_t ch = (kk - fa == 0u && ((mp >> j) & 1u)) ? 0u : 1u;   // a key emits P before M
-                const uint32_t bj = bjt[j];
-                const uint32_t kb = (bj >> 12) & 15u;
-                const uint32_t r = mod_small(aiL + (bj & 0xFFFu), Bm);
-                const ulonglong2 w = stg[(kb * Bm + r) * 2u + ch];
-                if (q0 + lane < T) {
-                    if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
-                    const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
-                    const uint64_t pq = ceo + oL + kk;
-                    g.C.meta[pq] = make_meta(lidk, r, ch);
-                    g.C.w_lo[pq] = w.x;
-                    g.C.w_hi[pq] = w.y;
-                    if (g.salt_pos) g.salt_pos[pq] = oL + kk;
+                if (mm & bit) {
+                    okey[o++] = (uint16_t)(jj | 64u | tid << 7);
+                    mm ^= bit;
                 }
             }
+            __syncthreads();
+            for (uint32_t q = tid; q < T; q += BS) {
+                const uint32_t v = okey[q];
+                const uint32_t l = v >> 7, jj = v & 63u, ch = (v >> 6) & 1u;
+                const uint32_t bj = bjt[jj];
+                const uint32_t kb = (bj >> 12) & 15u;
+                const uint32_t r = mod_small(oidx[l] + (bj & 0xFFFu), Bm);
+                const ulonglong2 w = stg[(kb * Bm + r) * 2u + ch];
+                if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
+                const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
+                const uint32_t pos = obase[l] + q;
+                const uint64_t pq = ceo + pos;
+                g.C.meta[pq] = make_meta(lidk, r, ch);
+                g.C.w_lo[pq] = w.x;
+                g.C.w_hi[pq] = w.y;
+                if (g.salt_pos) g.salt_pos[pq] = pos;
+            }
+            if (b0 + BS < nw) __syncthreads();   // the next round rewrites okey / obase
         }
         __syncthreads();   // the next A layer's staging overwrites dig and stg
+        DSTAMP(3);
+        la = lx;
+        a_start = late(st_nx);
+        a_n = late(n_nx);
+        a_nw = late(nw_nx);
     }
+#ifdef PVAC_DIR_STAMPS
+    if (tid == 0) {
+        for (int p = 0; p < 4; ++p) atomicAdd(&g_dir_stamps[p], st_acc[p]);
+        atomicAdd(&g_dir_stamps[4], (unsigned long long)(i1 - i0));
+        atomicAdd(&g_dir_stamps[5], 1ull);
+    }
+#endif
 }
 
 // the column-mode tasks k_large_products_la deferred: kDeferWG workgroups per pair walk its list
@@ -2017,7 +2101,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     if (a.any_direct && a.n_la && a.max_la_wg) {
         // direct pairs: presence counts, offsets, compact_layers, then products straight to C
         mul_large_args b = a;
-        b.lds_task = mx_lds_bytes(a.Bm);
+        b.lds_task = cnt_lds_bytes(a.Bm);
         const dim3 grid((unsigned)a.max_la_wg, a.n_la);
         hipLaunchKernelGGL((k_large_count_la<kLPX>), grid, dim3(kLPX),
                            (size_t)b.lds_task + kLaMaxLB * kMxMaxSparse * 16u + kIblkBjtBytes + kLaMaxLB * 4u * a.Bm, st, b);

@@ -302,7 +302,8 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     d.g_head = d.g_next = kNoGrp;
     // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
     d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
-    d.direct = d.iblk && allow_direct && PVAC_LARGE_DIRECT ? 1u : 0u;
+    // (direct A ids and writer lists pack an A edge with its dense cell: A edges < 2^21, 2 B <= 2^11)
+    d.direct = d.iblk && allow_direct && PVAC_LARGE_DIRECT && nA < (1ull << 21) && Bm <= 1024u ? 1u : 0u;
     d.nb_m = nB ? (1ull << 32) / nB : 0;
     uint64_t o = 0;
     auto even = [&]() { o = (o + 1) & ~1ull; };
@@ -323,6 +324,8 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
         d.o_neB = o; o += LB;
         d.o_defer = d.o_info = d.o_sums = d.o_nxt = d.o_tb = d.o_within = d.o_etot = d.o_cpos = d.o_order = d.o_hpos = o;
         d.o_icnt = o; o += nA;
+        d.o_wle = o; o += nA;
+        d.o_wln = o; o += LA;
         quad();
         d.o_imask = o; o += 4 * nA;
         quad();
@@ -360,6 +363,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     quad();
     d.o_imask = o; o += d.iblk ? 4 * nA : 0;
     quad();
+    d.o_wle = d.o_wln = o;
     d.words = o;
     return PVAC_OK;
 }
@@ -367,7 +371,8 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
 void rebase_desc(large_desc& d, uint64_t base) {
     uint64_t* f[] = {&d.o_zero, &d.o_cnt, &d.o_hkey, &d.o_hhead, &d.o_bmask, &d.o_bcnt, &d.o_used, &d.o_tkey,
                      &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_defer, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
-                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos, &d.o_icnt, &d.o_imask};
+                     &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos, &d.o_icnt, &d.o_imask,
+                     &d.o_wle, &d.o_wln};
     for (uint64_t* p : f) *p += base;
 }
 
