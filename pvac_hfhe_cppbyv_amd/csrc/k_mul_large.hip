@@ -867,19 +867,19 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
 // at kCntTtOff (iblk_layer<LIST> reads them there), from the cells in the direct pair's A ids; false
 // when the layer has duplicate (idx, ch) edges
 template <int BS>
-__device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t tmul) {
+__device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t tmul, const uint32_t (&pre)[4]) {
     uint32_t* tt = (uint32_t*)(lds + kCntTtOff * Bm);
     uint32_t* dup = (uint32_t*)(lds + (kCntTtOff + 16u) * Bm);
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = tid; k < 4 * Bm; k += BS) tt[k] = kInf;
     if (tid == 0) *dup = 0;
     __syncthreads();
-    for (uint32_t k0 = tid; k0 < D.n; k0 += 4u * BS) {   // four edges per round, loads first
+    for (uint32_t k0 = tid; k0 < D.n; k0 += 4u * BS) {   // four edges per round (the first: loaded ahead)
         uint32_t e[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint32_t k = k0 + (uint32_t)v * BS;
-            e[v] = D.ids[k < D.n ? k : 0u];   // direct pairs: A edge | dense cell << 21 (k_large_lists)
+            e[v] = k0 == tid ? pre[v] : D.ids[k < D.n ? k : 0u];   // A edge | dense cell << 21 (k_large_lists)
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -928,11 +928,16 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             const layer_src srcB = side_layer(&g.B, g.B.e_off[d.pair], S, d.o_lstB, LB, lb);
             lbv[k] = lb;
             nbv[k] = srcB.n;   // <= kIblkMaxSparse (k_large_lists failed the pair otherwise)
-            if (tid < srcB.n && srcB.n <= kMxMaxSparse) {
-                const uint32_t e = srcB.ids[tid];
-                const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + e];
-                const uint32_t sidx = meta_idx(mb), sch = meta_ch(mb);
-                sp[k * kMxMaxSparse + tid] = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, e, 0);
+            if (tid < ((srcB.n + 3u) & ~3u) && srcB.n <= kMxMaxSparse) {
+                // (P slot offset, M slot offset, j, 1); padding to a multiple of 4: (0, 0, INF, 0)
+                uint4 v = make_uint4(0, 0, kInf, 0);
+                if (tid < srcB.n) {
+                    const uint32_t e = srcB.ids[tid];
+                    const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + e];
+                    const uint32_t sidx = meta_idx(mb), sch = meta_ch(mb);
+                    v = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, e, 1);
+                }
+                sp[k * kMxMaxSparse + tid] = v;
             }
         }
     }
@@ -940,19 +945,30 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
         const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + tid];
         bjt[tid] = meta_idx(mb) | meta_ch(mb) << 16;
     }
-    const uint32_t* ghead = group_heads(g, d);
     const uint32_t* tt = (const uint32_t*)(plds + kCntTtOff * Bm);
     const uint32_t i1 = min(neA, i0 + g.la_per_wg);
 #ifdef PVAC_DIR_STAMPS
     unsigned long long st_acc[4] = {0, 0, 0, 0}, t_prev = dir_stamp();
 #endif
-    const uint64_t aeo = g.A.e_off[d.pair];
-    uint32_t la_nx = S[d.o_neA + i0];   // layer ids one layer ahead
+    // layers one ahead: the next layer's list range loads during this layer's keys, its first 4 BS
+    // ids during iblk_layer, so stage_tt starts from registers
+    const uint32_t* idsA = S + d.o_lstA + 2u * LA;
+    uint32_t pre[4];
+    auto load_ids = [&](uint32_t st, uint32_t n) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint32_t k = tid + (uint32_t)v * BS;
+            pre[v] = idsA[st + (k < n ? k : 0u)];
+        }
+    };
+    uint32_t la_c = S[d.o_neA + i0];
+    uint32_t st_c = S[d.o_lstA + la_c], n_c = S[d.o_lstA + LA + la_c];
+    load_ids(st_c, n_c);
+    uint32_t la_n = i0 + 1u < i1 ? S[d.o_neA + i0 + 1u] : 0u;
     for (uint32_t i = i0; i < i1; ++i) {
         DSTAMP(0);
-        const uint32_t la = late(la_nx);
-        const layer_src srcA = side_layer(&g.A, aeo, S, d.o_lstA, LA, la);
-        if (i + 1u < i1) la_nx = S[d.o_neA + i + 1u];
+        const uint32_t la = late(la_c);
+        const layer_src srcA{&g.A, 0, idsA + late(st_c), late(n_c)};
         bool ok = srcA.n >= kLargeDenseMin;
 #pragma unroll
         for (uint32_t k = 0; k < kLaMaxLB; ++k) ok &= k >= neB || (nbv[k] <= kMxMaxSparse && nbv[k] <= srcA.n);
@@ -960,34 +976,51 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             if (tid == 0) atomicExch(&cnt[kCntIFail], 1u);
             return;
         }
-        if (!stage_tt<BS>(plds, Bm, srcA, nB)) {
+        if (!stage_tt<BS>(plds, Bm, srcA, nB, pre)) {
             if (tid == 0) atomicExch(&cnt[kCntIFail], 1u);
             return;
         }
         DSTAMP(1);
+        const uint32_t lx = late(la_n);
+        uint32_t st_n = 0, n_n = 0;
+        if (i + 1u < i1) {   // workgroup-uniform
+            st_n = S[d.o_lstA + lx];
+            n_n = S[d.o_lstA + LA + lx];
+        }
         uint32_t usedm = 0;
         for (uint32_t q = tid; q < neB * Bm; q += BS) {
             const uint32_t k = q / Bm, r = q - k * Bm;
             const uint4* e = sp + k * kMxMaxSparse;
             uint32_t tmin = kInf, pp = 0, pm = 0;
-            for (uint32_t x = 0; x < nbv[k]; ++x) {
-                const uint4 in = e[x];
-                const uint32_t tp = tt[in.x + r], tm = tt[in.y + r];
-                pp |= tp != kInf ? 1u : 0u;
-                pm |= tm != kInf ? 1u : 0u;
-                tmin = min(tmin, min(__builtin_elementwise_add_sat(tp, in.z), __builtin_elementwise_add_sat(tm, in.z)));
+            // four sparse edges per step (padded lists): their LDS reads in flight together
+            for (uint32_t x = 0; x < nbv[k]; x += 4) {
+                uint4 in[4];
+                uint32_t tp[4], tm[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) in[u] = e[x + u];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    tp[u] = tt[in[u].x + r];
+                    tm[u] = tt[in[u].y + r];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    pp |= tp[u] != kInf ? in[u].w : 0u;
+                    pm |= tm[u] != kInf ? in[u].w : 0u;
+                    tmin = min(tmin, min(__builtin_elementwise_add_sat(tp[u], in[u].z),
+                                         __builtin_elementwise_add_sat(tm[u], in[u].z)));
+                }
             }
             uint32_t rv = 0;
             if (tmin != kInf) {
                 const uint32_t eb = pp | pm << 1;
-                const uint64_t s = (uint64_t)(la * LB + lbv[k]) * Bm + r;
-                const bool shared = ghead && ghead[s] != 0u;
+                // no shared buckets in a direct pair (the host's slots_share_bucket check)
                 uint32_t j;
                 const uint32_t ia = div_small(tmin, nB, d.nb_m, j);
                 const uint32_t ij = bjt[j] & 0xFFFFu;
                 const uint32_t xx = r >= ij ? r - ij : r + Bm - ij;
                 const uint32_t dd = tt[xx] == ia * nB ? xx : Bm + xx;
-                rv = dd | j << 12 | eb << 18 | (shared ? kRecShared : 0u) | kRecKey;
+                rv = dd | j << 12 | eb << 18 | kRecKey;
                 usedm |= 1u << k;
             }
             recs[k * Bm + r] = rv;
@@ -998,13 +1031,22 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             if ((usedm >> k) & 1u) S[d.o_used + (LA + LB) + la * LB + lbv[k]] = 1;
         __syncthreads();
         DSTAMP(2);
-        const uint32_t lbase = S[d.o_lstA + la];   // the layer's list slice: as its edge ids
+        uint32_t la_n2 = 0;
+        if (i + 1u < i1) {
+            load_ids(late(st_n), late(n_n));
+            if (i + 2u < i1) la_n2 = S[d.o_neA + i + 2u];
+        }
+        const uint32_t lbase = late(st_c);   // the layer's list slice: as its edge ids
         iblk_layer<BS, true>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, recs, S + d.o_icnt,
                              (ulonglong2*)(S + d.o_imask) + lbase, S + d.o_wle + lbase, S + d.o_wln + la);
         DSTAMP(3);
 #ifdef PVAC_DIR_STAMPS
         if (tid == 0) atomicAdd(&g_dir_stamps[13], (unsigned long long)S[d.o_wln + la]);
 #endif
+        la_c = lx;
+        st_c = st_n;
+        n_c = n_n;
+        la_n = la_n2;
     }
 #ifdef PVAC_DIR_STAMPS
     if (tid == 0) {
@@ -1227,7 +1269,8 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_la(mul_larg
 // LDS: dig1 [2][B] uint4 (one copy per channel: slot (r - idx) mod B with a wrap, 32 B per index) |
 // per B layer: prec | pinf (kMxSparseBytes) | bjt [64] | stg [neB][B][2] (16 B per cell)
 __host__ __device__ inline uint32_t dir_lds_base(uint32_t Bm) {   // the digit table, reused by the writer
-    return al16(max(32u * Bm, 16u * Bm + 8u * 256u + 64u));   // okey [8 B] u16 | obase, oidx [256] | part
+    // okey [8 B] u16 | obase, oidx, oexc [256] u32 | omk [256] 16 B | part
+    return al16(max(32u * Bm, 16u * Bm + 28u * 256u + 64u));
 }
 __host__ __device__ inline uint32_t dir_lds_bytes(uint32_t Bm, uint32_t nbl) {
     return dir_lds_base(Bm) + nbl * kMxSparseBytes + kIblkBjtBytes + nbl * 32u * Bm;
@@ -1438,7 +1481,10 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
         uint16_t* okey = (uint16_t*)dig;                       // [<= 8 B] j | ch << 6 | entry << 7
         uint32_t* obase = (uint32_t*)(plds + 16u * Bm);        // [BS] position base: off(i) - excl
         uint32_t* oidx = obase + BS;                           // [BS] the entry's A idx
-        uint32_t* part = oidx + BS;                            // [BS / 64] scan partials
+        uint32_t* oexc = oidx + BS;                            // [BS] the entry's first slot in okey
+        ulonglong2* omk = (ulonglong2*)(oexc + BS);            // [BS] the entry's P / M masks
+        uint32_t* part = (uint32_t*)(omk + BS);                // [BS / 64] scan partials
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
         for (uint32_t b0 = 0; b0 < nw; b0 += BS) {   // workgroup-uniform
             const uint32_t kq = b0 + tid;
             const bool lv = kq < nw;
@@ -1446,24 +1492,25 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
             const ulonglong2 mk = lv ? wlm[lbase + kq] : make_ulonglong2(0ull, 0ull);
             const uint32_t e = we & 0x1FFFFFu;
             const uint32_t oi = lv ? off[e] : 0u;
-            uint64_t mp = mk.x & ~(1ull << 63), mm = mk.y;   // bit 63: a shared bucket (such pairs are redone)
+            const uint64_t mp = mk.x & ~(1ull << 63), mm = mk.y;   // bit 63: a shared bucket (such pairs are redone)
             uint32_t T;
             const uint32_t excl = wg_exclusive_scan<BS>((uint32_t)__popcll(mp) + (uint32_t)__popcll(mm), part, T);
             obase[tid] = oi - excl;
             oidx[tid] = we >> 21;
-            uint32_t o = excl;
-            while (mp | mm) {
-                const uint32_t jp = mp ? 63u - (uint32_t)__clzll(mp) : 0u, jm = mm ? 63u - (uint32_t)__clzll(mm) : 0u;
-                const uint32_t jj = mp ? (mm ? max(jp, jm) : jp) : jm;
-                const uint64_t bit = 1ull << jj;
-                if (mp & bit) {
-                    okey[o++] = (uint16_t)(jj | tid << 7);
-                    mp ^= bit;
-                }
-                if (mm & bit) {
-                    okey[o++] = (uint16_t)(jj | 64u | tid << 7);
-                    mm ^= bit;
-                }
+            oexc[tid] = excl;
+            omk[tid] = make_ulonglong2(mp, mm);
+            __syncthreads();
+            // key expansion, one wave per entry and one lane per B edge j: the range's keys in emit
+            // order (j DESC, P before M at one j), so key (j, P) sits at the keys above j
+            const uint32_t ne = min(nw - b0, (uint32_t)BS);
+            for (uint32_t l = wave; l < ne; l += BS / 64) {   // wave-uniform
+                const ulonglong2 m2 = omk[l];
+                const uint32_t x0 = oexc[l];
+                const uint32_t hp = (uint32_t)(m2.x >> lane) & 1u, hm = (uint32_t)(m2.y >> lane) & 1u;
+                const uint32_t above = lane == 63u ? 0u
+                                                   : (uint32_t)__popcll(m2.x >> (lane + 1u)) + (uint32_t)__popcll(m2.y >> (lane + 1u));
+                if (hp) okey[x0 + above] = (uint16_t)(lane | l << 7);
+                if (hm) okey[x0 + above + hp] = (uint16_t)(lane | 64u | l << 7);
             }
             __syncthreads();
             for (uint32_t q = tid; q < T; q += BS) {
