@@ -796,23 +796,17 @@ __global__ __launch_bounds__(BS) void k_large_products(mul_large_args g) {
 // bit 63 of M1 = a key of a shared bucket lies in the range (`order` probes it); then icnt[i] and,
 // for ranges with keys, imask[i] = (M1, M2). M1 / M2 use the dense digit table's LDS (dead now), tt
 // maps dense slot d back to its A edge. Barriers inside; every thread calls it.
-// LIST (direct pairs, k_large_count_la): the ranges with keys go instead to the A layer's writer list,
-// wl[k] = A edge i | its idx << 21 and imask[k] = (M1, M2) in any order, its length to *wln, so that
-// k_large_products_direct reads one contiguous list per A layer rather than gathering per A edge.
-template <int BS, bool LIST = false>
+template <int BS>
 __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_desc& d, uint32_t la, uint4 lbq,
-                           uint32_t neB, const uint32_t* recs, uint32_t* icnt, ulonglong2* imask,
-                           uint32_t* wl = nullptr, uint32_t* wln = nullptr) {
+                           uint32_t neB, const uint32_t* recs, uint32_t* icnt, ulonglong2* imask) {
     const uint32_t Bm = g.Bm, nB = d.nB;
     uint32_t* S = g.scratch;
     unsigned long long* M1 = (unsigned long long*)plds;
     unsigned long long* M2 = M1 + 2u * Bm;
-    const uint32_t* tt = (const uint32_t*)(plds + (LIST ? kCntTtOff : 64u) * Bm);
+    const uint32_t* tt = (const uint32_t*)(plds + 64u * Bm);
     const uint64_t m = d.nb_m;
     const uint32_t tid = threadIdx.x, nk = neB * Bm;
-    uint32_t* wn = (uint32_t*)(plds + (kCntTtOff + 16u) * Bm) + 1;   // LIST: the layer's list length (after dup)
     for (uint32_t k = tid; k < 4u * Bm; k += BS) M1[k] = 0ull;
-    if (LIST && tid == 0) *wn = 0;
     __syncthreads();
     bool shared = false;
     for (uint32_t q = tid; q < nk; q += BS) {
@@ -835,26 +829,90 @@ __device__ void iblk_layer(uint8_t* plds, const mul_large_args& g, const large_d
         uint32_t j;
         const uint32_t i = div_small(te, nB, m, j);
         const unsigned long long x1 = M1[dd], x2 = M2[dd];
-        // (LIST: k_large_lists zeroed the counts, so only ranges with keys store theirs)
-        if (!LIST) icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
+        icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
         // only ranges that hold keys are read back (write_ranges, order): most A edges of a deep
         // chain step hold none (their keys were all inserted by earlier A edges)
-        if (x1 | x2) {
-            if (LIST) {   // direct pairs: the A layer's writer list (any order), A edge | its idx << 21
-                icnt[i] = (uint32_t)__popcll(x1 & ~(1ull << 63)) + (uint32_t)__popcll(x2);
-                const uint32_t k = atomicAdd(wn, 1u);
-                wl[k] = i | (dd - ch * Bm) << 21;
-                imask[k] = make_ulonglong2(x1, x2);
-            } else {
-                imask[i] = make_ulonglong2(x1, x2);
-            }
-        }
+        if (x1 | x2) imask[i] = make_ulonglong2(x1, x2);
     }
     __syncthreads();   // the next A layer's staging overwrites M1 / M2, tt and recs
-    if (LIST && tid == 0) *wln = *wn;
 }
 
 // ---- direct mode (large_desc::direct) ------------------------------------------------------
+// k_large_count_la's per-A-layer output, held in registers so that its global stores can be issued
+// after the next layer's staging has consumed its loads (a wave's vmcnt counts stores and loads in
+// one FIFO: stores issued between a load and its use made that use wait for them)
+constexpr uint32_t kPendCells = 3;   // dense cells per thread held (2 B <= 3 x 256 for B <= 384)
+struct cnt_pend {
+    uint32_t i[kPendCells], w[kPendCells], k[kPendCells];   // A edge, list word, list slot + 1 (0: none)
+    ulonglong2 m[kPendCells];
+    uint32_t n;        // the layer's list length
+    uint32_t used;     // product layers (bit k: B layer k) with a key, from this thread's keys
+};
+
+// iblk_layer's counts and masks for a direct pair, as the A layer's writer list: the A edges whose
+// ranges hold keys, wl[k] = A edge i | its idx << 21 and imask[k] = (P mask, M mask) in any order
+// (slots from an LDS counter), so that k_large_products_direct reads one contiguous list per A layer.
+// k_large_lists zeroed the counts; only ranges with keys store theirs. Cells beyond kPendCells per
+// thread store at once. Barriers inside; every thread calls it.
+template <int BS>
+__device__ void cnt_layer_list(uint8_t* plds, uint32_t Bm, uint32_t nB, uint64_t nb_m, uint32_t nk, const uint32_t* recs,
+                               cnt_pend& p, uint32_t* icnt, uint32_t* wl, ulonglong2* imask) {
+    unsigned long long* M1 = (unsigned long long*)plds;
+    unsigned long long* M2 = M1 + 2u * Bm;
+    const uint32_t* tt = (const uint32_t*)(plds + kCntTtOff * Bm);
+    uint32_t* wn = (uint32_t*)(plds + (kCntTtOff + 16u) * Bm) + 1;   // after stage_tt's dup word
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < 4u * Bm; k += BS) M1[k] = 0ull;
+    if (tid == 0) *wn = 0;
+    __syncthreads();
+    for (uint32_t q = tid; q < nk; q += BS) {   // (no shared buckets in a direct pair)
+        const uint32_t v = recs[q];
+        if (!v) continue;
+        const uint32_t dd = v & 0xFFFu, j = (v >> 12) & 63u, e = (v >> 18) & 3u;
+        if (e & 1u) atomicOr(&M1[dd], 1ull << j);
+        if (e & 2u) atomicOr(&M2[dd], 1ull << j);
+    }
+    __syncthreads();
+    // cell dd: its list word and slot + 1 (0: no range with keys), its masks
+    auto cell = [&](uint32_t dd, uint32_t& i, uint32_t& w, ulonglong2& mk) -> uint32_t {
+        if (dd >= 2u * Bm) return 0u;
+        const uint32_t ch = dd >= Bm ? 1u : 0u;
+        const uint32_t te = tt[dd + ch * Bm];   // tt slot ch 2B + idx
+        if (te == kInf) return 0u;
+        const unsigned long long x1 = M1[dd], x2 = M2[dd];
+        if (!(x1 | x2)) return 0u;
+        uint32_t j;
+        i = div_small(te, nB, nb_m, j);
+        w = i | (dd - ch * Bm) << 21;
+        mk = make_ulonglong2(x1, x2);
+        return atomicAdd(wn, 1u) + 1u;
+    };
+#pragma unroll
+    for (uint32_t v = 0; v < kPendCells; ++v) p.k[v] = cell(tid + v * BS, p.i[v], p.w[v], p.m[v]);
+    for (uint32_t dd = tid + kPendCells * BS; dd < 2u * Bm; dd += BS) {   // B > 384 only
+        uint32_t i, w;
+        ulonglong2 mk;
+        const uint32_t k = cell(dd, i, w, mk);
+        if (!k) continue;
+        icnt[i] = (uint32_t)__popcll(mk.x) + (uint32_t)__popcll(mk.y);
+        wl[k - 1u] = w;
+        imask[k - 1u] = mk;
+    }
+    __syncthreads();   // the next A layer's staging overwrites M1 / M2, tt and recs
+    p.n = *wn;
+}
+
+__device__ __forceinline__ void cnt_flush(const cnt_pend& p, uint32_t* icnt, uint32_t* wl, ulonglong2* imask,
+                                          uint32_t* wln) {
+#pragma unroll
+    for (uint32_t u = 0; u < kPendCells; ++u) {
+        if (!p.k[u]) continue;
+        icnt[p.i[u]] = (uint32_t)__popcll(p.m[u].x) + (uint32_t)__popcll(p.m[u].y);
+        wl[p.k[u] - 1u] = p.w[u];
+        imask[p.k[u] - 1u] = p.m[u];
+    }
+    if (threadIdx.x == 0) *wln = p.n;
+}
 // Which keys emit, and in which order, follows from key PRESENCE alone when no key's products cancel:
 // a P (M) cell emits iff some product lands in it (arithmetic.hpp:96-101 with sums assumed != 0).
 // So the per-A-edge counts and masks of iblk_layer can be built before any multiply, the counts
@@ -965,6 +1023,19 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
     uint32_t st_c = S[d.o_lstA + la_c], n_c = S[d.o_lstA + LA + la_c];
     load_ids(st_c, n_c);
     uint32_t la_n = i0 + 1u < i1 ? S[d.o_neA + i0 + 1u] : 0u;
+    // the previous layer's outputs, stored after this layer's staging (cnt_pend)
+    cnt_pend pend;
+    uint32_t pend_la = kInf, pend_base = 0;
+    auto flush = [&]() {
+        if (pend_la == kInf) return;   // workgroup-uniform
+        cnt_flush(pend, S + d.o_icnt, S + d.o_wle + pend_base, (ulonglong2*)(S + d.o_imask) + pend_base,
+                  S + d.o_wln + pend_la);
+        // product layers with a key: compact_layers keeps them (benign race: every writer stores 1)
+#pragma unroll
+        for (uint32_t k = 0; k < kLaMaxLB; ++k)
+            if ((pend.used >> k) & 1u) S[d.o_used + (LA + LB) + pend_la * LB + lbv[k]] = 1;
+        pend_la = kInf;
+    };
     for (uint32_t i = i0; i < i1; ++i) {
         DSTAMP(0);
         const uint32_t la = late(la_c);
@@ -987,6 +1058,7 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             st_n = S[d.o_lstA + lx];
             n_n = S[d.o_lstA + LA + lx];
         }
+        flush();   // the previous layer's stores, behind this layer's loads
         uint32_t usedm = 0;
         for (uint32_t q = tid; q < neB * Bm; q += BS) {
             const uint32_t k = q / Bm, r = q - k * Bm;
@@ -1025,10 +1097,6 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             }
             recs[k * Bm + r] = rv;
         }
-        // product layers with a key: compact_layers keeps them (benign race: every writer stores 1)
-#pragma unroll
-        for (uint32_t k = 0; k < kLaMaxLB; ++k)
-            if ((usedm >> k) & 1u) S[d.o_used + (LA + LB) + la * LB + lbv[k]] = 1;
         __syncthreads();
         DSTAMP(2);
         uint32_t la_n2 = 0;
@@ -1037,17 +1105,21 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             if (i + 2u < i1) la_n2 = S[d.o_neA + i + 2u];
         }
         const uint32_t lbase = late(st_c);   // the layer's list slice: as its edge ids
-        iblk_layer<BS, true>(plds, g, d, la, make_uint4(lbv[0], lbv[1], lbv[2], lbv[3]), neB, recs, S + d.o_icnt,
-                             (ulonglong2*)(S + d.o_imask) + lbase, S + d.o_wle + lbase, S + d.o_wln + la);
+        cnt_layer_list<BS>(plds, Bm, nB, d.nb_m, neB * Bm, recs, pend, S + d.o_icnt, S + d.o_wle + lbase,
+                           (ulonglong2*)(S + d.o_imask) + lbase);
+        pend.used = usedm;
+        pend_la = la;
+        pend_base = lbase;
         DSTAMP(3);
 #ifdef PVAC_DIR_STAMPS
-        if (tid == 0) atomicAdd(&g_dir_stamps[13], (unsigned long long)S[d.o_wln + la]);
+        if (tid == 0) atomicAdd(&g_dir_stamps[13], (unsigned long long)pend.n);
 #endif
         la_c = lx;
         st_c = st_n;
         n_c = n_n;
         la_n = la_n2;
     }
+    flush();
 #ifdef PVAC_DIR_STAMPS
     if (tid == 0) {
         for (int p = 0; p < 4; ++p) atomicAdd(&g_dir_stamps[8 + p], st_acc[p]);
@@ -1069,22 +1141,9 @@ __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
     const int tid = threadIdx.x;
     uint32_t* icnt = S + d.o_icnt;
     const uint32_t nA = d.nA;
-    bool direct = !cnt[kCntIFail] && !cnt[kCntIShared];
-    uint32_t total = 0;
-    if (direct) {
-        for (uint32_t base = 0; base < nA; base += 4u * kLBig) {
-            uint32_t local = 0;
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t r = base + 4u * (uint32_t)tid + (uint32_t)k;
-                local += r < nA ? icnt[r] : 0u;
-            }
-            uint32_t tot;
-            wg_exclusive_scan<kLBig>(local, part, tot);
-            total += tot;
-        }
-        direct = !((g.flags & PVAC_MUL_ORDER_CANONICAL) != 0 || total > g.edge_budget);
-    }
-    if (!direct) {
+    // one pass: the suffix offsets are written while the total accumulates; a pair that is not
+    // direct after all (checked after the pass) is redone, so offsets written for it are never read
+    if (cnt[kCntIFail] || cnt[kCntIShared] || (g.flags & PVAC_MUL_ORDER_CANONICAL) != 0) {
         if (tid == 0) {
             cnt[kCntRedo] = 1;
             g.pair_status[d.pair] = kPairRedo;
@@ -1111,6 +1170,14 @@ __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
             run += v[k];
         }
         run0 += tot;
+    }
+    const uint32_t total = run0;
+    if (total > g.edge_budget) {   // guard_budget's canonical order: the general path (redo)
+        if (tid == 0) {
+            cnt[kCntRedo] = 1;
+            g.pair_status[d.pair] = kPairRedo;
+        }
+        return;
     }
     if (tid == 0) {
         cnt[3] = total;

@@ -10,7 +10,7 @@ timeout -k 10 400 python3 -u -m pytest -x -q --timeout 150 --timeout-method thre
     "$R/tests/test_gpu_chain.py" > "$D/pytest_large_chain.log" 2>&1 || { tail -30 "$D/pytest_large_chain.log"; exit 1; }
 tail -2 "$D/pytest_large_chain.log"
 timeout -k 10 300 python3 "$R/tools/chain_ab.py" --inputs 8192 "$R/pvac_hfhe_cppbyv_amd/lib/libpvac_hip.so" \
-    "$R/pvac_hfhe_cppbyv_amd/lib/exp/libpvac_hip_la8.so" "$R/pvac_hfhe_cppbyv_amd/lib/exp/libpvac_hip_cnt4.so" "$R/pvac_hfhe_cppbyv_amd/lib/libpvac_hip.so" "$R/pvac_hfhe_cppbyv_amd/lib/exp/libpvac_hip_la8.so" > "$D/chain_ab.log" 2>&1 || { tail -20 "$D/chain_ab.log"; exit 1; }
+    "$R/pvac_hfhe_cppbyv_amd/lib/exp/libpvac_hip_prev.so" "$R/pvac_hfhe_cppbyv_amd/lib/libpvac_hip.so" "$R/pvac_hfhe_cppbyv_amd/lib/exp/libpvac_hip_prev.so" > "$D/chain_ab.log" 2>&1 || { tail -20 "$D/chain_ab.log"; exit 1; }
 cat "$D/chain_ab.log"
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$D/chain1" -o run --output-format csv \
     -- python3 "$R/bench.py" --only chain --chain-no-check --chain-streams 1 --chain-inputs 8192 > "$D/chain1.log" 2>&1) || { tail -20 "$D/chain1.log"; exit 1; }
