@@ -169,6 +169,10 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pva
                          const uint64_t* nonces, const uint64_t* salts, pvac_ct_batch* C, uint32_t flags);
 /* Pairs that ct_mul_exec re-ran on the general path (see above) since the context was created. */
 int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* ctx, uint64_t* out);
+/* Pair launches by path since the context was created (diagnostics and tests): out[0] the
+ * LDS-resident fresh-shape kernel, out[1] the general path (redo launches included), out[2] of
+ * those the per-A-edge emit order, out[3] the direct mode (positions from key presence). */
+int pvac_hip_ct_mul_path_count(pvac_hip_ctx* ctx, uint64_t* out);
 /* Per-pair outcome of the last ct_mul_exec, copied (stream-ordered) to the DEVICE array out[n]:
  * 0 = reference hash order, 1 = canonical (layer, idx, P<M) order (guard_budget or
  * PVAC_MUL_ORDER_CANONICAL), 2 = rejected. Rejection is stricter than the reference: an edge with

@@ -118,6 +118,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_ct_mul_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
                                   C.POINTER(CtBatch), u32], i32),
         "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
+        "pvac_hip_ct_mul_path_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ct_mul_status": ([vp, vp, C.c_size_t], i32),
         "pvac_hip_ct_mul_chain": ([vp, C.POINTER(CtBatch), C.POINTER(ChainOpts), C.POINTER(ChainStats)], i32),
         "pvac_hip_alu_ceiling": ([vp, i32, C.POINTER(C.c_double)], i32),
@@ -444,6 +445,12 @@ class Engine:
         v = C.c_uint64(0)
         self._check(self.lib.pvac_hip_ct_mul_redo_count(self.ctx, C.byref(v)))
         return v.value
+
+    def ct_mul_path_counts(self):
+        """Pair launches by path since the context was created: {fresh, general, iblk, direct}."""
+        v = (C.c_uint64 * 4)()
+        self._check(self.lib.pvac_hip_ct_mul_path_count(self.ctx, v))
+        return dict(zip(("fresh", "general", "iblk", "direct"), (int(x) for x in v)))
 
     def ct_mul_status(self, n):
         """Per-pair outcome of the last ct_mul (0 hash order, 1 canonical order, 2 rejected)."""

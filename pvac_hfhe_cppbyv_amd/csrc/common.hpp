@@ -340,6 +340,8 @@ struct mul_large_args {
 constexpr uint32_t kLaPerWG = 4;
 constexpr uint32_t kLaMaxLB = 4;
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
+// LDS of k_large_products_direct for B and nbl staged B layers (the direct mode needs it <= 160 KB)
+uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl);
 // measured integer-ALU ceilings (k_ubench.hip)
 hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s);
 // ct_mul gsum invariant (k_check.hip, utils/metrics.hpp:70-113)

@@ -2203,6 +2203,8 @@ hipError_t launch_grp_build(fastmod64 nbm, uint32_t Bm, uint64_t S, uint32_t hbi
     return hipGetLastError();
 }
 
+uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl) { return dir_lds_bytes(Bm, nbl); }
+
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     if (!a.nl) return hipSuccess;
     if (a.Bm > kBmax || a.max_lay > kLargeLayersMax) return hipErrorInvalidValue;

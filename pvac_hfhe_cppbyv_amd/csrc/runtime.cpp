@@ -100,6 +100,7 @@ struct pvac_hip_ctx {
     uint32_t plan_stamp = 0;
     uint64_t last_mul_pairs = 0;       // pairs of the last ct_mul_exec (pair_status is valid for these)
     uint64_t redo_total = 0;           // pairs re-run by redo_fresh_pairs since the context was created
+    uint64_t path_total[4] = {};       // pair launches: fresh kernel, general path, its iblk order, direct mode
     large_desc* desc_dev = nullptr;
     size_t desc_cap = 0;
     uint32_t* sel_dev = nullptr;       // products: descriptor order per sub-batch (A-layer-major class first)
@@ -303,7 +304,11 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     // per-A-edge emit order (k_mul_large.hip): static groups and the A-layer-major products kernel
     d.iblk = static_grp && LB <= kLaMaxLB && nA >= 1 && nB >= 1 && nB <= kIblkMaxNB && large_iblk_enabled() ? 1u : 0u;
     // (direct A ids and writer lists pack an A edge with its dense cell: A edges < 2^21, 2 B <= 2^11)
-    d.direct = d.iblk && allow_direct && PVAC_LARGE_DIRECT && nA < (1ull << 21) && Bm <= 1024u ? 1u : 0u;
+    // (and k_large_products_direct's LDS: the digit table, LB staged B layers and their sums)
+    d.direct = d.iblk && allow_direct && PVAC_LARGE_DIRECT && nA < (1ull << 21) && Bm <= 1024u &&
+                       large_direct_lds_bytes(Bm, (uint32_t)LB) <= 160u * 1024u
+                   ? 1u
+                   : 0u;
     d.nb_m = nB ? (1ull << 32) / nB : 0;
     uint64_t o = 0;
     auto even = [&]() { o = (o + 1) & ~1ull; };
@@ -491,6 +496,12 @@ int pvac_hip_ctx_synchronize(pvac_hip_ctx* c) {
 int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* c, uint64_t* out) {
     if (!c || !out) return PVAC_EINVAL;
     *out = c->redo_total;
+    return PVAC_OK;
+}
+
+int pvac_hip_ct_mul_path_count(pvac_hip_ctx* c, uint64_t* out) {
+    if (!c || !out) return PVAC_EINVAL;
+    for (int k = 0; k < 4; ++k) out[k] = c->path_total[k];
     return PVAC_OK;
 }
 
@@ -748,6 +759,9 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             all_ib &= d.iblk != 0;
             any_dir |= d.direct != 0;
             all_dir &= d.direct != 0;
+            ++c->path_total[1];
+            c->path_total[2] += d.iblk;
+            c->path_total[3] += d.direct;
             if (d.direct) mLBd = std::max<uint32_t>(mLBd, d.LB);
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
@@ -906,6 +920,7 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         const hipError_t e = hipMemsetAsync(c->redo_cnt, 0, sizeof(unsigned int), c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "reset redo count");
     }
+    c->path_total[0] += plan->n_small;
     if (plan->n_small) {
         mul_fresh_args a{};
         a.A = *A; a.B = *B; a.C = *C;

@@ -570,3 +570,38 @@ def test_direct_cancelling_key_redo_vs_oracle(oracle):
         ref = oracle.ct_mul(xs[p], ys[p], per[p], canon_tag=0xCA2D)
         _same(out[p], ref, view=False)
     assert out[0].nE == 8 * 337 * 2 and out[1].nE == 8 * 337 * 2 - 1   # saturated: every cell emits but one
+
+
+@pytest.mark.parametrize("Bm", [97, 337, 1024])
+def test_direct_mode_shapes_vs_oracle(oracle, Bm):
+    """The direct mode (k_large_count_la / scan_direct / products_direct) across B: saturated and
+    partly filled dense A layers (48 .. 2B distinct cells) times 1-4 B layers of <= 20 edges, 4 or 8
+    A layers. B = 1024 puts 2 B = 2,048 dense cells on a 256-thread workgroup, past the cells
+    count_la holds in registers (kPendCells x 256), so its direct-store path runs too. Every pair
+    bit-exact vs the oracle; the path counters show the direct mode ran and nothing was redone.
+    Then the same shapes with an edge_budget below their output: scan_direct hands each pair to the
+    redo (canonical order), again bit-exact."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    rng = np.random.default_rng(0xD1 + Bm)
+    xs, ys = [], []
+    for k in range(6):
+        nla = 4 if k % 2 == 0 else 8
+        counts = [2 * Bm if (k + l) % 3 else int(rng.integers(48, 2 * Bm)) for l in range(nla)]
+        xs.append(_mk_layers(rng, counts, B=Bm))
+        ys.append(_mk_layers(rng, [20, 20, 13, 7][: 1 + k % 4], B=Bm))
+    eng = Engine(device=0, B=Bm, canon_tag=0xD2)
+    p0, r0 = eng.ct_mul_path_counts(), eng.ct_mul_redo_count()
+    out, plan, per = _run_mul(eng, xs, ys, seed=0xD3)
+    p1 = eng.ct_mul_path_counts()
+    assert plan.n_large == len(xs)
+    nd = p1["direct"] - p0["direct"]   # pairs whose key slots share no libstdc++ bucket
+    assert nd >= 2 and eng.ct_mul_redo_count() == r0
+    for p in range(len(xs)):
+        _same(out[p], oracle.ct_mul(xs[p], ys[p], per[p], canon_tag=0xD2, Bm=Bm), view=False)
+    budget = min(o.nE for o in out) - 1
+    eng2 = Engine(device=0, B=Bm, canon_tag=0xD2, edge_budget=budget)
+    out2, plan2, per2 = _run_mul(eng2, xs, ys, seed=0xD3)
+    pc = eng2.ct_mul_path_counts()
+    assert pc["direct"] == nd and eng2.ct_mul_redo_count() == nd   # every direct pair is over budget
+    for p in range(len(xs)):
+        _same(out2[p], oracle.ct_mul(xs[p], ys[p], per2[p], canon_tag=0xD2, Bm=Bm, edge_budget=budget), view=False)
