@@ -216,8 +216,18 @@ constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compre
 // (round 4: 35.2 -> 30.5 ms per 5.05 M edges, A/B in one process). The noise rows wait in
 // kNoiseWords after the columns and are flipped with them; the output word is the XOR of its copies.
 constexpr uint32_t kNoiseWords = 64;
+#ifdef PVAC_EXP_SIG_COPY8   // experiment builds only: eight image copies (copy = lane & 7)
+constexpr uint32_t kSigCopies = 8;
+#else
+constexpr uint32_t kSigCopies = 4;
+#endif
+// words of the image region (sigma | bmX | bmN, and the delta path's copies)
+__host__ __device__ constexpr uint32_t sigma_img_words(uint32_t m_bits, uint32_t n_bits) {
+    return m_bits / 32 + n_bits / 32 + m_bits / 32 > kSigCopies * (m_bits / 32) ? m_bits / 32 + n_bits / 32 + m_bits / 32
+                                                                                  : kSigCopies * (m_bits / 32);
+}
 __host__ __device__ constexpr uint32_t sigma_wave_words(uint32_t m_bits, uint32_t n_bits, uint32_t x_col_wt) {
-    return ((m_bits / 32 + n_bits / 32 + m_bits / 32 + (x_col_wt + 1) / 2 + kNoiseWords + 3) & ~3u) + kMidBatch * 2 * 8;
+    return ((sigma_img_words(m_bits, n_bits) + (x_col_wt + 1) / 2 + kNoiseWords + 3) & ~3u) + kMidBatch * 2 * 8;
 }
 
 // Fast column expansion (default Params: m_bits 8192, n_bits 16384, x_col_wt <= 128, full
@@ -274,8 +284,8 @@ constexpr uint32_t kDeltaBytes = 208;   // 13 chunks of 16 increments; <= 8 brid
 template <int WV>
 __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0, uint32_t c1) {
     constexpr uint32_t img = WV * kFastWaveWords * 4u;   // byte address of wave WV's image
-    uint32_t two = 4u, one = 1u;   // word W of copy k at byte 16 W + 4 k
-    const uint32_t kofs = (threadIdx.x & 3u) << 2;
+    uint32_t two = kSigCopies == 8 ? 5u : 4u, one = 1u;   // word W of copy k at byte 4 (copies W + k)
+    const uint32_t kofs = (threadIdx.x & (kSigCopies - 1u)) << 2;
     asm volatile("" : "+v"(two), "+v"(one));   // VGPR operands for the SDWA shifts
     auto word4 = [&](uint32_t& R, uint32_t w) {
 #pragma unroll
@@ -288,7 +298,7 @@ __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0,
             asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
                 : "=v"(bit) : "v"(R), "v"(one));
             off |= kofs;
-            __builtin_assume(off < 4096u);
+            __builtin_assume(off < 1024u * kSigCopies);
             lds_xor(img + off, bit);
         }
     };
@@ -338,13 +348,14 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t slds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t sw32 = a.m_bits / 32, bx32 = a.n_bits / 32, bn32 = a.m_bits / 32;
-    const uint32_t per_wave = sw32 + bx32 + bn32 + (a.x_col_wt + 1) / 2 + kNoiseWords;
+    const uint32_t imgw = sigma_img_words(a.m_bits, a.n_bits);
+    const uint32_t per_wave = imgw + (a.x_col_wt + 1) / 2 + kNoiseWords;
     uint32_t* sig = slds + (size_t)wave * sigma_wave_words(a.m_bits, a.n_bits, a.x_col_wt);
     uint32_t* bmX = sig + sw32;
     uint32_t* bmN = bmX + bx32;
-    uint16_t* cols = (uint16_t*)(bmN + bn32);
+    uint16_t* cols = (uint16_t*)(sig + imgw);
     uint32_t* mids = sig + ((per_wave + 3) & ~3u);   // [edge j][stream][8]
-    for (uint32_t w = lane; w < sw32 + bx32 + bn32; w += 64) sig[w] = 0;
+    for (uint32_t w = lane; w < imgw; w += 64) sig[w] = 0;
 
     const bool isX = lane < 32;
     const uint32_t Nmod = isX ? a.n_bits : a.m_bits;
@@ -500,27 +511,34 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                     default: flip_cols_delta<3>(a.rows_delta, c0, c1); break;
                 }
                 {   // the noise rows, into the lane's copy like the columns
-                    const uint32_t kofs = ((uint32_t)lane & 3u) << 2;
+                    const uint32_t kofs = ((uint32_t)lane & (kSigCopies - 1u)) << 2;
                     for (uint32_t q = (uint32_t)lane; q < a.err_wt; q += 64) {
                         const uint32_t r = nrows[q];
-                        atomicXor((uint32_t*)((uint8_t*)sig + (((r >> 5) << 4) | kofs)), 1u << (r & 31u));
+                        atomicXor((uint32_t*)((uint8_t*)sig + (((r >> 5) << (kSigCopies == 8 ? 5 : 4)) | kofs)),
+                                  1u << (r & 31u));
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
                 uint64_t* out = a.X.sigma + e * words_per_sigma;
                 {
                     // output words 4 lane .. 4 lane + 3: each the XOR of its four copies (one b128 read)
-                    uint4* s4 = (uint4*)sig + 4 * lane;
+                    constexpr int kQ = (int)kSigCopies;   // b128 reads per lane (4 words x copies / 4)
+                    uint4* s4 = (uint4*)sig + kQ * lane;
                     uint32_t o[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const uint4 v = s4[q];
-                        o[q] = v.x ^ v.y ^ v.z ^ v.w;
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int h = 0; h < kQ / 4; ++h) {
+                            const uint4 v = s4[q * (kQ / 4) + h];
+                            x ^= v.x ^ v.y ^ v.z ^ v.w;
+                        }
+                        o[q] = x;
                     }
                     ((ulonglong2*)out)[lane] = make_ulonglong2((uint64_t)o[0] | ((uint64_t)o[1] << 32),
                                                                (uint64_t)o[2] | ((uint64_t)o[3] << 32));
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) s4[q] = make_uint4(0, 0, 0, 0);
+                    for (int q = 0; q < kQ; ++q) s4[q] = make_uint4(0, 0, 0, 0);
                 }
                 __builtin_amdgcn_s_setprio(0);
                 continue;
@@ -656,7 +674,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
                 ((ulonglong2*)out)[w4] = make_ulonglong2((uint64_t)v.x | ((uint64_t)v.y << 32),
                                                          (uint64_t)v.z | ((uint64_t)v.w << 32));
             }
-            for (uint32_t w = lane; w < sw32 + bx32 + bn32; w += 64) sig[w] = 0;
+            for (uint32_t w = lane; w < imgw; w += 64) sig[w] = 0;
           }
         }
     }
