@@ -208,7 +208,13 @@ struct sig_args {
 // noise rows [2 kNoiseWords] u16 | midstates [32 edges][2 streams][8] u32
 // 6 blocks per CU (6 waves per SIMD): the compiler keeps the pass loop within 80 VGPRs without
 // spills instead of hoisting the whole SHA-256 message schedule (149 VGPRs, 3 waves per SIMD)
+#ifdef PVAC_EXP_SIG_MID16   // experiment builds only: 16-edge midstate batches, 7 workgroups per CU
+constexpr uint32_t kMidBatch = 16;
+constexpr int kSigMinBlocks = 7;
+#else
 constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compression per lane covers
+constexpr int kSigMinBlocks = 6;
+#endif
 // The delta path flips into four bank-interleaved copies of the image (word W of copy k at dword
 // 4 W + k of the 1024 words sigma | bmX | bmN, dead after the selection), copy k = lane & 3: the 8
 // lanes of a 32-lane ds_xor group that share a copy meet on 8 banks, instead of 32 lanes on 32
@@ -344,7 +350,7 @@ __device__ __forceinline__ void flip_cols_delta(const uint8_t* tab, uint32_t c0,
 // POW2: n_bits and m_bits are powers of two (default Params), so the rejection bound is
 // 2^64 - N and x mod N is a mask instead of a 64-bit software division per draw
 template <bool POW2>
-__global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
+__global__ __launch_bounds__(kSigBlock, kSigMinBlocks) void k_sigma(sig_args a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t slds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t sw32 = a.m_bits / 32, bx32 = a.n_bits / 32, bn32 = a.m_bits / 32;
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(kSigBlock, 6) void k_sigma(sig_args a) {
           uint32_t pre[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
           {
             const uint64_t kk = kb + (uint64_t)(lane & 31) * nsub;
-            if (kk < ne) {
+            if (kk < ne && (uint32_t)(lane & 31) < kMidBatch) {
                 uint64_t words[7];
                 edge_words(eo, lo, nl, eo + kk, words);
                 uint32_t b0[16], b1[16];
