@@ -966,51 +966,38 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
     if (!d.direct) return;
     uint32_t* S = g.scratch;
     uint32_t* cnt = S + d.o_cnt;
-    if (cnt[2] || cnt[kCntIFail]) return;
-    const uint32_t neA = cnt[0], neB = min(cnt[1], kLaMaxLB);
-    const uint32_t i0 = blockIdx.x * g.la_per_wg;
-    if (i0 >= neA) return;
     const uint32_t LA = d.LA, LB = d.LB, Bm = g.Bm, nB = d.nB;
     const uint32_t tid = threadIdx.x;
-    // B layers: per edge (P slot offset, M slot offset, j) as mx_stage_sparse computes them
-    uint4* sp = (uint4*)(plds + g.lds_task);                          // [kLaMaxLB][kMxMaxSparse]
-    uint32_t* bjt = (uint32_t*)(sp + kLaMaxLB * kMxMaxSparse);        // [64] B edge j: idx | ch << 16
-    uint32_t* recs = bjt + 64;                                        // [kLaMaxLB][B]
-    uint32_t nbv[kLaMaxLB], lbv[kLaMaxLB];
+    const uint32_t i0 = blockIdx.x * g.la_per_wg;
+    // The prologue's loads in dependency levels, each level's loads issued together (the A and B
+    // chains are independent): 1 the pair's counters, its B layer ids, the first A layer id, B's
+    // edge offset; 2 the layers' list ranges; 3 the id lists; 4 B's edge metas. (Issued in program
+    // order the chains took seven dependent round trips per workgroup.) Reads past a short list
+    // stay inside the pair's scratch and are not used.
+    const uint32_t c2 = cnt[2], cf = cnt[kCntIFail], c0 = cnt[0], c1 = cnt[1];
+    uint32_t lbv[kLaMaxLB];
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) lbv[k] = S[d.o_neB + k];
+    uint32_t la_c = S[d.o_neA + min(i0, LA - 1u)];
+    const uint64_t beo = g.B.e_off[d.pair];
+    if (c2 || cf) return;
+    const uint32_t neA = c0, neB = min(c1, kLaMaxLB);
+    if (i0 >= neA) return;
+    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+    // level 2
+    uint32_t nbv[kLaMaxLB], bst[kLaMaxLB];
 #pragma unroll
     for (uint32_t k = 0; k < kLaMaxLB; ++k) {
-        nbv[k] = 0;
-        lbv[k] = 0;
-        if (k < neB) {
-            const uint32_t lb = S[d.o_neB + k];
-            const layer_src srcB = side_layer(&g.B, g.B.e_off[d.pair], S, d.o_lstB, LB, lb);
-            lbv[k] = lb;
-            nbv[k] = srcB.n;   // <= kIblkMaxSparse (k_large_lists failed the pair otherwise)
-            if (tid < ((srcB.n + 3u) & ~3u) && srcB.n <= kMxMaxSparse) {
-                // (P slot offset, M slot offset, j, 1); padding to a multiple of 4: (0, 0, INF, 0)
-                uint4 v = make_uint4(0, 0, kInf, 0);
-                if (tid < srcB.n) {
-                    const uint32_t e = srcB.ids[tid];
-                    const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + e];
-                    const uint32_t sidx = meta_idx(mb), sch = meta_ch(mb);
-                    v = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, e, 1);
-                }
-                sp[k * kMxMaxSparse + tid] = v;
-            }
-        }
+        const uint32_t lb = k < neB ? lbv[k] : 0u;
+        lbv[k] = lb;
+        bst[k] = S[d.o_lstB + lb];
+        nbv[k] = k < neB ? S[d.o_lstB + LB + lb] : 0u;   // <= kIblkMaxSparse (k_large_lists failed the pair otherwise)
     }
-    if (tid < nB) {   // published by stage_tt's barriers
-        const uint64_t mb = g.B.meta[g.B.e_off[d.pair] + tid];
-        bjt[tid] = meta_idx(mb) | meta_ch(mb) << 16;
-    }
-    const uint32_t* tt = (const uint32_t*)(plds + kCntTtOff * Bm);
-    const uint32_t i1 = min(neA, i0 + g.la_per_wg);
-#ifdef PVAC_DIR_STAMPS
-    unsigned long long st_acc[4] = {0, 0, 0, 0}, t_prev = dir_stamp();
-#endif
-    // layers one ahead: the next layer's list range loads during this layer's keys, its first 4 BS
-    // ids during iblk_layer, so stage_tt starts from registers
+    uint32_t st_c = S[d.o_lstA + la_c], n_c = S[d.o_lstA + LA + la_c];
+    const uint64_t mbj = tid < nB ? g.B.meta[beo + tid] : 0ull;   // bjt below
+    // level 3
     const uint32_t* idsA = S + d.o_lstA + 2u * LA;
+    const uint32_t* idsB = S + d.o_lstB + 2u * LB;
     uint32_t pre[4];
     auto load_ids = [&](uint32_t st, uint32_t n) {
 #pragma unroll
@@ -1019,10 +1006,35 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             pre[v] = idsA[st + (k < n ? k : 0u)];
         }
     };
-    uint32_t la_c = S[d.o_neA + i0];
-    uint32_t st_c = S[d.o_lstA + la_c], n_c = S[d.o_lstA + LA + la_c];
     load_ids(st_c, n_c);
+    uint32_t eb[kLaMaxLB];
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) eb[k] = k < neB ? idsB[bst[k] + (tid < nbv[k] ? tid : 0u)] : 0u;
     uint32_t la_n = i0 + 1u < i1 ? S[d.o_neA + i0 + 1u] : 0u;
+    // level 4: B layers as per-edge (P slot offset, M slot offset, j, 1), padded to a multiple of 4
+    // with (0, 0, INF, 0), as mx_stage_sparse computes them
+    uint4* sp = (uint4*)(plds + g.lds_task);                          // [kLaMaxLB][kMxMaxSparse]
+    uint32_t* bjt = (uint32_t*)(sp + kLaMaxLB * kMxMaxSparse);        // [64] B edge j: idx | ch << 16
+    uint32_t* recs = bjt + 64;                                        // [kLaMaxLB][B]
+    uint64_t mbk[kLaMaxLB];
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) mbk[k] = k < neB ? g.B.meta[beo + eb[k]] : 0ull;
+#pragma unroll
+    for (uint32_t k = 0; k < kLaMaxLB; ++k) {
+        if (k < neB && tid < ((nbv[k] + 3u) & ~3u) && nbv[k] <= kMxMaxSparse) {
+            uint4 v = make_uint4(0, 0, kInf, 0);
+            if (tid < nbv[k]) {
+                const uint32_t sidx = meta_idx(mbk[k]), sch = meta_ch(mbk[k]);
+                v = make_uint4(sch * 2u * Bm + Bm - sidx, (sch ^ 1u) * 2u * Bm + Bm - sidx, eb[k], 1);
+            }
+            sp[k * kMxMaxSparse + tid] = v;
+        }
+    }
+    if (tid < nB) bjt[tid] = meta_idx(mbj) | meta_ch(mbj) << 16;   // published by stage_tt's barriers
+    const uint32_t* tt = (const uint32_t*)(plds + kCntTtOff * Bm);
+#ifdef PVAC_DIR_STAMPS
+    unsigned long long st_acc[4] = {0, 0, 0, 0}, t_prev = dir_stamp();
+#endif
     // the previous layer's outputs, stored after this layer's staging (cnt_pend)
     cnt_pend pend;
     uint32_t pend_la = kInf, pend_base = 0;
