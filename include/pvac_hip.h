@@ -115,6 +115,10 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* ctx);
 int pvac_hip_ctx_set_stream(pvac_hip_ctx* ctx, void* hip_stream);
 void* pvac_hip_ctx_stream(pvac_hip_ctx* ctx);
 int pvac_hip_ctx_synchronize(pvac_hip_ctx* ctx);
+/* The noise fields of the reference's Params (core/types.hpp:48-50: noise_entropy_bits 120,
+ * tuple2_fraction 0.55, depth_slope_bits 16 by default), used by enc_value / enc_value_depth's
+ * plan_noise (ops/encrypt.hpp:16-27). A plan above 256 pre-merge edges per half is PVAC_ENOSYS. */
+int pvac_hip_ctx_set_noise(pvac_hip_ctx* ctx, double noise_entropy_bits, double tuple2_fraction, double depth_slope_bits);
 const char* pvac_hip_last_error(pvac_hip_ctx* ctx);
 /* Upload the public parity matrix H (pk.H, crypto/matrix.hpp:191-251) from a HOST dense
  * array of n_bits columns x ceil(m_bits/64) words; stored on device as per-column sparse
@@ -311,9 +315,10 @@ int pvac_hip_enc_value(pvac_hip_ctx* ctx, size_t n, const uint64_t* values, cons
                        pvac_ct_batch* C, uint32_t flags, uint32_t* status);
 /* enc_value_depth(pk, sk, v, depth_hint) (ops/encrypt.hpp:281-287): as pvac_hip_enc_value with the
  * noise plan of depth_hint (plan_noise, encrypt.hpp:16-27: more Z2 / Z3 groups as the hint grows;
- * supported while 8 + 2 Z2 + 3 Z3 <= 48, i.e. depth_hint <= 15 with the default Params, else
- * PVAC_ENOSYS). values[i] = 0 gives enc_zero_depth(pk, sk, depth_hint) (encrypt.hpp:293-298)
- * byte for byte: fp_add(0, mask) is mask and the draws are the same. Size outputs and rnd_stride with
+ * supported while 8 + 2 Z2 + 3 Z3 <= 256, i.e. depth_hint <= 124 with the default Params, else
+ * PVAC_ENOSYS; the Params noise fields from pvac_hip_ctx_set_noise). values[i] = 0 gives
+ * enc_zero_depth(pk, sk, depth_hint) (encrypt.hpp:293-298) byte for byte: fp_add(0, mask) is mask and
+ * the draws are the same. Size outputs and rnd_stride with
  * pvac_hip_enc_caps_depth. */
 int pvac_hip_enc_caps_depth(pvac_hip_ctx* ctx, int depth_hint, uint32_t* layers_per_value, uint32_t* edges_per_value,
                             uint32_t* draws_hint);

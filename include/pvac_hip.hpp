@@ -416,6 +416,9 @@ public:
     // under the same canon_tag replaces the device copy.
     template <class PubKeyT, class SecKeyT>
     void ensure_keys(const PubKeyT& pk, const SecKeyT& sk) {
+        // plan_noise's Params fields (core/types.hpp:48-50), read on every call like the reference
+        check(pvac_hip_ctx_set_noise(ctx_, (double)pk.prm.noise_entropy_bits, (double)pk.prm.tuple2_fraction,
+                                     (double)pk.prm.depth_slope_bits));
         const std::vector<uint64_t> fp = key_fingerprint(sk);
         if (keys_ready_ && fp == key_fp_) return;
         if (!keys_ready_) {

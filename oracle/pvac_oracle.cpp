@@ -830,13 +830,19 @@ void orc_prf_noise_delta(const orc_secret* sk, uint64_t canon, uint64_t z, uint6
     out[0] = r.lo; out[1] = r.hi;
 }
 
-// ops/encrypt.hpp:16-27 with the default Params (noise_entropy_bits 120, tuple2_fraction 0.55,
-// depth_slope_bits 16)
+// ops/encrypt.hpp:16-27; the Params noise fields (core/types.hpp:48-50), defaults 120 / 0.55 / 16,
+// set process-wide for tests by orc_set_noise
+static double g_noise_bits = 120.0, g_noise_t2 = 0.55, g_noise_slope = 16.0;
+void orc_set_noise(double noise_entropy_bits, double tuple2_fraction, double depth_slope_bits) {
+    g_noise_bits = noise_entropy_bits;
+    g_noise_t2 = tuple2_fraction;
+    g_noise_slope = depth_slope_bits;
+}
 static void plan_noise(uint32_t B, int depth, int& z2, int& z3) {
-    const double budget = 120.0 + 16.0 * std::max(0, depth);
+    const double budget = g_noise_bits + g_noise_slope * std::max(0, depth);
     const double per2 = 2.0 * std::log2((double)B), per3 = 3.0 * std::log2((double)B);
-    z2 = std::max(0, (int)std::floor((budget * 0.55) / std::max(1e-6, per2)));
-    z3 = std::max(0, (int)std::floor((budget * (1.0 - 0.55)) / std::max(1e-6, per3)));
+    z2 = std::max(0, (int)std::floor((budget * g_noise_t2) / std::max(1e-6, per2)));
+    z3 = std::max(0, (int)std::floor((budget * (1.0 - g_noise_t2)) / std::max(1e-6, per3)));
     if (z2 + z3 == 1) { if (z3 > 0) ++z3; else ++z2; }
 }
 

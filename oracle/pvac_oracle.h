@@ -106,6 +106,8 @@ int orc_enc_value(const orc_params* prm, const orc_secret* sk, const uint64_t* H
                   size_t* consumed);
 /* enc_value_depth(v, depth_hint) (ops/encrypt.hpp:281-287): the noise plan of depth_hint
  * (plan_noise, encrypt.hpp:16-27); v = 0 gives enc_zero_depth (:293-298) exactly. */
+/* plan_noise's Params fields (process-wide; defaults 120, 0.55, 16) */
+void orc_set_noise(double noise_entropy_bits, double tuple2_fraction, double depth_slope_bits);
 int orc_enc_value_depth(const orc_params* prm, const orc_secret* sk, const uint64_t* H_dense, const uint64_t* powg,
                         uint64_t v, int depth_hint, const uint64_t* stream, size_t n, int order, orc_cipher* out,
                         size_t* consumed);

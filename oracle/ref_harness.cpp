@@ -510,6 +510,55 @@ static void cmd_encdepth(const std::string& dir) {
     std::ofstream(dir + "/encd_manifest.json") << js.str();
 }
 
+// ---------------------------------------------------------------- deep depth hints, other noise Params
+// enc_value_depth / enc_zero_depth with depth hints past 15 and with non-default noise Params
+// (noise_entropy_bits, tuple2_fraction, depth_slope_bits: plan_noise, encrypt.hpp:16-27), including
+// a plan with no noise groups and one bumped from a single group to two. Same key as cmd_encdepth.
+static void cmd_encdeep(const std::string& dir) {
+    reseed(0x5EED0C00ULL);
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    (void)enc_value(pk, sk, 1);   // warm-up: the Toeplitz autotuner draws random words once
+    struct Case { int kind; uint64_t v; int depth; double ent, frac, slope; };
+    const Case cases[] = {{0, 77, 16, 120.0, 0.55, 16.0},   {0, 123456789, 31, 120.0, 0.55, 16.0},
+                          {0, 9, 60, 120.0, 0.55, 16.0},    {1, 0, 100, 120.0, 0.55, 16.0},
+                          {0, 31337, 2, 64.0, 0.8, 8.0},   {0, 4, 7, 200.0, 0.2, 20.0},
+                          {0, 1000003, 0, 40.0, 0.5, 16.0}, {0, 11, 0, 0.0, 0.55, 0.0}};
+    const int nc = (int)(sizeof cases / sizeof cases[0]);
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ",\n  \"cases\": [\n";
+    for (int i = 0; i < nc; ++i) {
+        const Case& c = cases[i];
+        PubKey pkc = pk;
+        pkc.prm.noise_entropy_bits = c.ent;
+        pkc.prm.tuple2_fraction = c.frac;
+        pkc.prm.depth_slope_bits = c.slope;
+        reseed(0x5EED0F10ULL + (uint64_t)i);
+        g_logging = true;
+        std::vector<uint64_t> stream;
+        Cipher X = run_logged([&] { return c.kind ? enc_zero_depth(pkc, sk, c.depth) : enc_value_depth(pkc, sk, c.v, c.depth); },
+                              stream);
+        g_logging = false;
+        const std::string pre = dir + "/encx" + std::to_string(i);
+        write_ct(pre + ".ct", {X}, true);
+        write_u64(pre + "_stream.u64", stream);
+        const Fp dv = dec_value(pkc, sk, X);
+        const auto z = plan_noise(pkc, c.depth);
+        js << "    {\"kind\": \"" << (c.kind ? "zero" : "value") << "\", \"v\": " << c.v << ", \"depth\": " << c.depth
+           << ", \"noise_entropy_bits\": " << c.ent << ", \"tuple2_fraction\": " << c.frac << ", \"depth_slope_bits\": "
+           << c.slope << ", \"Z2\": " << z.first << ", \"Z3\": " << z.second << ", \"edges\": " << X.E.size()
+           << ", \"layers\": " << X.L.size() << ", \"stream\": " << stream.size() << ", \"dec\": " << fpjson(dv)
+           << "}" << (i + 1 < nc ? "," : "") << "\n";
+        std::printf("encdeep case %d: depth %d Z2 %d Z3 %d edges %zu stream %zu\n", i, c.depth, z.first, z.second,
+                    X.E.size(), stream.size());
+    }
+    js << "  ],\n  \"generator\": \"oracle/ref_harness.cpp encdeep (reference pvac-hfhe 0.1.0)\"\n}\n";
+    std::ofstream(dir + "/encx_manifest.json") << js.str();
+}
+
 // ---------------------------------------------------------------- timing (CPU baseline leg)
 // Times the reference's own ct_mul (WITH sigma, arithmetic.hpp:47-106) on fresh pairs.
 static void cmd_time_mul(int npairs, int threads) {
@@ -659,6 +708,10 @@ int main(int argc, char** argv) {
     }
     if (cmd == "encdepth" && argc >= 3) {
         cmd_encdepth(argv[2]);
+        return 0;
+    }
+    if (cmd == "encdeep" && argc >= 3) {
+        cmd_encdeep(argv[2]);
         return 0;
     }
     if (cmd == "fullrange" && argc >= 3) {

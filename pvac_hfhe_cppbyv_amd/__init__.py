@@ -119,6 +119,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
                                   C.POINTER(CtBatch), u32], i32),
         "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ct_mul_path_count": ([vp, C.POINTER(u64)], i32),
+        "pvac_hip_ctx_set_noise": ([vp, C.c_double, C.c_double, C.c_double], i32),
         "pvac_hip_ct_mul_status": ([vp, vp, C.c_size_t], i32),
         "pvac_hip_ct_mul_chain": ([vp, C.POINTER(CtBatch), C.POINTER(ChainOpts), C.POINTER(ChainStats)], i32),
         "pvac_hip_alu_ceiling": ([vp, i32, C.POINTER(C.c_double)], i32),
@@ -445,6 +446,11 @@ class Engine:
         v = C.c_uint64(0)
         self._check(self.lib.pvac_hip_ct_mul_redo_count(self.ctx, C.byref(v)))
         return v.value
+
+    def set_noise(self, noise_entropy_bits=120.0, tuple2_fraction=0.55, depth_slope_bits=16.0):
+        """The reference Params' noise fields for enc_value's plan_noise (ops/encrypt.hpp:16-27)."""
+        self._check(self.lib.pvac_hip_ctx_set_noise(self.ctx, float(noise_entropy_bits), float(tuple2_fraction),
+                                                    float(depth_slope_bits)))
 
     def ct_mul_path_counts(self):
         """Pair launches by path since the context was created: {fresh, general, iblk, direct}."""

@@ -191,7 +191,10 @@ hipError_t launch_base_R(const prf_consts& k, const pvac_ct_batch& X, uint64_t n
                          uint64_t* core_scratch, uint64_t* R_out, hipStream_t st);
 
 // ---- enc_value (k_enc.hip, ops/encrypt.hpp:114-291)
-constexpr uint32_t kEncPreMax = 48;   // pre-merge edges per half: 8 signal + 2 Z2 + 3 Z3 (Z2, Z3 <= 8)
+// pre-merge edges per half, 8 signal + 2 Z2 + 3 Z3: two capacity classes of the per-half plan record
+// (the default plans and depth hints <= 15 fit the small one; depth hints up to 124 the large one)
+constexpr uint32_t kEncPreSmall = 48;
+constexpr uint32_t kEncPreMax = 256;
 struct enc_plan_args {
     const uint64_t* values;   // n plaintexts
     const uint64_t* rnd;      // csprng_u64 draws: stride words per value
@@ -201,7 +204,7 @@ struct enc_plan_args {
     uint64_t canon;
     const uint64_t* powg;     // B x (lo, hi)
 };
-size_t enc_half_bytes();
+size_t enc_half_bytes(uint32_t npre);   // per-half plan record of the capacity class npre needs
 // per value: 2 output layers, <= 2 * (8 + 2 Z2 + 3 Z3) edges; cores per value = 2 * 3 * max(Z2 + Z3, 1)
 uint32_t enc_cores_per_value(uint32_t Z2, uint32_t Z3);
 // 1. draws (exact csprng order), merge groups, shuffle, PRF requests, and the pre-merge edge batch

@@ -26,15 +26,17 @@ namespace {
 
 constexpr int kEB = 64;
 
+template <uint32_t CAP>   // pre-edge capacity: kEncPreSmall or kEncPreMax (group ids fit a byte)
 struct enc_half {
+    static_assert(CAP <= 256, "group ids and slots are bytes");
     uint64_t nlo, nhi, ztag;
     uint64_t vlo, vhi;            // the value this half encrypts (v + mask or -mask)
     uint32_t npre, nout;
-    uint32_t key[kEncPreMax];     // idx | ch << 16, creation order
-    uint64_t salt[kEncPreMax];
-    uint64_t rlo[kEncPreMax], rhi[kEncPreMax];   // coefficients; solved ones filled by k_enc_weights
-    uint8_t grp[kEncPreMax];      // compact_edges group of each pre-edge ((idx, P < M) order)
-    uint8_t slot[kEncPreMax];     // output slot -> group (after shuffle_edges)
+    uint32_t key[CAP];            // idx | ch << 16, creation order
+    uint64_t salt[CAP];
+    uint64_t rlo[CAP], rhi[CAP];  // coefficients; solved ones filled by k_enc_weights
+    uint8_t grp[CAP];             // compact_edges group of each pre-edge ((idx, P < M) order)
+    uint8_t slot[CAP];            // output slot -> group (after shuffle_edges)
 };
 
 struct rstream {
@@ -60,7 +62,8 @@ __device__ fp rand_fp_nonzero(rstream& rs) {   // core/types.hpp:145-155
 __device__ __forceinline__ fp powg_at(const uint64_t* g, uint32_t i) { return fp{g[2 * i], g[2 * i + 1]}; }
 
 // one enc_fp_depth draw replay (ops/encrypt.hpp:162-258, no PRF / weights)
-__device__ void plan_half(const enc_plan_args& a, rstream& rs, const fp& v, enc_half& H) {
+template <uint32_t CAP>
+__device__ void plan_half(const enc_plan_args& a, rstream& rs, const fp& v, enc_half<CAP>& H) {
     const uint32_t B = a.B;
     H.nlo = rs.next();
     H.nhi = rs.next();
@@ -112,39 +115,39 @@ __device__ void plan_half(const enc_plan_args& a, rstream& rs, const fp& v, enc_
         H.key[np] = k | (s3 << 16); H.rlo[np] = 0; H.rhi[np] = 0; H.salt[np] = rs.next(); ++np;
     }
     H.npre = np;
-    // compact_edges (encrypt.hpp:39-71) output order: (layer, idx, P before M) over distinct keys
+    // compact_edges (encrypt.hpp:39-71) output order: (layer, idx, P before M) over distinct keys.
+    // First occurrences marked in slot[] (reused for the order below), then each pre-edge's group is
+    // the number of distinct keys below its own: O(np^2)
     auto sk = [&](uint32_t e) { return (H.key[e] & 0xFFFFu) * 2u + (H.key[e] >> 16); };
     uint32_t ng = 0;
     for (uint32_t e = 0; e < np; ++e) {
         const uint32_t k = sk(e);
-        uint32_t rank = 0;
         bool first = true;
-        for (uint32_t f = 0; f < np; ++f) {
-            const uint32_t kf = sk(f);
-            bool f_first = true;   // f is the first pre-edge carrying its key
-            for (uint32_t q = 0; q < f; ++q) f_first &= sk(q) != kf;
-            rank += (f_first && kf < k) ? 1u : 0u;
-            if (f < e && kf == k) first = false;
-        }
-        H.grp[e] = (uint8_t)rank;
+        for (uint32_t q = 0; q < e; ++q) first &= sk(q) != k;
+        H.slot[e] = first ? 1u : 0u;
         ng += first ? 1u : 0u;
     }
-    // shuffle_edges (encrypt.hpp:155-160) on the ng compacted entries
-    uint8_t order[kEncPreMax];
-    for (uint32_t g = 0; g < ng; ++g) order[g] = (uint8_t)g;
+    for (uint32_t e = 0; e < np; ++e) {
+        const uint32_t k = sk(e);
+        uint32_t rank = 0;
+        for (uint32_t f = 0; f < np; ++f) rank += (H.slot[f] && sk(f) < k) ? 1u : 0u;
+        H.grp[e] = (uint8_t)rank;
+    }
+    // shuffle_edges (encrypt.hpp:155-160) on the ng compacted entries, in place in slot[]
+    for (uint32_t g = 0; g < ng; ++g) H.slot[g] = (uint8_t)g;
     for (uint32_t i = ng > 1 ? ng - 1 : 0; i > 0; --i) {
         const uint32_t j = (uint32_t)(rs.next() % (uint64_t)(i + 1));
-        const uint8_t t = order[i];
-        order[i] = order[j];
-        order[j] = t;
+        const uint8_t t = H.slot[i];
+        H.slot[i] = H.slot[j];
+        H.slot[j] = t;
     }
-    for (uint32_t g = 0; g < ng; ++g) H.slot[g] = order[g];
     H.nout = ng;
 }
 
 // prf requests of one half: prf_R's three cores (seed = the layer seed) and, for every group but
 // the last, prf_noise_delta's three cores on the derived seed (encrypt.hpp:113-128, 205-210)
-__device__ void half_requests(const enc_plan_args& a, const enc_half& H, prf_request* req) {
+template <class HALF>
+__device__ void half_requests(const enc_plan_args& a, const HALF& H, prf_request* req) {
     for (uint32_t c = 0; c < 3; ++c) req[c] = prf_request{H.ztag, H.nlo, H.nhi, c, 0};
     const uint32_t G = a.Z2 + a.Z3;
     for (uint32_t g = 0; g + 1 < G; ++g) {
@@ -158,15 +161,16 @@ __device__ void half_requests(const enc_plan_args& a, const enc_half& H, prf_req
     }
 }
 
-__global__ __launch_bounds__(kEB) void k_enc_plan(enc_plan_args a, enc_half* halves, prf_request* req,
+template <uint32_t CAP>
+__global__ __launch_bounds__(kEB) void k_enc_plan(enc_plan_args a, enc_half<CAP>* halves, prf_request* req,
                                                   pvac_ct_batch pre, uint64_t* pre_salt, uint32_t* status) {
     const uint64_t i = (uint64_t)blockIdx.x * kEB + threadIdx.x;
     if (i >= a.n) return;
     rstream rs{a.rnd + i * a.stride, a.stride, 0, false};
     const fp mask = rand_fp_nonzero(rs);
     const fp va = fp_add(fp{a.values[i], 0}, mask), vb = fp_neg(mask);
-    enc_half& A = halves[2 * i];       // output layer 0: enc_fp_depth(v + mask)
-    enc_half& Bh = halves[2 * i + 1];  // output layer 1: enc_fp_depth(-mask), drawn first
+    enc_half<CAP>& A = halves[2 * i];       // output layer 0: enc_fp_depth(v + mask)
+    enc_half<CAP>& Bh = halves[2 * i + 1];  // output layer 1: enc_fp_depth(-mask), drawn first
     plan_half(a, rs, vb, Bh);
     plan_half(a, rs, va, A);
     status[i] = rs.over ? 1u : 0u;
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(kEB) void k_enc_plan(enc_plan_args a, enc_half* hal
     pre.e_off[i] = i * 2 * npre;
     pre.e_cnt[i] = 2 * npre;
     for (int h = 0; h < 2; ++h) {
-        const enc_half& H = h ? Bh : A;
+        const enc_half<CAP>& H = h ? Bh : A;
         pvac_layer y{};
         y.ztag = H.ztag;
         y.nonce_lo = H.nlo;
@@ -194,11 +198,12 @@ __global__ __launch_bounds__(kEB) void k_enc_plan(enc_plan_args a, enc_half* hal
     }
 }
 
-__global__ __launch_bounds__(kEB) void k_enc_weights(enc_plan_args a, enc_half* halves, const uint64_t* cores,
+template <uint32_t CAP>
+__global__ __launch_bounds__(kEB) void k_enc_weights(enc_plan_args a, enc_half<CAP>* halves, const uint64_t* cores,
                                                      pvac_ct_batch pre) {
     const uint64_t hi_ = (uint64_t)blockIdx.x * kEB + threadIdx.x;
     if (hi_ >= 2 * a.n) return;
-    enc_half& H = halves[hi_];
+    enc_half<CAP>& H = halves[hi_];
     const uint32_t G = a.Z2 + a.Z3;
     const uint32_t per_half = 3 * max(G, 1u);
     const uint64_t* c = cores + 2 * hi_ * per_half;
@@ -258,7 +263,8 @@ __global__ __launch_bounds__(kEB) void k_enc_weights(enc_plan_args a, enc_half* 
 }
 
 // one wave per value: merged groups in shuffled order; lanes XOR sigma words
-__global__ __launch_bounds__(kEB) void k_enc_finish(enc_plan_args a, const enc_half* halves, pvac_ct_batch pre,
+template <uint32_t CAP>
+__global__ __launch_bounds__(kEB) void k_enc_finish(enc_plan_args a, const enc_half<CAP>* halves, pvac_ct_batch pre,
                                                     pvac_ct_batch C, uint32_t* status) {
     const uint64_t i = blockIdx.x;
     if (i >= a.n) return;
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(kEB) void k_enc_finish(enc_plan_args a, const enc_h
     uint32_t pos = 0;
     bool vanished = false;
     for (int h = 0; h < 2; ++h) {
-        const enc_half& H = halves[2 * i + h];
+        const enc_half<CAP>& H = halves[2 * i + h];
         if (lane == 0) {
             pvac_layer y{};
             y.ztag = H.ztag;
@@ -319,24 +325,38 @@ __global__ __launch_bounds__(kEB) void k_enc_finish(enc_plan_args a, const enc_h
 
 }  // namespace
 
-size_t enc_half_bytes() { return sizeof(enc_half); }
+static bool enc_small(uint32_t npre) { return npre <= kEncPreSmall; }
+
+size_t enc_half_bytes(uint32_t npre) {
+    return enc_small(npre) ? sizeof(enc_half<kEncPreSmall>) : sizeof(enc_half<kEncPreMax>);
+}
 
 uint32_t enc_cores_per_value(uint32_t Z2, uint32_t Z3) { return 2u * 3u * std::max(Z2 + Z3, 1u); }
 
 hipError_t launch_enc_plan(const enc_plan_args& a, void* halves, prf_request* req, pvac_ct_batch& pre,
                            uint64_t* pre_salt, uint32_t* status, hipStream_t st) {
     if (!a.n) return hipSuccess;
-    if (8 + 2 * a.Z2 + 3 * a.Z3 > kEncPreMax || a.B == 0 || a.B > 65536) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_enc_plan, dim3((unsigned)((a.n + kEB - 1) / kEB)), dim3(kEB), 0, st, a, (enc_half*)halves, req,
-                       pre, pre_salt, status);
+    const uint32_t npre = 8 + 2 * a.Z2 + 3 * a.Z3;
+    if (npre > kEncPreMax || a.B == 0 || a.B > 65536) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((a.n + kEB - 1) / kEB));
+    if (enc_small(npre))
+        hipLaunchKernelGGL(k_enc_plan<kEncPreSmall>, grid, dim3(kEB), 0, st, a, (enc_half<kEncPreSmall>*)halves, req, pre,
+                           pre_salt, status);
+    else
+        hipLaunchKernelGGL(k_enc_plan<kEncPreMax>, grid, dim3(kEB), 0, st, a, (enc_half<kEncPreMax>*)halves, req, pre,
+                           pre_salt, status);
     return hipGetLastError();
 }
 
 hipError_t launch_enc_weights(const enc_plan_args& a, void* halves, const uint64_t* cores, pvac_ct_batch& pre,
                               hipStream_t st) {
     if (!a.n) return hipSuccess;
-    hipLaunchKernelGGL(k_enc_weights, dim3((unsigned)((2 * a.n + kEB - 1) / kEB)), dim3(kEB), 0, st, a,
-                       (enc_half*)halves, cores, pre);
+    const dim3 grid((unsigned)((2 * a.n + kEB - 1) / kEB));
+    if (enc_small(8 + 2 * a.Z2 + 3 * a.Z3))
+        hipLaunchKernelGGL(k_enc_weights<kEncPreSmall>, grid, dim3(kEB), 0, st, a, (enc_half<kEncPreSmall>*)halves, cores,
+                           pre);
+    else
+        hipLaunchKernelGGL(k_enc_weights<kEncPreMax>, grid, dim3(kEB), 0, st, a, (enc_half<kEncPreMax>*)halves, cores, pre);
     return hipGetLastError();
 }
 
@@ -344,7 +364,12 @@ hipError_t launch_enc_finish(const enc_plan_args& a, const void* halves, const p
                              uint32_t* status, hipStream_t st) {
     if (!a.n) return hipSuccess;
     if (a.n > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_enc_finish, dim3((unsigned)a.n), dim3(kEB), 0, st, a, (const enc_half*)halves, pre, C, status);
+    if (enc_small(8 + 2 * a.Z2 + 3 * a.Z3))
+        hipLaunchKernelGGL(k_enc_finish<kEncPreSmall>, dim3((unsigned)a.n), dim3(kEB), 0, st, a,
+                           (const enc_half<kEncPreSmall>*)halves, pre, C, status);
+    else
+        hipLaunchKernelGGL(k_enc_finish<kEncPreMax>, dim3((unsigned)a.n), dim3(kEB), 0, st, a,
+                           (const enc_half<kEncPreMax>*)halves, pre, C, status);
     return hipGetLastError();
 }
 

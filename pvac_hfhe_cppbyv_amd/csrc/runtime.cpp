@@ -101,6 +101,7 @@ struct pvac_hip_ctx {
     uint64_t last_mul_pairs = 0;       // pairs of the last ct_mul_exec (pair_status is valid for these)
     uint64_t redo_total = 0;           // pairs re-run by redo_fresh_pairs since the context was created
     uint64_t path_total[4] = {};       // pair launches: fresh kernel, general path, its iblk order, direct mode
+    double noise_bits = 120.0, noise_t2 = 0.55, noise_slope = 16.0;   // Params noise fields (enc plan_noise)
     large_desc* desc_dev = nullptr;
     size_t desc_cap = 0;
     uint32_t* sel_dev = nullptr;       // products: descriptor order per sub-batch (A-layer-major class first)
@@ -496,6 +497,16 @@ int pvac_hip_ctx_synchronize(pvac_hip_ctx* c) {
 int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* c, uint64_t* out) {
     if (!c || !out) return PVAC_EINVAL;
     *out = c->redo_total;
+    return PVAC_OK;
+}
+
+int pvac_hip_ctx_set_noise(pvac_hip_ctx* c, double noise_entropy_bits, double tuple2_fraction, double depth_slope_bits) {
+    if (!c || !(noise_entropy_bits >= 0.0) || !(tuple2_fraction >= 0.0 && tuple2_fraction <= 1.0) ||
+        !(depth_slope_bits >= 0.0) || noise_entropy_bits > 1e6 || depth_slope_bits > 1e6)
+        return fail(c, PVAC_EINVAL, "ctx_set_noise: noise_entropy_bits, depth_slope_bits >= 0, tuple2_fraction in [0, 1]");
+    c->noise_bits = noise_entropy_bits;
+    c->noise_t2 = tuple2_fraction;
+    c->noise_slope = depth_slope_bits;
     return PVAC_OK;
 }
 
@@ -1234,13 +1245,14 @@ int pvac_hip_prf(pvac_hip_ctx* c, int kind, size_t n, const uint64_t* seeds, uin
 
 // ---------------------------------------------------------------- enc_value
 namespace {
-// ops/encrypt.hpp:16-27 with the reference's default Params (noise_entropy_bits 120,
-// tuple2_fraction 0.55, depth_slope_bits 16); enc_value uses depth_hint 0
-void plan_noise(uint32_t B, int depth, uint32_t& z2, uint32_t& z3) {
-    const double budget = 120.0 + 16.0 * std::max(0, depth);
+// ops/encrypt.hpp:16-27 with the context's noise Params (the reference's defaults: noise_entropy_bits
+// 120, tuple2_fraction 0.55, depth_slope_bits 16; pvac_hip_ctx_set_noise); enc_value uses depth_hint 0
+void plan_noise(const pvac_hip_ctx* c, int depth, uint32_t& z2, uint32_t& z3) {
+    const uint32_t B = c->prm.B;
+    const double budget = c->noise_bits + c->noise_slope * std::max(0, depth);
     const double per2 = 2.0 * std::log2((double)B), per3 = 3.0 * std::log2((double)B);
-    int a = std::max(0, (int)std::floor((budget * 0.55) / std::max(1e-6, per2)));
-    int b = std::max(0, (int)std::floor((budget * (1.0 - 0.55)) / std::max(1e-6, per3)));
+    int a = std::max(0, (int)std::floor((budget * c->noise_t2) / std::max(1e-6, per2)));
+    int b = std::max(0, (int)std::floor((budget * (1.0 - c->noise_t2)) / std::max(1e-6, per3)));
     if (a + b == 1) { if (b > 0) ++b; else ++a; }
     z2 = (uint32_t)a;
     z3 = (uint32_t)b;
@@ -1255,8 +1267,9 @@ int pvac_hip_enc_caps_depth(pvac_hip_ctx* c, int depth_hint, uint32_t* layers_pe
                             uint32_t* draws_hint) {
     if (!c) return PVAC_EINVAL;
     uint32_t z2, z3;
-    plan_noise(c->prm.B, depth_hint, z2, z3);
-    if (8 + 2 * z2 + 3 * z3 > kEncPreMax) return fail(c, PVAC_ENOSYS, "enc_caps: noise plan beyond the supported group counts");
+    plan_noise(c, depth_hint, z2, z3);
+    if ((uint64_t)8 + 2ull * z2 + 3ull * z3 > kEncPreMax)
+        return fail(c, PVAC_ENOSYS, "enc_caps: noise plan beyond 256 pre-merge edges per half (depth hint > 124 with the default Params)");
     const uint32_t npre = 8 + 2 * z2 + 3 * z3;
     if (layers_per_value) *layers_per_value = 2;
     if (edges_per_value) *edges_per_value = 2 * npre;
@@ -1289,18 +1302,19 @@ int pvac_hip_enc_value_depth(pvac_hip_ctx* c, size_t n, const uint64_t* values, 
     a.rnd = rnd;
     a.stride = rnd_stride;
     a.B = c->prm.B;
-    plan_noise(c->prm.B, depth_hint, a.Z2, a.Z3);
+    plan_noise(c, depth_hint, a.Z2, a.Z3);
     a.n = n;
     a.canon = c->prm.canon_tag;
     a.powg = c->powg;
     const uint32_t npre = 8 + 2 * a.Z2 + 3 * a.Z3;
-    if (npre > kEncPreMax) return fail(c, PVAC_ENOSYS, "enc_value: noise plan beyond the supported group counts");
+    if ((uint64_t)8 + 2ull * a.Z2 + 3ull * a.Z3 > kEncPreMax)
+        return fail(c, PVAC_ENOSYS, "enc_value: noise plan beyond 256 pre-merge edges per half (depth hint > 124 with the default Params)");
     const uint64_t cores = (uint64_t)n * enc_cores_per_value(a.Z2, a.Z3);
     const uint64_t pe = (uint64_t)n * 2 * npre;
     const uint32_t sw = c->prm.m_bits / 64;
     // arena: halves | requests | cores | pre CSR (4 x n) | pre layers | meta, w_lo, w_hi, salt | sigma
     auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-    const uint64_t off_req = al((uint64_t)2 * n * enc_half_bytes());
+    const uint64_t off_req = al((uint64_t)2 * n * enc_half_bytes(npre));
     const uint64_t off_core = off_req + al(cores * prf_request_bytes());
     const uint64_t off_csr = off_core + al(cores * 16);
     const uint64_t off_lay = off_csr + al((uint64_t)n * 32);

@@ -29,6 +29,7 @@ struct Edge { uint32_t layer_id; uint16_t idx; uint8_t ch; Fp w; BitVec s; };
 struct Cipher { std::vector<Layer> L; std::vector<Edge> E; };
 struct Params {
     int B = 337, m_bits = 8192, n_bits = 16384, h_col_wt = 192, x_col_wt = 128, err_wt = 128;
+    double noise_entropy_bits = 120.0, tuple2_fraction = 0.55, depth_slope_bits = 16.0;
     size_t edge_budget = 1200000;
     int lpn_n = 4096, lpn_t = 16384, lpn_tau_num = 1, lpn_tau_den = 8;
 };

@@ -250,6 +250,8 @@ class Oracle:
         lib.orc_enc_value_depth.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSecret), u64p, u64p, C.c_uint64,
                                             C.c_int, u64p, C.c_size_t, C.c_int, C.POINTER(OrcCipher),
                                             C.POINTER(C.c_size_t)]
+        lib.orc_set_noise.argtypes = [C.c_double, C.c_double, C.c_double]
+        lib.orc_set_noise.restype = None
 
     # ---- Fp
     def fp(self, op, a_lo, a_hi, b_lo=None, b_hi=None):
@@ -369,13 +371,17 @@ class Oracle:
     def enc_value(self, sk, v, stream, powg, H=None, canon_tag=0, order=1, depth=0):
         """enc_value_depth(v, depth) (ops/encrypt.hpp:281-287); depth 0 is enc_value, v = 0 enc_zero_depth."""
         prm = default_params(canon_tag)
-        oc, ov = self._out(4, 128, H is not None)
+        oc, ov = self._out(4, 1024, H is not None)   # <= 2 x 256 pre-merge edges (depth hints <= 124)
         used = C.c_size_t()
         st = np.ascontiguousarray(stream, np.uint64)
         rc = self.lib.orc_enc_value_depth(C.byref(prm), C.byref(sk), _p(H), _p(np.ascontiguousarray(powg, np.uint64)),
                                           int(v), int(depth), _p(st), len(st), order, C.byref(ov), C.byref(used))
         assert rc == 0, rc
         return self._trim(oc, ov), used.value
+
+    def set_noise(self, noise_entropy_bits=120.0, tuple2_fraction=0.55, depth_slope_bits=16.0):
+        """plan_noise's Params fields for the following enc_value calls (process-wide)."""
+        self.lib.orc_set_noise(float(noise_entropy_bits), float(tuple2_fraction), float(depth_slope_bits))
 
     def bucket_count(self, n):
         return self.lib.orc_bucket_count_after_reserve(n)

@@ -163,8 +163,46 @@ def test_enc_value_depth_and_zero_fixtures(sigma):
         assert vals[0] == c["v"] and not dst.any(), i
 
 
+@pytest.mark.parametrize("sigma", [False, True])
+def test_enc_deep_depth_and_noise_params_fixtures(sigma):
+    """enc_value_depth / enc_zero_depth past depth hint 15 (16, 31, 60, 100: the large plan-record
+    class, up to 210 pre-merge edges per half) and with non-default noise Params set through
+    pvac_hip_ctx_set_noise (a plan with no noise group, one bumped from one group to two): byte-exact
+    .ct output against the reference's (ref_harness encdeep), sigmas included, and every case
+    decrypting to its value."""
+    import json
+    from helpers import Cipher, write_ct
+    eng, _, man, _ = _eng()
+    with open(os.path.join(REF, "encx_manifest.json")) as f:
+        fm = json.load(f)
+    for i, c in enumerate(fm["cases"]):
+        eng.set_noise(c["noise_entropy_bits"], c["tuple2_fraction"], c["depth_slope_bits"])
+        st = read_u64(f"encx{i}_stream.u64")
+        _, ep, dh = eng.enc_caps(c["depth"])
+        assert len(st) <= dh and c["edges"] <= ep, i
+        rnd = np.zeros((1, dh), np.uint64)
+        rnd[0, :len(st)] = st
+        C_, status = eng.enc_value(np.array([c["v"]], np.uint64), rnd, sigma=sigma, depth=c["depth"])
+        assert not status.any(), i
+        got = C_.to_host()[0]
+        ref = read_ct(os.path.join(REF, f"encx{i}.ct"))[0]
+        assert np.array_equal(got.meta, ref.meta) and np.array_equal(got.w_lo, ref.w_lo), i
+        assert np.array_equal(got.w_hi, ref.w_hi), i
+        if sigma:
+            with open(os.path.join(REF, f"encx{i}.ct"), "rb") as f:
+                assert write_ct([Cipher(got.layers, got.meta, got.w_lo, got.w_hi, got.sigma)]) == f.read(), i
+        vals, dst = eng.dec_value(C_, eng.base_R(C_))
+        assert vals[0] == c["v"] and not dst.any(), i
+
+
 def test_enc_depth_beyond_supported_plan_is_refused():
+    """Plans above 256 pre-merge edges per half (depth hint > 124 with the default Params) are
+    PVAC_ENOSYS; bad noise Params are PVAC_EINVAL."""
     from pvac_hfhe_cppbyv_amd import PvacError
     eng, _, _, _ = _eng()
+    assert eng.enc_caps(124)[1] <= 2 * 256
     with pytest.raises(PvacError):
-        eng.enc_caps(16)
+        eng.enc_caps(125)
+    for bad in ((-1.0, 0.55, 16.0), (120.0, 1.5, 16.0), (120.0, 0.55, -2.0), (float("nan"), 0.55, 16.0)):
+        with pytest.raises(PvacError):
+            eng.set_noise(*bad)

@@ -87,3 +87,26 @@ def test_enc_value_depth_and_zero_fixtures(oracle, key):
         assert used == len(st) == c["stream"] and got.nE == c["edges"], i
         with open(os.path.join(REF, f"encd{i}.ct"), "rb") as f:
             assert write_ct([got]) == f.read(), i
+
+
+def test_enc_deep_depth_and_noise_params_fixtures(oracle, key):
+    """enc_value_depth / enc_zero_depth past depth hint 15 (16, 31, 60, 100) and with non-default noise
+    Params (noise_entropy_bits, tuple2_fraction, depth_slope_bits), including a plan with no noise group
+    and one bumped from one group to two (plan_noise, ops/encrypt.hpp:16-27): the oracle reproduces the
+    reference's .ct bytes from the streams it consumed (ref_harness encdeep)."""
+    import json
+    sk, man, _ = key
+    H, _ = oracle.gen_H(man["canon_tag"])
+    powg = read_u64("powg_B.u64")
+    with open(os.path.join(REF, "encx_manifest.json")) as f:
+        fm = json.load(f)
+    try:
+        for i, c in enumerate(fm["cases"]):
+            oracle.set_noise(c["noise_entropy_bits"], c["tuple2_fraction"], c["depth_slope_bits"])
+            st = read_u64(f"encx{i}_stream.u64")
+            got, used = oracle.enc_value(sk, c["v"], st, powg, H=H, canon_tag=man["canon_tag"], depth=c["depth"])
+            assert used == len(st) == c["stream"] and got.nE == c["edges"], i
+            with open(os.path.join(REF, f"encx{i}.ct"), "rb") as f:
+                assert write_ct([got]) == f.read(), i
+    finally:
+        oracle.set_noise()
