@@ -266,6 +266,7 @@ __host__ __device__ inline uint32_t prod_lds_bytes(uint32_t Bm) {
 // A lane l = (m = l & 31, half h = l >> 5) byte j  x  B lane (r = l & 31, h) byte j, for the same
 // (h, j); D lane l register i = position (i & 3) + 8 (i >> 2) + 4 h of row l & 31.
 typedef int mx_v4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
 typedef int mx_v16 __attribute__((ext_vector_type(16)));
 constexpr int kMxKS = 10;                          // k-steps held in registers: 2 sparse edges each
 constexpr uint32_t kMxMaxSparse = 2u * kMxKS;      // sparse sides up to this size take the MFMA path
@@ -1524,6 +1525,10 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     const ulonglong2* wlm = (const ulonglong2*)(S + d.o_imask);   // writer lists (k_large_count_la)
     const uint32_t* wle = S + d.o_wle;
     const uint32_t* remap = S + d.o_used;  // k_large_layers left the remap here (k_large_layers ran before)
+    // C's records by buffer stores: one 32-bit offset for the three arrays, streaming (not re-read here)
+    const __amdgpu_buffer_rsrc_t rmeta = __builtin_amdgcn_make_buffer_rsrc(g.C.meta + ceo, 0, 0x7FFFFFF8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rlo = __builtin_amdgcn_make_buffer_rsrc(g.C.w_lo + ceo, 0, 0x7FFFFFF8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rhi = __builtin_amdgcn_make_buffer_rsrc(g.C.w_hi + ceo, 0, 0x7FFFFFF8, 0x00020000);
     const uint32_t i1 = min(neA, i0 + g.la_per_wg);
     // layer headers one layer ahead: the next layer's id loads during this layer's staging, its
     // list range and writer-list length during this layer's writer
@@ -1602,11 +1607,12 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                 if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
                 const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
                 const uint32_t pos = obase[l] + q;
-                const uint64_t pq = ceo + pos;
-                g.C.meta[pq] = make_meta(lidk, r, ch);
-                g.C.w_lo[pq] = w.x;
-                g.C.w_hi[pq] = w.y;
-                if (g.salt_pos) g.salt_pos[pq] = pos;
+                const uint64_t mv = make_meta(lidk, r, ch);
+                const uint32_t bo = pos * 8u;   // < 2^31: the host caps a direct pair at 2^21 A edges
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta, bo, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.x, (uint32_t)(w.x >> 32)}, rlo, bo, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.y, (uint32_t)(w.y >> 32)}, rhi, bo, 0, 2);
+                if (g.salt_pos) g.salt_pos[ceo + pos] = pos;
             }
             if (b0 + BS < nw) __syncthreads();   // the next round rewrites okey / obase
         }

@@ -211,6 +211,9 @@ struct sig_args {
 #ifdef PVAC_EXP_SIG_MID16   // experiment builds only: 16-edge midstate batches, 7 workgroups per CU
 constexpr uint32_t kMidBatch = 16;
 constexpr int kSigMinBlocks = 7;
+#elif defined(PVAC_EXP_SIG_MINB5)   // experiment builds only: 5 workgroups per CU (96 VGPRs, no spills)
+constexpr uint32_t kMidBatch = 32;
+constexpr int kSigMinBlocks = 5;
 #else
 constexpr uint32_t kMidBatch = 32;   // edges whose block-0 midstates one compression per lane covers
 constexpr int kSigMinBlocks = 6;

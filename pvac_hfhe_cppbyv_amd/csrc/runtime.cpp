@@ -638,7 +638,8 @@ int plan_static_groups(pvac_hip_ctx* c) {
         std::string why;
         large_desc x;
         rc = build_large_desc(x, d.pair, d.LA, d.LB, d.nA, d.nB, c->prm.B, why, true,
-                              !c->large_no_direct && !slots_share_bucket(d.nbm.d, d.S, c->prm.B));
+                              !c->large_no_direct && c->prm.edge_budget < (1ull << 28) &&   // 8-byte offsets < 2^31
+                                  !slots_share_bucket(d.nbm.d, d.S, c->prm.B));
         if (rc) return fail(c, rc, why);
         x.g_head = it->second;
         x.g_next = it->second + cfg[d.nbm.d];
