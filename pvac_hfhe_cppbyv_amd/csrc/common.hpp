@@ -302,7 +302,10 @@ struct large_desc {
                                  // (slice o_lstA's ids offset) the masks of its writer list
     uint64_t o_wle;              // direct pairs: [nA] writer lists, A edge | idx << 21 (k_large_count_la)
     uint64_t o_wln;              // direct pairs: [LA] writer list length per A layer
-    uint64_t words;              // end of this pair's scratch (absolute)
+    // direct pairs: o_icnt holds one count byte per A edge (32-edge groups, 32 B each, zero padded)
+    // and o_iwo [ceil(nA / 32)] each group's exclusive suffix offset (k_large_scan_direct)
+    uint64_t o_iwo;
+    uint64_t words;             // end of this pair's scratch (absolute)
 };
 
 struct mul_large_args {

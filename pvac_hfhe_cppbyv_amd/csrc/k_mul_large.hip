@@ -118,6 +118,8 @@ __device__ __forceinline__ bool iblk_dead(const uint32_t* S, const large_desc& d
 // One workgroup per pair: validates edges (layer < |L|, idx < B, ch <= 1), buckets edge ids
 // by layer (any order inside a layer: first-insert times are minima, not positions) and
 // lists the non-empty layers of both sides.
+constexpr uint32_t kListRegRounds = 8;   // rounds of 4 x kLBig A edges whose pass 2 reads registers
+static_assert(kLargeLayersMax <= (1u << 15), "k_large_lists packs a layer in 15 bits");
 __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // [LA + LB] counts, then cursors
     __shared__ uint32_t flag;
@@ -131,8 +133,11 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     for (uint32_t l = tid; l < LA + LB; l += kLBig) hist[l] = 0;
     if (tid == 0) flag = 0;
     __syncthreads();
-    // four edges per thread and round, loads first (one WG walks a pair's |A.E| edges twice)
-    for (uint32_t i0 = tid; i0 < nA; i0 += 4u * kLBig) {
+    // four edges per thread and round, loads first; the first kListRegRounds rounds keep each edge's
+    // layer and cell in registers for the scatter pass (layer < 2^15, cell < 2^11), later rounds
+    // load their metas again
+    uint32_t pk[kListRegRounds][4];
+    auto hist_round = [&](uint32_t i0, uint32_t (&pr)[4]) {
         uint64_t m[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -141,11 +146,19 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (i0 + (uint32_t)u * kLBig >= nA) break;
+            pr[u] = meta_layer(m[u]) | (meta_ch(m[u]) * Bm + meta_idx(m[u])) << 15;
+            if (i0 + (uint32_t)u * kLBig >= nA) continue;
             const uint32_t la = meta_layer(m[u]);
             if (la >= LA || meta_idx(m[u]) >= Bm || meta_ch(m[u]) > 1) flag = 1;
             else atomicAdd(&hist[la], 1u);
         }
+    };
+#pragma unroll
+    for (uint32_t r = 0; r < kListRegRounds; ++r)
+        if (tid + r * 4u * kLBig < nA) hist_round(tid + r * 4u * kLBig, pk[r]);
+    for (uint32_t i0 = tid + kListRegRounds * 4u * kLBig; i0 < nA; i0 += 4u * kLBig) {
+        uint32_t pr[4];
+        hist_round(i0, pr);
     }
     for (uint32_t j = tid; j < nB; j += kLBig) {
         const uint64_t m = g.B.meta[beo + j];
@@ -184,25 +197,36 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     __syncthreads();
     uint32_t* idsA = S + d.o_lstA + 2 * LA;
     uint32_t* idsB = S + d.o_lstB + 2 * LB;
-    if (d.direct)   // k_large_count_la stores the counts of the A edges whose ranges hold keys only
-        for (uint32_t i = tid; i < nA; i += kLBig) S[d.o_icnt + i] = 0;
+    if (d.direct) {   // k_large_count_la stores the count bytes of the A edges whose ranges hold keys only
+        uint4* z = (uint4*)(S + d.o_icnt);
+        for (uint32_t i = tid; i < 2u * ((nA + 31u) >> 5); i += kLBig) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     // direct pairs: an A id carries its dense cell, i | (ch B + idx) << 21 (the host checked
     // |A.E| < 2^21, B <= 1024), so their passes need no per-edge meta gather
     const uint32_t dsh = d.direct ? 21u : 32u;
-    for (uint32_t i0 = tid; i0 < nA; i0 += 4u * kLBig) {
+    auto scatter_round = [&](uint32_t i0, const uint32_t (&pr)[4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * kLBig;
+            if (i >= nA) break;
+            const uint64_t cell = pr[u] >> 15;
+            idsA[atomicAdd(&hist[pr[u] & 0x7FFFu], 1u)] = i | (uint32_t)((cell << dsh) & 0xFFFFFFFFull);
+        }
+    };
+#pragma unroll
+    for (uint32_t r = 0; r < kListRegRounds; ++r)
+        if (tid + r * 4u * kLBig < nA) scatter_round(tid + r * 4u * kLBig, pk[r]);
+    for (uint32_t i0 = tid + kListRegRounds * 4u * kLBig; i0 < nA; i0 += 4u * kLBig) {
         uint64_t m[4];
+        uint32_t pr[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = i0 + (uint32_t)u * kLBig;
             m[u] = i < nA ? g.A.meta[aeo + i] : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = i0 + (uint32_t)u * kLBig;
-            if (i >= nA) break;
-            const uint64_t cell = (uint64_t)(meta_ch(m[u]) * Bm + meta_idx(m[u]));
-            idsA[atomicAdd(&hist[meta_layer(m[u])], 1u)] = i | (uint32_t)((cell << dsh) & 0xFFFFFFFFull);
-        }
+        for (int u = 0; u < 4; ++u) pr[u] = meta_layer(m[u]) | (meta_ch(m[u]) * Bm + meta_idx(m[u])) << 15;
+        scatter_round(i0, pr);
     }
     for (uint32_t j = tid; j < nB; j += kLBig) {
         const uint32_t lb = meta_layer(g.B.meta[beo + j]);
@@ -853,11 +877,11 @@ struct cnt_pend {
 // iblk_layer's counts and masks for a direct pair, as the A layer's writer list: the A edges whose
 // ranges hold keys, wl[k] = A edge i | its idx << 21 and imask[k] = (P mask, M mask) in any order
 // (slots from an LDS counter), so that k_large_products_direct reads one contiguous list per A layer.
-// k_large_lists zeroed the counts; only ranges with keys store theirs. Cells beyond kPendCells per
+// k_large_lists zeroed the count bytes; only ranges with keys store theirs. Cells beyond kPendCells per
 // thread store at once. Barriers inside; every thread calls it.
 template <int BS>
 __device__ void cnt_layer_list(uint8_t* plds, uint32_t Bm, uint32_t nB, uint64_t nb_m, uint32_t nk, const uint32_t* recs,
-                               cnt_pend& p, uint32_t* icnt, uint32_t* wl, ulonglong2* imask) {
+                               cnt_pend& p, uint8_t* icnt, uint32_t* wl, ulonglong2* imask) {
     unsigned long long* M1 = (unsigned long long*)plds;
     unsigned long long* M2 = M1 + 2u * Bm;
     const uint32_t* tt = (const uint32_t*)(plds + kCntTtOff * Bm);
@@ -895,7 +919,7 @@ __device__ void cnt_layer_list(uint8_t* plds, uint32_t Bm, uint32_t nB, uint64_t
         ulonglong2 mk;
         const uint32_t k = cell(dd, i, w, mk);
         if (!k) continue;
-        icnt[i] = (uint32_t)__popcll(mk.x) + (uint32_t)__popcll(mk.y);
+        icnt[i] = (uint8_t)(__popcll(mk.x) + __popcll(mk.y));   // <= 128
         wl[k - 1u] = w;
         imask[k - 1u] = mk;
     }
@@ -903,12 +927,12 @@ __device__ void cnt_layer_list(uint8_t* plds, uint32_t Bm, uint32_t nB, uint64_t
     p.n = *wn;
 }
 
-__device__ __forceinline__ void cnt_flush(const cnt_pend& p, uint32_t* icnt, uint32_t* wl, ulonglong2* imask,
+__device__ __forceinline__ void cnt_flush(const cnt_pend& p, uint8_t* icnt, uint32_t* wl, ulonglong2* imask,
                                           uint32_t* wln) {
 #pragma unroll
     for (uint32_t u = 0; u < kPendCells; ++u) {
         if (!p.k[u]) continue;
-        icnt[p.i[u]] = (uint32_t)__popcll(p.m[u].x) + (uint32_t)__popcll(p.m[u].y);
+        icnt[p.i[u]] = (uint8_t)(__popcll(p.m[u].x) + __popcll(p.m[u].y));
         wl[p.k[u] - 1u] = p.w[u];
         imask[p.k[u] - 1u] = p.m[u];
     }
@@ -1041,7 +1065,7 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
     uint32_t pend_la = kInf, pend_base = 0;
     auto flush = [&]() {
         if (pend_la == kInf) return;   // workgroup-uniform
-        cnt_flush(pend, S + d.o_icnt, S + d.o_wle + pend_base, (ulonglong2*)(S + d.o_imask) + pend_base,
+        cnt_flush(pend, (uint8_t*)(S + d.o_icnt), S + d.o_wle + pend_base, (ulonglong2*)(S + d.o_imask) + pend_base,
                   S + d.o_wln + pend_la);
         // product layers with a key: compact_layers keeps them (benign race: every writer stores 1)
 #pragma unroll
@@ -1118,7 +1142,7 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
             if (i + 2u < i1) la_n2 = S[d.o_neA + i + 2u];
         }
         const uint32_t lbase = late(st_c);   // the layer's list slice: as its edge ids
-        cnt_layer_list<BS>(plds, Bm, nB, d.nb_m, neB * Bm, recs, pend, S + d.o_icnt, S + d.o_wle + lbase,
+        cnt_layer_list<BS>(plds, Bm, nB, d.nb_m, neB * Bm, recs, pend, (uint8_t*)(S + d.o_icnt), S + d.o_wle + lbase,
                            (ulonglong2*)(S + d.o_imask) + lbase);
         pend.used = usedm;
         pend_la = la;
@@ -1141,9 +1165,29 @@ __global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
 #endif
 }
 
+// count bytes of a direct pair's A edges (4 per word): their sum, and the sum over the bytes of a
+// 32-edge group at positions above b (the word holding positions lo .. lo + 3)
+__device__ __forceinline__ uint32_t byte_sum(uint32_t x) { return __builtin_amdgcn_sad_u8(x, 0u, 0u); }
+__device__ __forceinline__ uint32_t byte_sum(const uint4& x) {
+    return __builtin_amdgcn_sad_u8(x.x, 0u, __builtin_amdgcn_sad_u8(x.y, 0u, __builtin_amdgcn_sad_u8(x.z, 0u, byte_sum(x.w))));
+}
+__device__ __forceinline__ uint32_t bytes_above(uint32_t x, uint32_t lo, uint32_t b) {
+    const uint32_t m = b < lo ? 0xFFFFFFFFu : b >= lo + 3u ? 0u : 0xFFFFFFFFu << (8u * (b - lo + 1u));
+    return byte_sum(x & m);
+}
+// an A edge's exclusive suffix offset: its group's offset plus the counts of the group's later edges
+__device__ __forceinline__ uint32_t dir_edge_off(const uint4* c8, const uint32_t* wo, uint32_t e) {
+    const uint32_t gi = e >> 5, b = e & 31u;
+    const uint4 a = c8[2u * gi], c = c8[2u * gi + 1u];
+    return wo[gi] + bytes_above(a.x, 0u, b) + bytes_above(a.y, 4u, b) + bytes_above(a.z, 8u, b) +
+           bytes_above(a.w, 12u, b) + bytes_above(c.x, 16u, b) + bytes_above(c.y, 20u, b) + bytes_above(c.z, 24u, b) +
+           bytes_above(c.w, 28u, b);
+}
+
 // Pass 2 of a direct pair, one workgroup per pair: the total, the guard_budget decision, and the
-// per-A-edge counts turned into exclusive suffix offsets (as k_large_scan). A pair with shared
-// buckets, a fallback or the canonical order is not direct after all: it goes to the host's redo.
+// per-A-edge count bytes turned into exclusive suffix offsets per 32-edge group (an edge's own
+// offset adds its group's later bytes: dir_edge_off). A pair with shared buckets, a fallback or
+// the canonical order is not direct after all: it goes to the host's redo.
 __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
     __shared__ uint32_t part[kLBig / 64];
     const large_desc& d = g.desc[blockIdx.x];
@@ -1152,10 +1196,11 @@ __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
     uint32_t* cnt = S + d.o_cnt;
     if (cnt[2]) return;
     const int tid = threadIdx.x;
-    uint32_t* icnt = S + d.o_icnt;
-    const uint32_t nA = d.nA;
-    // one pass: the suffix offsets are written while the total accumulates; a pair that is not
-    // direct after all (checked after the pass) is redone, so offsets written for it are never read
+    const uint4* c8 = (const uint4*)(S + d.o_icnt);   // count bytes, two uint4 per group of 32 A edges
+    uint32_t* wo = S + d.o_iwo;
+    const uint32_t ng = (d.nA + 31u) >> 5;
+    // one pass: the groups' suffix offsets are written while the total accumulates; a pair that is
+    // not direct after all (checked after the pass) is redone, so offsets written for it are never read
     if (cnt[kCntIFail] || cnt[kCntIShared] || (g.flags & PVAC_MUL_ORDER_CANONICAL) != 0) {
         if (tid == 0) {
             cnt[kCntRedo] = 1;
@@ -1164,14 +1209,20 @@ __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
         return;
     }
     uint32_t run0 = 0;
-    for (uint32_t base = 0; base < nA; base += 4u * kLBig) {
+    for (uint32_t base = 0; base < ng; base += 4u * kLBig) {
         const uint32_t r0 = base + 4u * (uint32_t)tid;
+        uint4 x[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // loads first
+            const uint32_t r = r0 + (uint32_t)k, w = ng - 1u - r;
+            x[2 * k] = r < ng ? c8[2u * w] : make_uint4(0u, 0u, 0u, 0u);
+            x[2 * k + 1] = r < ng ? c8[2u * w + 1u] : make_uint4(0u, 0u, 0u, 0u);
+        }
         uint32_t v[4];
         uint32_t local = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t r = r0 + (uint32_t)k;
-            v[k] = r < nA ? icnt[nA - 1 - r] : 0u;
+            v[k] = byte_sum(x[2 * k]) + byte_sum(x[2 * k + 1]);
             local += v[k];
         }
         uint32_t tot;
@@ -1179,7 +1230,7 @@ __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t r = r0 + (uint32_t)k;
-            if (r < nA) icnt[nA - 1 - r] = run;
+            if (r < ng) wo[ng - 1u - r] = run;
             run += v[k];
         }
         run0 += tot;
@@ -1521,7 +1572,8 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
             if (k < neB && lbv[k] == lb) kk = k;
         bjt[tid] = meta_idx(g.B.meta[beo + tid]) | kk << 12 | lb << 16;
     }
-    const uint32_t* off = S + d.o_icnt;   // exclusive suffix offsets (k_large_scan_direct)
+    const uint4* c8 = (const uint4*)(S + d.o_icnt);   // count bytes (k_large_count_la)
+    const uint32_t* wo = S + d.o_iwo;                 // group offsets (k_large_scan_direct)
     const ulonglong2* wlm = (const ulonglong2*)(S + d.o_imask);   // writer lists (k_large_count_la)
     const uint32_t* wle = S + d.o_wle;
     const uint32_t* remap = S + d.o_used;  // k_large_layers left the remap here (k_large_layers ran before)
@@ -1575,7 +1627,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
             const uint32_t we = lv ? wle[lbase + kq] : 0u;
             const ulonglong2 mk = lv ? wlm[lbase + kq] : make_ulonglong2(0ull, 0ull);
             const uint32_t e = we & 0x1FFFFFu;
-            const uint32_t oi = lv ? off[e] : 0u;
+            const uint32_t oi = lv ? dir_edge_off(c8, wo, e) : 0u;
             const uint64_t mp = mk.x & ~(1ull << 63), mm = mk.y;   // bit 63: a shared bucket (such pairs are redone)
             uint32_t T;
             const uint32_t excl = wg_exclusive_scan<BS>((uint32_t)__popcll(mp) + (uint32_t)__popcll(mm), part, T);

@@ -329,7 +329,10 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
         d.o_neA = o; o += LA;
         d.o_neB = o; o += LB;
         d.o_defer = d.o_info = d.o_sums = d.o_nxt = d.o_tb = d.o_within = d.o_etot = d.o_cpos = d.o_order = d.o_hpos = o;
-        d.o_icnt = o; o += nA;
+        const uint64_t ngrp = (nA + 31) / 32;
+        quad();
+        d.o_icnt = o; o += 8 * ngrp;   // count bytes
+        d.o_iwo = o; o += ngrp;
         d.o_wle = o; o += nA;
         d.o_wln = o; o += LA;
         quad();
@@ -369,7 +372,7 @@ int build_large_desc(large_desc& d, uint64_t pair, uint64_t LA, uint64_t LB, uin
     quad();
     d.o_imask = o; o += d.iblk ? 4 * nA : 0;
     quad();
-    d.o_wle = d.o_wln = o;
+    d.o_wle = d.o_wln = d.o_iwo = o;
     d.words = o;
     return PVAC_OK;
 }
@@ -378,7 +381,7 @@ void rebase_desc(large_desc& d, uint64_t base) {
     uint64_t* f[] = {&d.o_zero, &d.o_cnt, &d.o_hkey, &d.o_hhead, &d.o_bmask, &d.o_bcnt, &d.o_used, &d.o_tkey,
                      &d.o_lstA, &d.o_lstB, &d.o_neA, &d.o_neB, &d.o_defer, &d.o_info, &d.o_sums, &d.o_nxt, &d.o_tb,
                      &d.o_within, &d.o_etot, &d.o_cpos, &d.o_order, &d.o_hpos, &d.o_icnt, &d.o_imask,
-                     &d.o_wle, &d.o_wln};
+                     &d.o_wle, &d.o_wln, &d.o_iwo};
     for (uint64_t* p : f) *p += base;
 }
 
