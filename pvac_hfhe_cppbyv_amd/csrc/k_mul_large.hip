@@ -1526,6 +1526,12 @@ __device__ void dir_rows(const uint4* dig, const uint4* prec, const uint4* pinf,
     }
 }
 
+// cache policy bits of the products kernel's record stores. Streaming (2) was measured against the
+// default (0) on the cfg-4 chain: HBM writes 84.4 against 70.8 GB per 4096 inputs (lines leave L2
+// before their neighbours' records fill them, then go out again), reads 47.2 against 58.5, time equal
+#ifndef PVAC_DIR_STORE_AUX
+#define PVAC_DIR_STORE_AUX 0
+#endif
 template <int BS>
 __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
@@ -1577,7 +1583,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     const ulonglong2* wlm = (const ulonglong2*)(S + d.o_imask);   // writer lists (k_large_count_la)
     const uint32_t* wle = S + d.o_wle;
     const uint32_t* remap = S + d.o_used;  // k_large_layers left the remap here (k_large_layers ran before)
-    // C's records by buffer stores: one 32-bit offset for the three arrays, streaming (not re-read here)
+    // C's records by buffer stores: one 32-bit offset for the three arrays
     const __amdgpu_buffer_rsrc_t rmeta = __builtin_amdgcn_make_buffer_rsrc(g.C.meta + ceo, 0, 0x7FFFFFF8, 0x00020000);
     const __amdgpu_buffer_rsrc_t rlo = __builtin_amdgcn_make_buffer_rsrc(g.C.w_lo + ceo, 0, 0x7FFFFFF8, 0x00020000);
     const __amdgpu_buffer_rsrc_t rhi = __builtin_amdgcn_make_buffer_rsrc(g.C.w_hi + ceo, 0, 0x7FFFFFF8, 0x00020000);
@@ -1661,9 +1667,9 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                 const uint32_t pos = obase[l] + q;
                 const uint64_t mv = make_meta(lidk, r, ch);
                 const uint32_t bo = pos * 8u;   // < 2^31: the host caps a direct pair at 2^21 A edges
-                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta, bo, 0, 2);
-                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.x, (uint32_t)(w.x >> 32)}, rlo, bo, 0, 2);
-                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.y, (uint32_t)(w.y >> 32)}, rhi, bo, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta, bo, 0, PVAC_DIR_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.x, (uint32_t)(w.x >> 32)}, rlo, bo, 0, PVAC_DIR_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.y, (uint32_t)(w.y >> 32)}, rhi, bo, 0, PVAC_DIR_STORE_AUX);
                 if (g.salt_pos) g.salt_pos[ceo + pos] = pos;
             }
             if (b0 + BS < nw) __syncthreads();   // the next round rewrites okey / obase
