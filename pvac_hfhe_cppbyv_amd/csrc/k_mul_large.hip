@@ -985,7 +985,12 @@ __device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t
 // matrix-core mode cannot take (duplicate edges, fewer than kLargeDenseMin edges) fails the pair
 // (cnt[kCntIFail]): k_large_scan_direct sends it to the host's redo.
 template <int BS>
-__global__ __launch_bounds__(BS) void k_large_count_la(mul_large_args g) {
+// resident workgroups per CU k_large_count_la is compiled for: 6 (<= 80 VGPRs, no spills) against
+// 5 (81 VGPRs unconstrained): cfg-4 chain 195 K against 188-190 K ct_mul/s on one stream; 7 spills
+#ifndef PVAC_CNT_MINB
+#define PVAC_CNT_MINB 6
+#endif
+__global__ __launch_bounds__(BS, PVAC_CNT_MINB) void k_large_count_la(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint8_t plds[];
     const large_desc d = g.desc[g.sel[blockIdx.y]];   // registers (the kernel's stores could alias it)
     if (!d.direct) return;
