@@ -69,6 +69,32 @@ def test_chain_api_equals_stepwise_and_oracle(oracle):
     assert np.array_equal(r2["digests"], dig) and r2["gsum_pairs"] == 0
 
 
+def test_chain_depth8_vs_oracle(oracle):
+    """cfg 4's full depth on a few chains: steps 3-8 run the direct mode, and from step 7 on the A
+    operand holds more edges than k_large_lists keeps in registers (its later rounds re-read the
+    metas) and spans many 32-edge count groups; final digests and counts equal the CPU port's."""
+    from pvac_hfhe_cppbyv_amd import Engine
+    sk, man, em = fixture_secret()
+    eng = Engine(device=0, canon_tag=man["canon_tag"])
+    assert eng.gen_H().hex() == man["H_digest"]
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    eng.set_powg(read_u64("powg_B.u64"))
+    rng = np.random.default_rng(0xD8)
+    n, depth = 3, 8
+    X, st = eng.enc_value(rng.integers(0, 2**64, n, dtype=np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    r = eng.ct_mul_chain(X, depth, nonce_seed=0xD8, streams=2, chunk=2, check_gsum=True, digest_n=n)
+    assert r["gsum_pairs"] == n * depth and r["gsum_failed"] == 0 and r["redo"] == 0
+    assert r["edges"][5] > n * 4 * 8192   # step 7's A operands: > 32 K edges each
+    px = pack_device_batch(X, n)
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
+    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(man["canon_tag"])), n, *(P_(a) for a in px), depth, 8,
+                                      P_(ocnt), P_(odig), P_(se))
+    assert np.array_equal(ocnt, r["counts"]) and np.array_equal(odig, r["digests"])
+
+
 def test_chain_api_callbacks_and_errors():
     """fill_nonces / on_chunk callbacks from the worker threads: every chunk arrives once with its
     first input and size, the nonces come from the callback (different nonces, same edges: a digest
