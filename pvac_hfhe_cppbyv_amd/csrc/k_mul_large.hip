@@ -118,7 +118,10 @@ __device__ __forceinline__ bool iblk_dead(const uint32_t* S, const large_desc& d
 // One workgroup per pair: validates edges (layer < |L|, idx < B, ch <= 1), buckets edge ids
 // by layer (any order inside a layer: first-insert times are minima, not positions) and
 // lists the non-empty layers of both sides.
-constexpr uint32_t kListRegRounds = 8;   // rounds of 4 x kLBig A edges whose pass 2 reads registers
+#ifndef PVAC_LIST_REG_ROUNDS   // rounds of 4 x kLBig A edges whose pass 2 reads registers
+#define PVAC_LIST_REG_ROUNDS 8
+#endif
+constexpr uint32_t kListRegRounds = PVAC_LIST_REG_ROUNDS;
 static_assert(kLargeLayersMax <= (1u << 15), "k_large_lists packs a layer in 15 bits");
 __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // [LA + LB] counts, then cursors
