@@ -136,6 +136,15 @@ int pvac_hip_ctx_gen_H(pvac_hip_ctx* ctx, uint8_t digest_out[32]);
  * 5 = general-path dense-mode products on the matrix cores (v_mfma_i32_32x32x32_i8 rate x 64).
  * Synchronous. */
 int pvac_hip_alu_ceiling(pvac_hip_ctx* ctx, int kind, double* per_s);
+/* Per-opcode VALU issue probe (k_ubench.hip): one opcode alone on 16 independent accumulators per
+ * lane, waves_per_simd (1..8) waves on every SIMD. Returns wave64 instructions per second chip-wide
+ * and the shader clock the SIMDs ran at during the same launch (s_memtime ticks per s_memrealtime
+ * tick x 100 MHz, median over workgroups), so cycles per instruction = SIMDs x clock / per_s.
+ * op: 0 v_add_u32, 1 v_xor_b32, 2 v_alignbit_b32, 3 v_lshlrev_b32, 4 v_min_u32, 5 v_add3_u32,
+ * 6 v_pk_add_u16, 7 v_fma_f32, 8 v_mul_lo_u32, 9 v_mul_hi_u32, 10 v_cndmask_b32, 11 v_bfe_u32,
+ * 12 v_add_co_u32, 13 v_and_or_b32, 14 v_pk_min_u16, 15 v_bitop3_b32, 16 v_mad_u64_u32.
+ * Measurement only (never used by an op). Synchronous. */
+int pvac_hip_issue_probe(pvac_hip_ctx* ctx, int op, int waves_per_simd, double* per_s, double* clock_hz);
 /* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */
 int pvac_hip_timing_enable(pvac_hip_ctx* ctx, int on);
 /* kernel_name: "fp_binop", "ct_mul_small", "ct_mul_large", "ct_add", "sigma", ... ; returns

@@ -123,6 +123,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_ct_mul_status": ([vp, vp, C.c_size_t], i32),
         "pvac_hip_ct_mul_chain": ([vp, C.POINTER(CtBatch), C.POINTER(ChainOpts), C.POINTER(ChainStats)], i32),
         "pvac_hip_alu_ceiling": ([vp, i32, C.POINTER(C.c_double)], i32),
+        "pvac_hip_issue_probe": ([vp, i32, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)], i32),
         "pvac_hip_check_mul_gsum": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
                                      C.POINTER(u64)], i32),
         "pvac_hip_ct_add_plan": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch),
@@ -469,6 +470,19 @@ class Engine:
         v = C.c_double(0)
         self._check(self.lib.pvac_hip_alu_ceiling(self.ctx, kind, C.byref(v)))
         return v.value
+
+    ISSUE_OPS = ("v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_lshlrev_b32", "v_min_u32", "v_add3_u32",
+                 "v_pk_add_u16", "v_fma_f32", "v_mul_lo_u32", "v_mul_hi_u32", "v_cndmask_b32", "v_bfe_u32",
+                 "v_add_co_u32", "v_and_or_b32", "v_pk_min_u16", "v_bitop3_b32", "v_mad_u64_u32")
+
+    def issue_probe(self, op, waves_per_simd=8):
+        """Per-opcode VALU issue rate (pvac_hip_issue_probe): (wave64 inst/s chip-wide, shader clock Hz
+        measured in the same launch). `op` is an index or a name of ISSUE_OPS."""
+        if isinstance(op, str):
+            op = self.ISSUE_OPS.index(op)
+        v, hz = C.c_double(0), C.c_double(0)
+        self._check(self.lib.pvac_hip_issue_probe(self.ctx, op, waves_per_simd, C.byref(v), C.byref(hz)))
+        return v.value, hz.value
 
     def check_mul_gsum(self, A: DeviceBatch, B: DeviceBatch, C_: DeviceBatch, nonces, status=False):
         """The reference's gsum invariant (utils/metrics.hpp:88-113) on every pair of a ct_mul

@@ -350,6 +350,7 @@ hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
 uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl);
 // measured integer-ALU ceilings (k_ubench.hip)
 hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s);
+hipError_t run_issue_probe(int op, int wps, int num_cus, hipStream_t st, double* per_s, double* clock_hz);
 // ct_mul gsum invariant (k_check.hip, utils/metrics.hpp:70-113)
 hipError_t launch_check_sizes(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C, unsigned int* mx,
                               hipStream_t st);

@@ -12,6 +12,11 @@
 //   kind 3: column-accumulated products (col26_mac: 25 v_mad_u64_u32 into nine u64 columns, the
 //           general path's dense loop since round 2) per second, two accumulators per lane
 // Grids fill every CU at 8 waves per SIMD. Used by measurement only, never by the ct_* ops.
+#include <algorithm>
+#include <array>
+#include <utility>
+#include <vector>
+
 #include "common.hpp"
 
 namespace pvhip {
@@ -183,7 +188,135 @@ __global__ __launch_bounds__(kUB) void k_probe_mfma8(uint64_t* out, uint32_t ite
     out[(uint64_t)blockIdx.x * kUB + threadIdx.x] = (uint32_t)r;
 }
 
+// ---------------------------------------------------------------- per-opcode issue probe
+// One opcode alone, 16 independent accumulators per lane (16 instructions per iteration, each
+// depending only on its own previous value), `wps` waves per SIMD on every CU. Thread 0 of every
+// workgroup records s_memtime (shader clock) and s_memrealtime (100 MHz) at its start and end, so
+// the host gets the clock the SIMDs actually ran at next to the instruction rate: cycles per
+// wave64 instruction = (SIMDs x shader clock) / (instructions per second).
+#define PVAC_IP16(OPS)                                                                                       \
+    asm volatile(OPS                                                                                         \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]),       \
+                   "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]),   \
+                   "+v"(r[14]), "+v"(r[15])                                                                  \
+                 : "v"(a), "v"(b)                                                                            \
+                 : "vcc")
+#define PVAC_IPS(I, T0, T1, T2, T3)                                                                         \
+    I " %0," T0 "\n\t" I " %1," T1 "\n\t" I " %2," T2 "\n\t" I " %3," T3 "\n\t" I " %4," T0 "\n\t" I " %5," \
+    T1 "\n\t" I " %6," T2 "\n\t" I " %7," T3 "\n\t" I " %8," T0 "\n\t" I " %9," T1 "\n\t" I " %10," T2   \
+    "\n\t" I " %11," T3 "\n\t" I " %12," T0 "\n\t" I " %13," T1 "\n\t" I " %14," T2 "\n\t" I " %15," T3
+
+template <int OP>
+__global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint32_t seed) {
+    const uint32_t a = threadIdx.x ^ seed, b = a * 2654435761u + 1u;
+    uint32_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = a * (k + 3) + b;
+    uint64_t t0 = 0, q0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        q0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (uint32_t i = 0; i < iters; ++i) {
+        // each accumulator's operands: itself and the loop-invariant a / b (16 independent chains)
+        if constexpr (OP == 0) PVAC_IP16(PVAC_IPS("v_add_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 1) PVAC_IP16(PVAC_IPS("v_xor_b32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 2) PVAC_IP16(PVAC_IPS("v_alignbit_b32", "%0,%16,7", "%1,%17,7", "%2,%16,9", "%3,%17,9"));
+        if constexpr (OP == 3) PVAC_IP16(PVAC_IPS("v_lshlrev_b32", "%16,%0", "%17,%1", "%16,%2", "%17,%3"));
+        if constexpr (OP == 4) PVAC_IP16(PVAC_IPS("v_min_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 5) PVAC_IP16(PVAC_IPS("v_add3_u32", "%0,%16,%17", "%1,%17,%16", "%2,%16,%16", "%3,%17,%17"));
+        if constexpr (OP == 6) PVAC_IP16(PVAC_IPS("v_pk_add_u16", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 7) PVAC_IP16(PVAC_IPS("v_fma_f32", "%0,%16,%17", "%1,%17,%16", "%2,%16,%16", "%3,%17,%17"));
+        if constexpr (OP == 8) PVAC_IP16(PVAC_IPS("v_mul_lo_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 9) PVAC_IP16(PVAC_IPS("v_mul_hi_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 10) PVAC_IP16(PVAC_IPS("v_cndmask_b32", "%0,%16,vcc", "%1,%17,vcc", "%2,%16,vcc", "%3,%17,vcc"));
+        if constexpr (OP == 11) PVAC_IP16(PVAC_IPS("v_bfe_u32", "%0,%16,12", "%1,%17,12", "%2,%16,12", "%3,%17,12"));
+        if constexpr (OP == 12) PVAC_IP16(PVAC_IPS("v_add_co_u32", "vcc,%0,%16", "vcc,%1,%17", "vcc,%2,%16", "vcc,%3,%17"));
+        if constexpr (OP == 13) PVAC_IP16(PVAC_IPS("v_and_or_b32", "%0,%16,%17", "%1,%17,%16", "%2,%16,%16", "%3,%17,%17"));
+        if constexpr (OP == 14) PVAC_IP16(PVAC_IPS("v_pk_min_u16", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
+        if constexpr (OP == 15) PVAC_IP16(PVAC_IPS("v_bitop3_b32", "%0,%16,%17 bitop3:0x96", "%1,%17,%16 bitop3:0x96",
+                                                   "%2,%16,%16 bitop3:0x96", "%3,%17,%17 bitop3:0x96"));
+        if constexpr (OP == 16) {
+            // v_mad_u64_u32 on 8 64-bit accumulators (register pairs r[2k], r[2k + 1]): 8 per iteration
+            uint64_t* x = (uint64_t*)r;
+            asm volatile(
+                "v_mad_u64_u32 %0, vcc, %8, %9, %0\n\tv_mad_u64_u32 %1, vcc, %9, %8, %1\n\t"
+                "v_mad_u64_u32 %2, vcc, %8, %8, %2\n\tv_mad_u64_u32 %3, vcc, %9, %9, %3\n\t"
+                "v_mad_u64_u32 %4, vcc, %8, %9, %4\n\tv_mad_u64_u32 %5, vcc, %9, %8, %5\n\t"
+                "v_mad_u64_u32 %6, vcc, %8, %8, %6\n\tv_mad_u64_u32 %7, vcc, %9, %9, %7"
+                : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                : "v"(a), "v"(b)
+                : "vcc");
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc ^= r[k];
+    out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    if (threadIdx.x == 0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = q1 - q0;
+    }
+}
+#undef PVAC_IP16
+#undef PVAC_IPS
+
+constexpr int kIssueOps = 17;
+using probe_fn = void (*)(uint64_t*, uint64_t*, uint32_t, uint32_t);
+template <int... I>
+constexpr auto issue_table(std::integer_sequence<int, I...>) {
+    return std::array<probe_fn, sizeof...(I)>{&k_probe_issue<I>...};
+}
+
 }  // namespace
+
+// Per-opcode VALU issue probe (pvac_hip_issue_probe): wave64 instructions per second chip-wide and
+// the shader clock measured inside the same launch (median over workgroups of s_memtime ticks per
+// s_memrealtime tick x 100 MHz). The launch fills every CU with `wps` waves per SIMD.
+hipError_t run_issue_probe(int op, int wps, int num_cus, hipStream_t st, double* per_s, double* clock_hz) {
+    static const auto table = issue_table(std::make_integer_sequence<int, kIssueOps>{});
+    if (op < 0 || op >= kIssueOps || wps < 1 || wps > 8) return hipErrorInvalidValue;
+    const uint32_t threads = 256u;                                      // 4 waves: one per SIMD
+    const uint32_t blocks = (uint32_t)num_cus * (uint32_t)wps;          // wps workgroups per CU
+    const uint32_t iters = 8192u;
+    const double per_iter = op == 16 ? 8.0 : 16.0;
+    uint64_t *buf = nullptr, *clk = nullptr;
+    hipError_t e = hipMalloc(&buf, (size_t)blocks * threads * 8);
+    if (e == hipSuccess) e = hipMalloc(&clk, (size_t)blocks * 16);
+    if (e != hipSuccess) {
+        hipFree(buf);
+        return e;
+    }
+    hipEvent_t t0, t1;
+    hipEventCreate(&t0);
+    hipEventCreate(&t1);
+    float ms = 0;
+    for (int rep = 0; rep < 3; ++rep) {   // the first launches warm clocks and code
+        hipEventRecord(t0, st);
+        hipLaunchKernelGGL(table[op], dim3(blocks), dim3(threads), 0, st, buf, clk, iters, 0x5EEDu + rep);
+        hipEventRecord(t1, st);
+    }
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventSynchronize(t1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
+    std::vector<uint64_t> h((size_t)blocks * 2);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost);
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    hipFree(buf);
+    hipFree(clk);
+    if (e != hipSuccess) return e;
+    std::vector<double> hz;
+    hz.reserve(blocks);
+    for (uint32_t k = 0; k < blocks; ++k)
+        if (h[2 * k + 1]) hz.push_back((double)h[2 * k] / (double)h[2 * k + 1] * 1.0e8);
+    std::sort(hz.begin(), hz.end());
+    *clock_hz = hz.empty() ? 0.0 : hz[hz.size() / 2];
+    const double insts = (double)blocks * (threads / 64) * iters * per_iter;
+    *per_s = ms > 0 ? insts / (ms / 1000.0) : 0.0;
+    return hipSuccess;
+}
 
 // ops per second of probe `kind` (see above), timed with HIP events on `st` (synchronises)
 hipError_t run_alu_probe(int kind, int num_cus, hipStream_t st, double* per_s) {

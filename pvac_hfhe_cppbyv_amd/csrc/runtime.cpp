@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <new>
 #include <mutex>
 #include <string>
@@ -569,13 +570,14 @@ namespace {
 // reference's 0x9E3779B97F4A7C15, arithmetic.hpp:72-77). A pair whose slots can share a bucket is not
 // taken in the direct mode (its emit order then needs bucket leaders across A layers): chain step 2
 // (|A.L| = 8, bucket counts near 49 K) has hundreds of such buckets, deeper steps none (the structured
-// keys (lp << 32) | r spread perfectly there). Memoised per (nb, S): chunks of one step repeat them.
+// keys (lp << 32) | r spread perfectly there). Memoised per (nb, S, B): chunks of one step repeat them,
+// and the slot -> key map depends on B (two contexts with different B can meet the same (nb, S)).
 bool slots_share_bucket(uint64_t nb, uint64_t S, uint32_t Bm) {
     static std::mutex mu;
-    static std::map<std::pair<uint64_t, uint64_t>, bool> memo;
+    static std::map<std::tuple<uint64_t, uint64_t, uint32_t>, bool> memo;
     {
         std::lock_guard<std::mutex> g(mu);
-        auto it = memo.find({nb, S});
+        auto it = memo.find({nb, S, Bm});
         if (it != memo.end()) return it->second;
     }
     bool shared = false;
@@ -592,7 +594,7 @@ bool slots_share_bucket(uint64_t nb, uint64_t S, uint32_t Bm) {
         }
     }
     std::lock_guard<std::mutex> g(mu);
-    memo[{nb, S}] = shared;
+    memo[{nb, S, Bm}] = shared;
     return shared;
 }
 
@@ -758,6 +760,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         uint64_t mS = 0, mZ = 0, mT = 0, mE = 0, mL = 0, mTa = 0, mLa = 0, mA = 0;
         bool dyn = false, all_ib = true, any_dir = false, all_dir = true;
         uint32_t mLBd = 0;
+        uint64_t n_ib = 0, n_dir = 0;   // path counters, added once the sub-batch has launched
         while (j < nl && (j == i || words + c->large_exec[j].words <= budget) && j - i < 65535) {
             large_desc& d = c->large_exec[j];
             const uint64_t w = d.words;
@@ -774,9 +777,8 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
             all_ib &= d.iblk != 0;
             any_dir |= d.direct != 0;
             all_dir &= d.direct != 0;
-            ++c->path_total[1];
-            c->path_total[2] += d.iblk;
-            c->path_total[3] += d.direct;
+            n_ib += d.iblk;
+            n_dir += d.direct;
             if (d.direct) mLBd = std::max<uint32_t>(mLBd, d.LB);
             mL = std::max(mL, std::max<uint64_t>(d.Lc, (uint64_t)d.LA + d.LB));
             ++j;
@@ -859,6 +861,9 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.la_xcd = la_xcd;
         e = launch_ct_mul_large(a, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "ct_mul_large");
+        c->path_total[1] += j - i;
+        c->path_total[2] += n_ib;
+        c->path_total[3] += n_dir;
         i = j;
     }
     return PVAC_OK;
@@ -974,6 +979,19 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         scoped_timer t(c, "ct_mul_fresh");
         e = launch_ct_mul_fresh(a, c->fresh_args, c->num_cus, c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "ct_mul_fresh");
+    }
+    if (plan->n_large && (flags & PVAC_MUL_ORDER_CANONICAL) &&
+        std::any_of(c->large_host.begin(), c->large_host.end(), [](const large_desc& d) { return d.direct != 0; })) {
+        // the direct mode emits hash order only: with the canonical order asked for, its pairs would
+        // all be redone, so take them on the full layout from the start (descriptors rebuilt once;
+        // the plan stays valid, its direct pairs now run the exact path)
+        c->large_no_direct = true;
+        const int rc = plan_static_groups(c);
+        c->large_no_direct = false;
+        if (rc) {
+            ++c->plan_stamp;
+            return rc;
+        }
     }
     if (plan->n_large) {
         scoped_timer t(c, "ct_mul_large");
@@ -1384,6 +1402,12 @@ int pvac_hip_alu_ceiling(pvac_hip_ctx* c, int kind, double* per_s) {
     if (!c || !per_s || kind < 0 || kind > 5) return fail(c, PVAC_EINVAL, "alu_ceiling: bad arguments");
     const hipError_t e = run_alu_probe(kind, c->num_cus, c->stream, per_s);
     return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "alu_ceiling");
+}
+
+int pvac_hip_issue_probe(pvac_hip_ctx* c, int op, int waves_per_simd, double* per_s, double* clock_hz) {
+    if (!c || !per_s || !clock_hz) return fail(c, PVAC_EINVAL, "issue_probe: bad arguments");
+    const hipError_t e = run_issue_probe(op, waves_per_simd, c->num_cus, c->stream, per_s, clock_hz);
+    return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "issue_probe");
 }
 
 // ---------------------------------------------------------------- gsum invariant

@@ -421,3 +421,43 @@ def pack_device_batch(X, k):
     cs = np.ascontiguousarray
     return (cs(u(lo)), cs(X.layers[li].cpu().numpy()), cs(u(eo)), cs(u(X.meta[ei])), cs(u(X.w_lo[ei])),
             cs(u(X.w_hi[ei])))
+
+
+_HIP = None
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        _HIP = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+        _HIP.hipStreamSynchronize.argtypes = [C.c_void_p]
+        _HIP.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    return _HIP
+
+
+def hip_batch_to_host(b, stream, sigma_words=0):
+    """Copy a device pvac_ct_batch (a CtBatch struct handed to a chain's on_chunk callback, whose
+    arrays live only during the callback) to host ciphers: synchronises `stream`, then plain
+    hipMemcpy device-to-host of the counts/offsets and each cipher's rows. Test helper."""
+    hip = _hip()
+    assert hip.hipStreamSynchronize(C.c_void_p(stream)) == 0
+    n = int(b.n)
+
+    def d2h(ptr, count, dtype, off=0, width=1):
+        out = np.zeros(count * width, dtype)
+        if count:
+            assert hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr + off * width * out.itemsize),
+                                 out.nbytes, 2) == 0   # hipMemcpyDeviceToHost
+        return out
+
+    lo, lc = d2h(b.l_off, n, np.uint64), d2h(b.l_cnt, n, np.uint64)
+    eo, ec = d2h(b.e_off, n, np.uint64), d2h(b.e_cnt, n, np.uint64)
+    out = []
+    for i in range(n):
+        L = d2h(b.layers, int(lc[i]), np.uint8, int(lo[i]), 40).view(LAYER_DT)
+        args = [d2h(p, int(ec[i]), np.uint64, int(eo[i])) for p in (b.meta, b.w_lo, b.w_hi)]
+        sg = None
+        if sigma_words and b.sigma:
+            sg = d2h(b.sigma, int(ec[i]), np.uint64, int(eo[i]), sigma_words).reshape(-1, sigma_words)
+        out.append(Cipher(L, *args, sg))
+    return out

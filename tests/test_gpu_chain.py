@@ -159,3 +159,52 @@ def test_chain_api_callbacks_and_errors():
     r3 = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n)
     assert np.array_equal(r3["digests"], base["digests"])
     torch.cuda.synchronize()
+
+
+def test_reference_chain_2_pow_10_on_gpu(oracle):
+    """The reference's own end-to-end chain check (tests/test_main.cpp:289-293: enc_value(2), nine
+    ct_mul steps, dec_value == 2^10), all on the GPU through the chain entry point: x = enc_value(2)
+    per chain (GPU PRF), c_0 = x, c_k = ct_mul(c_{k-1}, x) for 9 steps through pvac_hip_ct_mul_chain
+    (step 9's A operands hold ~340 K edges, its outputs ~690 K), the final ciphers taken from the
+    on_chunk callback, then base_R (prf_R of the BASE layers) and dec_value: every chain decrypts to
+    2^10. The depth-9 digests and edge counts equal the CPU port's on the same inputs."""
+    import threading
+    from pvac_hfhe_cppbyv_amd import ON_CHUNK_CB, DeviceBatch, Engine, HostCipher
+    from helpers import hip_batch_to_host
+    sk, man, em = fixture_secret()
+    eng = Engine(device=0, canon_tag=man["canon_tag"])
+    assert eng.gen_H().hex() == man["H_digest"]
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    eng.set_powg(read_u64("powg_B.u64"))
+    rng = np.random.default_rng(0x2A10)
+    n, depth = 4, 9
+    X, st = eng.enc_value(np.full(n, 2, np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    lock = threading.Lock()
+    finals = {}
+
+    def keep(user, first, cb, stream):
+        cs = hip_batch_to_host(cb.contents, stream)
+        with lock:
+            for i, c in enumerate(cs):
+                finals[first + i] = c
+        return 0
+
+    r = eng.ct_mul_chain(X, depth, nonce_seed=0x2A11, streams=2, chunk=2, check_gsum=True, digest_n=n,
+                         on_chunk=ON_CHUNK_CB(keep))
+    assert r["gsum_pairs"] == n * depth and r["gsum_failed"] == 0
+    assert sorted(finals) == list(range(n))
+    assert min(c.nE for c in finals.values()) > 600000   # step 9 on the GPU: ~690 K-edge ciphers
+    cs = [finals[i] for i in range(n)]
+    F = DeviceBatch.from_host([HostCipher(c.layers, c.meta, c.w_lo, c.w_hi, None) for c in cs], eng.device)
+    vals, dst = eng.dec_value(F, eng.base_R(F))
+    assert not dst.any()
+    assert vals == [1 << 10] * n
+    px = pack_device_batch(X, n)
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
+    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(man["canon_tag"])), n, *(P_(a) for a in px), depth, 8,
+                                      P_(ocnt), P_(odig), P_(se))
+    assert np.array_equal(ocnt, r["counts"]) and np.array_equal(odig, r["digests"])
+    assert np.array_equal(ocnt, np.array([c.nE for c in cs], np.uint64))

@@ -605,3 +605,28 @@ def test_direct_mode_shapes_vs_oracle(oracle, Bm):
     assert pc["direct"] == nd and eng2.ct_mul_redo_count() == nd   # every direct pair is over budget
     for p in range(len(xs)):
         _same(out2[p], oracle.ct_mul(xs[p], ys[p], per2[p], canon_tag=0xD2, Bm=Bm, edge_budget=budget), view=False)
+
+
+def test_direct_pairs_canonical_flag_no_redo(oracle):
+    """PVAC_MUL_ORDER_CANONICAL on a batch of direct-eligible chain-step pairs: exec
+    rebuilds their descriptors for the exact path before launching, so no pair runs the direct
+    kernels only to be redone. Output is the canonical (layer, idx, P<M) order, which the oracle
+    produces for any pair over edge_budget (here 0: every pair), bit-exact; the path counters show
+    no direct pair and the redo count stays put. The same engine then runs the same batch without
+    the flag, and the direct mode comes back (the plan's descriptors are rebuilt per exec)."""
+    from pvac_hfhe_cppbyv_amd import Engine, MUL_ORDER_CANONICAL
+    rng = np.random.default_rng(0xCA70)
+    xs = [_mk_layers(rng, [674] * 4) for _ in range(3)]
+    ys = [_mk_layers(rng, [20, 20]) for _ in range(3)]
+    eng = Engine(device=0, canon_tag=0xCA71)
+    p0, r0 = eng.ct_mul_path_counts(), eng.ct_mul_redo_count()
+    out, plan, per = _run_mul(eng, xs, ys, seed=0xCA72, flags=MUL_ORDER_CANONICAL)
+    p1 = eng.ct_mul_path_counts()
+    assert plan.n_large == 3
+    assert p1["direct"] == p0["direct"] and eng.ct_mul_redo_count() == r0
+    for p in range(3):
+        _same(out[p], oracle.ct_mul(xs[p], ys[p], per[p], canon_tag=0xCA71, edge_budget=0), view=False)
+    out2, _, per2 = _run_mul(eng, xs, ys, seed=0xCA72)
+    assert eng.ct_mul_path_counts()["direct"] - p1["direct"] == 3 and eng.ct_mul_redo_count() == r0
+    for p in range(3):
+        _same(out2[p], oracle.ct_mul(xs[p], ys[p], per2[p], canon_tag=0xCA71), view=False)

@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 
-def main(root):
+def summarize(root):
     tot = defaultdict(lambda: defaultdict(float))
     ms = defaultdict(lambda: defaultdict(float))
     n = defaultdict(lambda: defaultdict(set))
@@ -71,7 +71,11 @@ def main(root):
     tr = sum(r.get("hbm_read_bytes_corrected", 0) for r in out.values())
     out["_total"] = {"hbm_write_bytes": tw, "hbm_read_bytes_corrected": tr, "hbm_bytes": tw + tr,
                      "windows": windows}
-    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    return out
+
+
+def main(root):
+    json.dump(summarize(root), sys.stdout, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -22,7 +22,7 @@ import sys
 from collections import defaultdict
 
 
-def main(root):
+def summarize(root):
     acc = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(dict)   # (kernel, pass file) -> {dispatch: ns}
     for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True):
@@ -73,7 +73,11 @@ def main(root):
                 m["lds_bank_conflict_frac"] = m["SQ_LDS_BANK_CONFLICT"] / (256.0 * cyc)
         if m.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in m:
             m["wait_frac"] = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
-    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    return out
+
+
+def main(root):
+    json.dump(summarize(root), sys.stdout, indent=1, sort_keys=True)
     print()
 
 
