@@ -321,41 +321,13 @@ def main():
         },
         "cpu_baseline": None,
     }
-    # HBM traffic and VALU instruction count of the same kernel from the committed PMC summary
-    # (tools/prof_pmc.sh), used only when it was taken on this kernel and this batch shape
-    pm = {}
-    pmc = os.path.join(ROOT, "profiles", "pmc_ct_mul_fresh.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("pairs") != n or pm.get("epl") != args.epl or pm.get("kernel") != FRESH_KERNEL:
-                pm = {}
-        except Exception:
-            pm = {}
-    if pm:
-        result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-        result["roofline"]["traffic_source"] = pm.get("source")
-    # the integer-ALU roofline of the same kernel: VALU wave-instructions per second (PMC count per
-    # launch / HIP-event kernel time) against the ceiling measured now on this GPU (k_ubench.hip)
-    try:
-        ceil_w = eng.alu_ceiling(4)
-        ceil_mix = eng.alu_ceiling(0)
-    except Exception:
-        ceil_w = ceil_mix = None
-    vi = pm.get("valu_insts_per_launch")
-    if ceil_w and vi and avg_kernel_ms > 0:
-        ach = vi / (avg_kernel_ms / 1000.0)
-        result["roofline"]["valu"] = {
-            "achieved": ach, "peak": ceil_w, "unit": "wave64 VALU inst/s", "frac": ach / ceil_w,
-            "insts_per_pair": vi / n, "lds_bank_conflict_frac": pm.get("lds_bank_conflict_frac"),
-            "mad_mix_ceiling": ceil_mix,
-            "source": "SQ_INSTS_VALU per full-batch launch (profiles/pmc_ct_mul_fresh.json) / kernel time; peak: "
-                      "pvac_hip_alu_ceiling(4), independent 32-bit v_add_u32 / v_xor_b32 / v_alignbit_b32 "
-                      "at 8 waves per SIMD on this GPU (the kind-0 v_mad_u64_u32 mix beside it)"}
-    elif ceil_w:
-        result["roofline"]["valu"] = {"peak": ceil_w, "unit": "wave64 VALU inst/s", "achieved": None,
-                                      "note": "no PMC summary for this kernel / batch in profiles/"}
+    # HBM traffic and the VALU counters of the same kernel from the committed PMC record
+    # (tools/pmc_target.sh -> profiles/pmc/headline.json), quoted only when the record was taken on
+    # THIS library binary (sha256 of libpvac_hip.so) and this batch shape; null plus the reason else
+    pm, why = pmc_record("headline", {"pairs": n, "epl": args.epl})
+    result["roofline"]["traffic"] = pm.get("traffic") if pm else None
+    result["roofline"]["traffic_source"] = PMC_SOURCE if pm else why
+    result["roofline"]["valu"] = valu_roofline(eng, pm, why, avg_kernel_ms, n, "pair")
 
     # fresh-kernel pairs re-run on the general path during the timed steps (a key sum of 0 mod p:
     # never for these uniform nonzero weights, so any redo here is a kernel defect costing time)
@@ -384,6 +356,74 @@ def main():
 
 
 FRESH_KERNEL = "k_ct_mul_fresh3"   # the fresh-pair kernel launch_ct_mul_fresh runs (k_mul_fresh.hip)
+PMC_SOURCE = ("rocprofv3 --pmc, one counter group per run, mean per full-size dispatch; traffic = 2 x FETCH_SIZE "
+              "(wide-read correction) + WRITE_SIZE (tools/pmc_target.sh, tools/pmc_stamp.py)")
+_LIB_SHA = None
+
+
+def lib_sha256():
+    """sha256 of the libpvac_hip.so this process loaded (the PMC records are stamped with it)."""
+    global _LIB_SHA
+    if _LIB_SHA is None:
+        import hashlib
+        from pvac_hfhe_cppbyv_amd import _LIB_PATH
+        h = hashlib.sha256()
+        with open(_LIB_PATH, "rb") as f:
+            for blk in iter(lambda: f.read(1 << 20), b""):
+                h.update(blk)
+        _LIB_SHA = h.hexdigest()
+    return _LIB_SHA
+
+
+def pmc_record(target, workload):
+    """profiles/pmc/<target>.json when it was taken on this library binary and this workload:
+    (record, None); else ({}, the reason)."""
+    path = os.path.join(ROOT, "profiles", "pmc", target + ".json")
+    if not os.path.exists(path):
+        return {}, f"no PMC record profiles/pmc/{target}.json"
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except Exception as ex:
+        return {}, f"unreadable PMC record: {ex!r}"
+    if rec.get("lib_sha256") != lib_sha256():
+        return {}, (f"profiles/pmc/{target}.json was taken on libpvac_hip.so sha256 {str(rec.get('lib_sha256'))[:12]}, "
+                    f"this run loaded {lib_sha256()[:12]}: counters of another binary are not quoted")
+    got = rec.get("workload") or {}
+    for k, v in workload.items():
+        if got.get(k) != v:
+            return {}, f"PMC record workload {got} differs from this run's {workload}"
+    return rec, None
+
+
+def valu_roofline(eng, rec, why, kernel_ms, units, unit_name):
+    """The VALU side of a kernel's roofline from its PMC record: frac = the counter-measured VALU-busy
+    fraction, 4 x SQ_ACTIVE_INST_VALU (quad-cycles) / (kernel cycles x 1,024 SIMDs), <= 1 by
+    construction; beside it the VALU instruction rate against two ceilings measured now on this GPU
+    (pvac_hip_alu_ceiling 4: a 32-bit mix, 0: the v_mad_u64_u32 mix; the per-opcode issue costs are
+    in profiles/r05/issue_probe.json)."""
+    try:
+        ceil32, ceilmad = eng.alu_ceiling(4), eng.alu_ceiling(0)
+    except Exception:
+        ceil32 = ceilmad = None
+    out = {"unit": "fraction of SIMD cycles issuing VALU (SQ_ACTIVE_INST_VALU)", "frac": None,
+           "mix32_ceiling_inst_per_s": ceil32, "madmix_ceiling_inst_per_s": ceilmad}
+    if not rec:
+        out["note"] = why
+        return out
+    vi = rec.get("valu_insts")
+    out.update({"frac": rec.get("valu_busy"), "achieved": rec.get("valu_busy"), "peak": 1.0,
+                f"insts_per_{unit_name}": vi / units if vi else None,
+                "lds_active_frac": rec.get("lds_active_frac"),
+                "lds_bank_conflict_frac": rec.get("lds_bank_conflict_frac"), "wait_frac": rec.get("wait_frac"),
+                "clock_hz_pmc_run": rec.get("clock_hz_est"), "source": PMC_SOURCE,
+                "lib_sha256": rec.get("lib_sha256")})
+    if vi and kernel_ms > 0:
+        rate = vi / (kernel_ms / 1000.0)
+        out["inst_per_s"] = rate
+        if ceil32:
+            out["rate_vs_mix32_ceiling"] = rate / ceil32
+    return out
 
 
 def self_checks(eng, args, A, B, out, nonces, n, first, seed, world, rank):
@@ -736,27 +776,13 @@ def sigma_bench(eng, args, with_cpu):
                 del os.environ["PVAC_SIGMA_PATH"]
             del C2, Cb2
         full["checks"] = {"sigma_paths_agree": all(agree.values()), "paths": ["delta"] + list(agree)}
-    # k_sigma is not HBM-bound (1 KiB written per edge): it is bound by the LDS pipe (its atomic-XOR
-    # flips, bank conflicts in most of the LDS cycles; PMC, profiles/r02/pmc_sigma) with integer VALU
-    # beside it (PMC VALU count per launch over this kernel time, against the ceiling measured now)
-    try:
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_sigma", "summary.json")) as f:
-            ks = json.load(f).get("k_sigma", {})
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_sigma", "notes.json")) as f:
-            notes = json.load(f)
-        ceil_w = eng.alu_ceiling(0)
-        if ks and notes.get("edges_per_launch") == int(edges) and sig_avg > 0 and ceil_w:
-            ach = ks["SQ_INSTS_VALU"] / (sig_avg / 1000.0)
-            full["roofline"] = {
-                "bound": "lds",
-                "lds_busy_frac": notes.get("lds_busy_frac"),
-                "lds_bank_conflict_frac": ks.get("lds_bank_conflict_frac"),
-                "valu": {"achieved": ach, "peak": ceil_w, "unit": "wave64 VALU inst/s", "frac": ach / ceil_w,
-                         "per_edge": ks["SQ_INSTS_VALU"] / edges},
-                "source": "PMC of this batch (profiles/r02/pmc_sigma: SQ_LDS_IDX_ACTIVE / CU cycles, "
-                          "SQ_LDS_BANK_CONFLICT, SQ_INSTS_VALU); VALU peak: pvac_hip_alu_ceiling(0) on this GPU"}
-    except Exception:
-        pass
+    # k_sigma is not HBM-bound (1 KiB written per edge): VALU issue (SHA-256) and the LDS pipe (its
+    # atomic-XOR flips) bound it; the counters come from profiles/pmc/sigma.json when it was taken on
+    # this library binary and this batch
+    rec, why = pmc_record("sigma", {"pairs": ns, "edges": edges})
+    full["roofline"] = {"bound": "valu+lds", "valu": valu_roofline(eng, rec, why, sig_avg, edges, "edge"),
+                        "traffic": rec.get("traffic") if rec else None,
+                        "lds_active_frac": rec.get("lds_active_frac") if rec else None}
     if with_cpu:
         full["cpu_baseline"] = _ref_full_baseline()
     return full
@@ -875,9 +901,10 @@ def chain_bench(eng, args):
     # same command pick out this pass's dispatches: tools/chain_window.py)
     w0 = time.monotonic_ns()
     t1 = time.perf_counter()
-    # (final edge counts of every chain: device-to-device copies; the FNV-1a digests walk each cipher's
-    # edges serially, ~0.2 s per 16 depth-8 chains, so they come from the check pass)
-    r = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, count_n=n)
+    # (final edge counts and position-keyed sum digests of EVERY chain: a copy and one parallel
+    # reduction per chunk; the serial FNV-1a digests, ~0.2 s per 16 depth-8 chains, come from the
+    # check pass, which must reproduce every sum digest of this timed pass)
+    r = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, count_n=n, sumdigest=True)
     torch.cuda.synchronize(dev)
     chain_s = time.perf_counter() - t1
     w1 = time.monotonic_ns()
@@ -891,9 +918,10 @@ def chain_bench(eng, args):
     # check pass (untimed): same nonces, gsum invariant on every pair-step, every final digest
     t2 = time.perf_counter()
     rc = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, check_gsum=True, digest_n=n_chk,
-                          count_n=n)
+                          count_n=n, sumdigest=True)
     check_s = time.perf_counter() - t2
     same = bool(np.array_equal(rc["counts"], r["counts"]))
+    same_dig = bool(np.array_equal(rc["sumdigests"], r["sumdigests"]))
     x_host = _pack_host(X_all, n_chk) if n_chk else None   # the sampled chains' inputs
     del X_all, vals
     products = float(sum(r["products"]))
@@ -914,6 +942,7 @@ def chain_bench(eng, args):
                                  "step, on the device (second, untimed pass with the same nonces)", "pair_steps": gp,
                         "failed": gf, "invariant_ok": gf == 0 and gp == n * depth, "check_pass_seconds": check_s,
                         "timed_pass_counts_equal": same,
+                        "timed_pass_sumdigests_equal": same_dig,
                         "edges_equal": rc["edges"] == r["edges"]}
     # Roofline of the products: per second against the matrix-core ceiling measured on this GPU
     # (k_ubench.hip k_probe_mfma8: back-to-back v_mfma_i32_32x32x32_i8, 64 dense-mode products
@@ -928,6 +957,19 @@ def chain_bench(eng, args):
                            "col26_ceiling": eng.alu_ceiling(3), "fold1_ceiling": eng.alu_ceiling(1)}
     except Exception as ex:
         out["roofline"] = {"error": repr(ex)}
+    # chain PMC record (profiles/pmc/chain.json, tools/pmc_target.sh chain): HBM traffic and VALU /
+    # MFMA counts per input chain of the same depth / chunk / streams, when taken on this binary
+    crec, cwhy = pmc_record("chain", {"depth": depth, "chunk": chunk, "streams": S})
+    if crec:
+        ni = max(1, (crec.get("workload") or {}).get("inputs") or 1)
+        tot = crec.get("total") or {}
+        out["pmc_per_input"] = {
+            "hbm_write_bytes": tot.get("hbm_write_bytes", 0) / ni, "hbm_read_bytes": tot.get("hbm_read_bytes_corrected", 0) / ni,
+            "kernels": {k: {f: v / ni for f, v in d.items() if f in ("traffic", "valu_insts")}
+                        for k, d in (crec.get("kernels") or {}).items()},
+            "inputs_profiled": ni, "lib_sha256": crec.get("lib_sha256"), "source": PMC_SOURCE}
+    else:
+        out["pmc_per_input"] = {"note": cwhy}
     if args.chain_compare_streams:
         # the same call with S worker streams and with ONE on 4 chunks per worker of new inputs
         try:

@@ -142,7 +142,12 @@ int pvac_hip_alu_ceiling(pvac_hip_ctx* ctx, int kind, double* per_s);
  * tick x 100 MHz, median over workgroups), so cycles per instruction = SIMDs x clock / per_s.
  * op: 0 v_add_u32, 1 v_xor_b32, 2 v_alignbit_b32, 3 v_lshlrev_b32, 4 v_min_u32, 5 v_add3_u32,
  * 6 v_pk_add_u16, 7 v_fma_f32, 8 v_mul_lo_u32, 9 v_mul_hi_u32, 10 v_cndmask_b32, 11 v_bfe_u32,
- * 12 v_add_co_u32, 13 v_and_or_b32, 14 v_pk_min_u16, 15 v_bitop3_b32, 16 v_mad_u64_u32.
+ * 12 v_add_co_u32, 13 v_and_or_b32, 14 v_pk_min_u16, 15 v_bitop3_b32, 16 v_mad_u64_u32,
+ * 17 v_cndmask_b32_e64 (SGPR-pair mask), 18 v_lshl_add_u32, 19 v_mov_b32 DPP row_shr, 20 v_perm_b32,
+ * 21 v_mul_u32_u24, 22 v_sub_u32, 23 v_max3_u32, 24 v_cmp (VCC) + VOP2 v_cndmask_b32 pairs, 25 v_cndmask_b32_e64
+ * reading VCC, 26 VOP2 v_addc_co_u32 (VCC carry), 27 v_addc_co_u32_e64 (SGPR carry), 28 v_cmp_e64 + v_cndmask_b32_e64
+ * (SGPR mask) pairs, 29 v_min_u32_e64, 30 v_add_u32_e64, 31 v_and_b32, 32 v_or_b32, 33 v_lshrrev_b32,
+ * 34 v_mov_b32, 35 v_max_u32.
  * Measurement only (never used by an op). Synchronous. */
 int pvac_hip_issue_probe(pvac_hip_ctx* ctx, int op, int waves_per_simd, double* per_s, double* clock_hz);
 /* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */
@@ -213,7 +218,12 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * plan's shape read-back) and its short dependent launches overlap other chunks' kernels, so a
  * single caller thread gets the concurrency. Synchronous: returns when every chunk is done.
  * Each step is exactly pvac_hip_ct_mul_plan + pvac_hip_ct_mul_exec (weights only, reference hash
- * order unless flags has PVAC_MUL_ORDER_CANONICAL; WITH_SIGMA is not accepted here).
+ * order unless flags has PVAC_MUL_ORDER_CANONICAL). With PVAC_MUL_WITH_SIGMA the FINAL step also
+ * gets its sigmas (sigma_from_H per output edge, arithmetic.hpp:90-94; the context needs H): the
+ * reference draws one salt per emitted edge at every step, but only c_depth's sigmas survive (an
+ * output sigma depends on its layer seed, idx, ch and salt alone), so intermediate steps stay
+ * weights-only and a caller replaying a reference stream skips their salts (after_step gives the
+ * counts). The final chunk buffer then holds 1 KiB of sigma per edge: size `chunk` for it.
  * Nonces: fill_nonces(user, step, first_input, n_words, dev_words, stream) when given (called on
  * the worker thread; fill n_words device words on `stream`, the 2-words-per-output-layer-slot
  * array of pvac_hip_ct_mul_exec), else splitmix64 words: pvac_hip_fill_random with seed
@@ -225,15 +235,38 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * inputs [0, count_n).
  * PVAC_CHAIN_CHECK_GSUM runs the reference's gsum invariant (pvac_hip_check_mul_gsum) on every pair
  * of every step (needs pvac_hip_ctx_set_powg). A callback's nonzero return stops the chain with
- * PVAC_EINVAL. */
+ * PVAC_EINVAL.
+ * Step hooks (all optional, called on the worker thread with the worker's stream; A = c_{step},
+ * X = the chunk's inputs, C = c_{step+1}, all device batches valid during the call):
+ *   nonces_at  before step `step`'s exec: fill dev_words[0, n_words) (2 words per layer slot of C,
+ *              product layer (la, lb) of pair i at C.l_off[i] + |A_i.L| + |X_i.L| + la |X_i.L| + lb,
+ *              lo then hi). Replaces fill_nonces.
+ *   after_step after step `step`'s exec (C's weights, counts and layers are final; dev_words null).
+ *   salts_at   WITH_SIGMA, final step, after its weights: fill dev_words[0, n_words) (n_words = C's
+ *              edge slots): dev_words[C.e_off[i] + k] is the salt of pair i's k-th emitted edge in
+ *              the reference's emit order (hash order; a pair in the canonical order still takes its
+ *              salts in hash order, as pvac_hip_ct_mul_exec does).
+ * Devices: with n_devices > 0 the inputs are split into n_devices contiguous ranges of whole chunks
+ * (by global input index; a range never splits a chunk, so every chunk, its nonce seeds and its
+ * results are those of a one-device run) and each range runs on `streams` worker threads on
+ * devices[j] (an ordinal may repeat). A worker whose device is not X's (or every worker of a range
+ * j > 0 with PVAC_CHAIN_STAGE_INPUTS) first copies its chunk's inputs into worker-local buffers
+ * (peer reads over xGMI when the devices differ); digests and counts are written to the caller's
+ * arrays on X's device. ctx keeps the worker contexts of every device between calls. */
 #define PVAC_CHAIN_CHECK_GSUM 0x100u
+#define PVAC_CHAIN_STAGE_INPUTS 0x200u   /* ranges j > 0 stage their chunks even on X's device (tests) */
+#define PVAC_CHAIN_MAX_DEVICES 64
+typedef int (*pvac_chain_step_fn)(void* user, uint32_t step, uint64_t first_input, const pvac_ct_batch* A,
+                                  const pvac_ct_batch* X, const pvac_ct_batch* C, uint64_t* dev_words,
+                                  uint64_t n_words, void* stream);
 #define PVAC_CHAIN_MAX_DEPTH 32
 typedef struct pvac_chain_opts {
     uint32_t depth;        /* 1 .. PVAC_CHAIN_MAX_DEPTH */
     uint32_t streams;      /* worker streams, 0 = 4 */
     uint64_t chunk;        /* inputs per chunk, 0 = 1024 */
     uint64_t nonce_seed;
-    uint32_t flags;        /* PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM */
+    uint32_t flags;        /* PVAC_MUL_ORDER_CANONICAL | PVAC_MUL_WITH_SIGMA | PVAC_CHAIN_CHECK_GSUM |
+                              PVAC_CHAIN_STAGE_INPUTS */
     uint32_t pad;
     uint64_t digest_n;     /* leading inputs whose final digests are written */
     uint64_t* digest_out;  /* DEVICE [digest_n], nullable */
@@ -243,6 +276,13 @@ typedef struct pvac_chain_opts {
                        void* stream);
     int (*on_chunk)(void* user, uint64_t first_input, const pvac_ct_batch* C, void* stream);
     void* user;
+    pvac_chain_step_fn nonces_at;    /* step hooks (above), nullable */
+    pvac_chain_step_fn after_step;
+    pvac_chain_step_fn salts_at;
+    const int* devices;              /* HOST [n_devices] GPU ordinals; null / 0 = ctx's device */
+    uint32_t n_devices;              /* 0 .. PVAC_CHAIN_MAX_DEVICES */
+    uint32_t pad2;
+    uint64_t* sumdigest_out;         /* DEVICE [count_n], nullable: pvac_hip_batch_sumdigest of c_depth */
 } pvac_chain_opts;
 typedef struct pvac_chain_stats {
     uint64_t pair_steps;                        /* inputs x depth */
@@ -256,6 +296,13 @@ typedef struct pvac_chain_stats {
 } pvac_chain_stats;
 int pvac_hip_ct_mul_chain(pvac_hip_ctx* ctx, const pvac_ct_batch* X, const pvac_chain_opts* opts,
                           pvac_chain_stats* stats);
+/* Copy `bytes` between any host / device pointers (hipMemcpyDefault) ordered on `stream` (a chain
+ * hook's stream, or null for the legacy stream) and wait for it: lets an FFI caller (ctypes, cgo, JNI)
+ * that does not link the HIP runtime read a hook's batch view or fill its words. */
+int pvac_hip_memcpy(void* dst, const void* src, size_t bytes, void* stream);
+/* First input of range j of n_inputs inputs split over `parts` device ranges of whole chunks (the
+ * split pvac_hip_ct_mul_chain uses): first[j] for j = 0 .. parts (first[parts] = n_inputs). */
+int pvac_hip_chain_partition(uint64_t n_inputs, uint64_t chunk, uint32_t parts, uint64_t* first);
 
 /* ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45; combine_ciphers ops/encrypt.hpp:260-279).
  * negate_b != 0 gives ct_sub (B's weights scaled by p-1). Dense CSR output: the plan writes
@@ -296,6 +343,10 @@ int pvac_hip_fill_random(pvac_hip_ctx* ctx, uint64_t seed, uint64_t* out, size_t
 uint64_t pvac_hip_bucket_count(uint64_t n);
 /* per-cipher FNV-1a digest over (meta, w_lo, w_hi) of its edges in order (device out[n]). */
 int pvac_hip_batch_digest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
+/* per-cipher position-keyed digest (device out[n]): |E| + sum over edges e of
+ * m(m(m(e * 0x9E3779B97F4A7C15 ^ meta) ^ w_lo) ^ w_hi) mod 2^64, m = the splitmix64 finaliser.
+ * Order-sensitive, computed in parallel (one workgroup per cipher). */
+int pvac_hip_batch_sumdigest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
 
 /* ---------------------------------------------------------------- LPN PRF
  * SecKey (core/types.hpp:134-137): prf_k and the LPN secret (ceil(lpn_n/64) words, host) with

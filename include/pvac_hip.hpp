@@ -35,12 +35,15 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <exception>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
 #include <string>
@@ -195,21 +198,9 @@ inline void alloc_out(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint
     c.l_cnt.resize(n);
 }
 
+// host SoA image (c.l_off ... c.sigma filled) -> reference Ciphers
 template <class CipherT>
-std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t m_bits,
-                                 bool with_sigma, hipStream_t s) {
-    c.l_off.resize(n); c.l_cnt.resize(n); c.e_off.resize(n); c.e_cnt.resize(n);
-    c.layers.resize(lslots); c.meta.resize(eslots); c.w_lo.resize(eslots); c.w_hi.resize(eslots);
-    c.d_l_off.download(c.l_off.data(), n, s); c.d_l_cnt.download(c.l_cnt.data(), n, s);
-    c.d_e_off.download(c.e_off.data(), n, s); c.d_e_cnt.download(c.e_cnt.data(), n, s);
-    c.d_layers.download(c.layers.data(), lslots, s);
-    c.d_meta.download(c.meta.data(), eslots, s);
-    c.d_w_lo.download(c.w_lo.data(), eslots, s); c.d_w_hi.download(c.w_hi.data(), eslots, s);
-    if (with_sigma) {
-        c.sigma.resize(eslots * c.sigma_words);
-        c.d_sigma.download(c.sigma.data(), c.sigma.size(), s);
-    }
-    hip_ok(hipStreamSynchronize(s), "sync");
+std::vector<CipherT> convert_host(batch& c, size_t n, uint32_t m_bits, bool with_sigma) {
     std::vector<CipherT> out(n);
     parallel_ranges(n, [&](size_t i0, size_t i1) {
     for (size_t i = i0; i < i1; ++i) {
@@ -240,6 +231,58 @@ std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t e
     }
     });
     return out;
+}
+
+template <class CipherT>
+std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t m_bits,
+                                 bool with_sigma, hipStream_t s) {
+    c.l_off.resize(n); c.l_cnt.resize(n); c.e_off.resize(n); c.e_cnt.resize(n);
+    c.layers.resize(lslots); c.meta.resize(eslots); c.w_lo.resize(eslots); c.w_hi.resize(eslots);
+    c.d_l_off.download(c.l_off.data(), n, s); c.d_l_cnt.download(c.l_cnt.data(), n, s);
+    c.d_e_off.download(c.e_off.data(), n, s); c.d_e_cnt.download(c.e_cnt.data(), n, s);
+    c.d_layers.download(c.layers.data(), lslots, s);
+    c.d_meta.download(c.meta.data(), eslots, s);
+    c.d_w_lo.download(c.w_lo.data(), eslots, s); c.d_w_hi.download(c.w_hi.data(), eslots, s);
+    if (with_sigma) {
+        c.sigma.resize(eslots * c.sigma_words);
+        c.d_sigma.download(c.sigma.data(), c.sigma.size(), s);
+    }
+    hip_ok(hipStreamSynchronize(s), "sync");
+    return convert_host<CipherT>(c, n, m_bits, with_sigma);
+}
+
+// small synchronous device -> host copies of a batch view handed to a chain hook (valid only there)
+inline std::vector<uint64_t> d2h_u64(const uint64_t* p, size_t n, hipStream_t s) {
+    std::vector<uint64_t> v(n);
+    if (n) hip_ok(hipMemcpyAsync(v.data(), p, n * 8, hipMemcpyDeviceToHost, s), "D2H");
+    hip_ok(hipStreamSynchronize(s), "sync");
+    return v;
+}
+
+// the used rows of a capacity-padded device batch view -> reference Ciphers
+template <class CipherT>
+std::vector<CipherT> from_view(const pvac_ct_batch& v, uint32_t m_bits, hipStream_t s) {
+    batch c;
+    const size_t n = v.n;
+    c.l_off = d2h_u64(v.l_off, n, s); c.l_cnt = d2h_u64(v.l_cnt, n, s);
+    c.e_off = d2h_u64(v.e_off, n, s); c.e_cnt = d2h_u64(v.e_cnt, n, s);
+    uint64_t nl = 0, ne = 0;
+    for (size_t i = 0; i < n; ++i) {
+        nl = std::max(nl, c.l_off[i] + c.l_cnt[i]);
+        ne = std::max(ne, c.e_off[i] + c.e_cnt[i]);
+    }
+    const bool sig = v.sigma != nullptr;
+    c.sigma_words = v.sigma_words;
+    c.layers.resize(nl); c.meta.resize(ne); c.w_lo.resize(ne); c.w_hi.resize(ne);
+    if (sig) c.sigma.resize(ne * c.sigma_words);
+    auto get = [&](void* dst, const void* src, size_t bytes) {
+        if (bytes) hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "D2H");
+    };
+    get(c.layers.data(), v.layers, nl * sizeof(pvac_layer));
+    get(c.meta.data(), v.meta, ne * 8); get(c.w_lo.data(), v.w_lo, ne * 8); get(c.w_hi.data(), v.w_hi, ne * 8);
+    if (sig) get(c.sigma.data(), v.sigma, c.sigma.size() * 8);
+    hip_ok(hipStreamSynchronize(s), "sync");
+    return convert_host<CipherT>(c, n, m_bits, sig);
 }
 
 }  // namespace detail
@@ -370,6 +413,111 @@ public:
         }
         return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits, false,
                                             stream_);
+    }
+
+    // Depth chains through pvac_hip_ct_mul_chain (the chain entry point): for every input x of xs,
+    // c_0 = x, c_k = ct_mul(pk, c_{k-1}, x) for k = 1..depth (the test_depth / cfg-4 shape of
+    // tests/test_main.cpp:289-293's loop); returns every c_depth. Randomness of chain i comes from
+    // rnds[i] in the reference's draw order, step after step: 2 words per new product layer (la, lb
+    // row-major, lo then hi), then one salt per emitted edge (arithmetic.hpp:64, 93). Only c_depth's
+    // sigmas survive a chain, so the intermediate salts are drawn and discarded; with_sigma computes
+    // the final step's sigmas (needs pk.H), otherwise the final salts are discarded too. A chain
+    // replayed from a reference stream is byte-identical to the reference's c_depth. devices: GPU
+    // ordinals to spread the chains over (whole chunks per device; empty = this engine's device);
+    // chunk: inputs per worker chunk (with sigma the last step holds 1 KiB per edge: keep it small).
+    template <class PubKeyT, class CipherT>
+    std::vector<CipherT> ct_mul_chain(const PubKeyT& pk, const std::vector<const CipherT*>& xs, uint32_t depth,
+                                      bool with_sigma, std::vector<RandomSource>& rnds,
+                                      const std::vector<int>& devices = {}, uint32_t streams = 2, uint64_t chunk = 16) {
+        const size_t n = xs.size();
+        if (rnds.size() != n) throw Error(PVAC_EINVAL, "ct_mul_chain: one RandomSource per input");
+        if (!n) return {};
+        if (with_sigma) ensure_H(pk);
+        detail::batch x;
+        detail::to_host(xs, sigma_words(), false, x);
+        detail::upload(x, stream_, false);
+        detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+        struct state {
+            std::vector<RandomSource>* rnds;
+            std::vector<CipherT> out;
+            uint32_t depth, m_bits;
+            bool sigma;
+        } stt{&rnds, std::vector<CipherT>(n), depth, prm_.m_bits, with_sigma};
+        pvac_chain_opts o{};
+        o.depth = depth;
+        o.streams = streams;
+        o.chunk = chunk;
+        o.flags = with_sigma ? PVAC_MUL_WITH_SIGMA : 0u;
+        o.user = &stt;
+        o.devices = devices.empty() ? nullptr : devices.data();
+        o.n_devices = (uint32_t)devices.size();
+        // hooks run on the library's worker threads; chunks (and so their inputs' sources) are disjoint
+        o.nonces_at = [](void* u, uint32_t, uint64_t c0, const pvac_ct_batch* A, const pvac_ct_batch* X,
+                         const pvac_ct_batch* C, uint64_t* words, uint64_t nw, void* st) -> int {
+            try {
+                state& S = *(state*)u;
+                const hipStream_t s = (hipStream_t)st;
+                const auto la = detail::d2h_u64(A->l_cnt, A->n, s), lx = detail::d2h_u64(X->l_cnt, X->n, s);
+                const auto lo = detail::d2h_u64(C->l_off, C->n, s);
+                std::vector<uint64_t> w(nw, 0);
+                for (size_t i = 0; i < A->n; ++i) {
+                    RandomSource& r = (*S.rnds)[c0 + i];
+                    const uint64_t s0 = lo[i] + la[i] + lx[i];
+                    for (uint64_t k = 0; k < la[i] * lx[i]; ++k) {
+                        w[2 * (s0 + k)] = r();
+                        w[2 * (s0 + k) + 1] = r();
+                    }
+                }
+                detail::hip_ok(hipMemcpyAsync(words, w.data(), nw * 8, hipMemcpyHostToDevice, s), "H2D");
+                detail::hip_ok(hipStreamSynchronize(s), "sync");
+                return 0;
+            } catch (...) {
+                return 1;
+            }
+        };
+        o.after_step = [](void* u, uint32_t step, uint64_t c0, const pvac_ct_batch*, const pvac_ct_batch*,
+                          const pvac_ct_batch* C, uint64_t*, uint64_t, void* st) -> int {
+            try {
+                state& S = *(state*)u;
+                if (S.sigma && step + 1 == S.depth) return 0;   // salts_at draws these
+                const auto ec = detail::d2h_u64(C->e_cnt, C->n, (hipStream_t)st);
+                for (size_t i = 0; i < C->n; ++i)
+                    for (uint64_t k = 0; k < ec[i]; ++k) (void)(*S.rnds)[c0 + i]();
+                return 0;
+            } catch (...) {
+                return 1;
+            }
+        };
+        o.salts_at = [](void* u, uint32_t, uint64_t c0, const pvac_ct_batch*, const pvac_ct_batch*,
+                        const pvac_ct_batch* C, uint64_t* words, uint64_t nw, void* st) -> int {
+            try {
+                state& S = *(state*)u;
+                const hipStream_t s = (hipStream_t)st;
+                const auto ec = detail::d2h_u64(C->e_cnt, C->n, s), eo = detail::d2h_u64(C->e_off, C->n, s);
+                std::vector<uint64_t> w(nw ? nw : 1, 0);
+                for (size_t i = 0; i < C->n; ++i)
+                    for (uint64_t k = 0; k < ec[i]; ++k) w[eo[i] + k] = (*S.rnds)[c0 + i]();
+                detail::hip_ok(hipMemcpyAsync(words, w.data(), nw * 8, hipMemcpyHostToDevice, s), "H2D");
+                detail::hip_ok(hipStreamSynchronize(s), "sync");
+                return 0;
+            } catch (...) {
+                return 1;
+            }
+        };
+        o.on_chunk = [](void* u, uint64_t c0, const pvac_ct_batch* C, void* st) -> int {
+            try {
+                state& S = *(state*)u;
+                auto cs = detail::from_view<CipherT>(*C, S.m_bits, (hipStream_t)st);
+                for (size_t i = 0; i < cs.size(); ++i) S.out[c0 + i] = std::move(cs[i]);
+                return 0;
+            } catch (...) {
+                return 1;
+            }
+        };
+        pvac_ct_batch vx = x.view(false);
+        pvac_chain_stats st{};
+        check(pvac_hip_ct_mul_chain(ctx_, &vx, &o, &st));
+        return std::move(stt.out);
     }
 
     // Batched ct_add / ct_sub (ops/arithmetic.hpp:12-31, 43-45); sigmas carried through.
@@ -628,6 +776,91 @@ std::vector<CipherT> ct_mul_batch(const PubKeyT& pk, const std::vector<CipherT>&
     for (auto& x : A) a.push_back(&x);
     for (auto& x : B) b.push_back(&x);
     return engine_for(pk).ct_mul(pk, a, b, with_sigma, rnd);
+}
+
+// Multi-device batch: pairs split into contiguous ranges, one per entry of `devices` (an ordinal may
+// repeat), each range on its own host thread and context. Draws from rnd stay in the one-device order:
+// every pair's nonces first (pair order; their counts, 2 |A.L| |B.L| per pair, are known up front, so
+// they are drawn before any device starts), then every pair's salts (pair order: range j draws its
+// salts once its own weights are known and ranges < j have drawn theirs). So a replayed stream gives
+// the bytes of ct_mul_batch on one device.
+template <class PubKeyT, class CipherT>
+std::vector<CipherT> ct_mul_batch(const PubKeyT& pk, const std::vector<CipherT>& A, const std::vector<CipherT>& B,
+                                  bool with_sigma, const RandomSource& rnd, const std::vector<int>& devices) {
+    if (devices.size() <= 1) {
+        std::vector<const CipherT*> a, b;
+        for (auto& x : A) a.push_back(&x);
+        for (auto& x : B) b.push_back(&x);
+        if (devices.empty()) return engine_for(pk).ct_mul(pk, a, b, with_sigma, rnd);
+        Engine e(devices[0], Engine::params_of(pk));
+        return e.ct_mul(pk, a, b, with_sigma, rnd);
+    }
+    if (A.size() != B.size()) throw Error(PVAC_EINVAL, "ct_mul_batch: |A| != |B|");
+    const size_t n = A.size(), D = devices.size();
+    std::vector<uint64_t> first(D + 1);
+    for (size_t j = 0; j <= D; ++j) first[j] = n * j / D;
+    // every nonce word, pair order
+    std::vector<std::vector<uint64_t>> nonces(D);
+    for (size_t j = 0; j < D; ++j)
+        for (size_t i = first[j]; i < first[j + 1]; ++i)
+            for (size_t k = 0; k < 2 * A[i].L.size() * B[i].L.size(); ++k) nonces[j].push_back(rnd());
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t turn = 0;   // the range whose salts are drawn next
+    std::vector<std::vector<CipherT>> out(D);
+    std::vector<std::exception_ptr> err(D);
+    std::vector<std::thread> th;
+    for (size_t j = 0; j < D; ++j)
+        th.emplace_back([&, j] {
+            bool my_turn = false;
+            try {
+                size_t pos = 0;
+                // a range's source: its pre-drawn nonces, then (in range order) salts from rnd
+                RandomSource src = [&]() -> uint64_t {
+                    if (pos < nonces[j].size()) return nonces[j][pos++];
+                    if (!my_turn) {
+                        std::unique_lock<std::mutex> g(mu);
+                        cv.wait(g, [&] { return turn == j; });
+                        my_turn = true;
+                    }
+                    std::lock_guard<std::mutex> g(mu);
+                    return rnd();
+                };
+                std::vector<const CipherT*> a, b;
+                for (size_t i = first[j]; i < first[j + 1]; ++i) {
+                    a.push_back(&A[i]);
+                    b.push_back(&B[i]);
+                }
+                Engine e(devices[j], Engine::params_of(pk));
+                out[j] = e.ct_mul(pk, a, b, with_sigma, src);
+            } catch (...) {
+                err[j] = std::current_exception();
+            }
+            {
+                // hand the salt turn on (also when this range drew none, or failed)
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return turn == j; });
+                ++turn;
+            }
+            cv.notify_all();
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+    std::vector<CipherT> all;
+    all.reserve(n);
+    for (auto& v : out)
+        for (auto& c : v) all.push_back(std::move(c));
+    return all;
+}
+
+// Chains through the chain entry point (Engine::ct_mul_chain): one RandomSource per input.
+template <class PubKeyT, class CipherT>
+std::vector<CipherT> ct_mul_chain(const PubKeyT& pk, const std::vector<CipherT>& xs, uint32_t depth, bool with_sigma,
+                                  std::vector<RandomSource>& rnds, const std::vector<int>& devices = {}) {
+    std::vector<const CipherT*> x;
+    for (auto& c : xs) x.push_back(&c);
+    return engine_for(pk).ct_mul_chain(pk, x, depth, with_sigma, rnds, devices);
 }
 
 template <class PubKeyT, class CipherT>

@@ -695,6 +695,48 @@ static void cmd_enc(const std::string& dir, int nenc) {
     std::ofstream(dir + "/enc_manifest.json") << js.str();
 }
 
+// ---- chain entry-point fixture (pvac_hip_ct_mul_chain with a final-step WITH_SIGMA): x = enc_value(2),
+//      c_0 = x, c_k = ct_mul(pk, c_{k-1}, x) for k = 1..depth (the test_depth / cfg-4 chain shape;
+//      tests/test_main.cpp:289-293 multiplies by a fresh enc_value(2) per step instead), the full
+//      getrandom stream of the chain (every step's nonces and salts, in the reference's order), and
+//      c_depth: weights-only .ct, full layer table, per-edge sigma digests, its decryption.
+static void cmd_chainx(const std::string& dir, int depth) {
+    reseed(0x5EED0C00ULL);   // the same key as cmd_fixtures
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    g_logging = true;
+    reseed(0x5EED0CC0ULL);
+    std::vector<uint64_t> sx;
+    Cipher x = run_logged([&] { return enc_value(pk, sk, 2); }, sx);
+    write_ct(dir + "/chainx_x.ct", {x}, true);
+    dump_R(dir + "/chainx_x_R.u64", base_layer_R(pk, sk, x));
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ", \"depth\": " << depth << ", \"x_stream\": " << sx.size()
+       << ",\n  \"steps\": [";
+    const size_t before = g_log.size();
+    Cipher c = x;
+    for (int k = 1; k <= depth; ++k) {
+        const size_t b0 = g_log.size();
+        c = ct_mul(pk, c, x);
+        js << (k > 1 ? ", " : "") << "{\"edges\": " << c.E.size() << ", \"layers\": " << c.L.size()
+           << ", \"stream\": " << (g_log.size() - b0) << "}";
+        std::printf("chainx step %d edges %zu\n", k, c.E.size());
+        std::fflush(stdout);
+    }
+    std::vector<uint64_t> st(g_log.begin() + (long)before, g_log.end());
+    write_u64(dir + "/chainx_stream.u64", st);
+    write_ct(dir + "/chainx_final.ct", {c}, false);
+    write_layers(dir + "/chainx_final_layers.u64", c);
+    write_u64(dir + "/chainx_final_sigdig.u64", sigma_digests(c));
+    g_logging = false;
+    const Fp d = dec_value(pk, sk, c);
+    js << "],\n  \"stream\": " << st.size() << ", \"dec\": " << fpjson(d) << "\n}\n";
+    std::ofstream(dir + "/chainx_manifest.json") << js.str();
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: ref_harness fp|fixtures|time_mul ...\n"); return 2; }
     std::string cmd = argv[1];
@@ -704,6 +746,10 @@ int main(int argc, char** argv) {
         int cs = argc > 4 ? std::atoi(argv[4]) : 3;
         int ss = argc > 5 ? std::atoi(argv[5]) : 2;
         cmd_fixtures(argv[2], np, cs, ss);
+        return 0;
+    }
+    if (cmd == "chainx" && argc >= 3) {
+        cmd_chainx(argv[2], argc > 3 ? std::atoi(argv[3]) : 4);
         return 0;
     }
     if (cmd == "encdepth" && argc >= 3) {

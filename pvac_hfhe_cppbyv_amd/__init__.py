@@ -27,6 +27,7 @@ LAYER_DT = np.dtype([("rule", "<u4"), ("pa", "<u4"), ("pb", "<u4"), ("pad", "<u4
 FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE, FP_INV = 0, 1, 2, 3, 4, 5
 MUL_WITH_SIGMA, MUL_ORDER_CANONICAL = 0x1, 0x2
 CHAIN_CHECK_GSUM = 0x100
+CHAIN_STAGE_INPUTS = 0x200
 CHAIN_MAX_DEPTH = 32
 ENC_WITH_SIGMA = 0x1
 
@@ -78,6 +79,9 @@ class Plan(C.Structure):
 
 FILL_NONCES_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p)
 ON_CHUNK_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.POINTER(CtBatch), C.c_void_p)
+# pvac_chain_step_fn(user, step, first_input, A, X, C, dev_words, n_words, stream): nonces_at / after_step / salts_at
+STEP_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(CtBatch), C.POINTER(CtBatch),
+                      C.POINTER(CtBatch), C.c_void_p, C.c_uint64, C.c_void_p)
 
 
 class ChainOpts(C.Structure):
@@ -85,7 +89,9 @@ class ChainOpts(C.Structure):
                 ("flags", C.c_uint32), ("pad", C.c_uint32), ("digest_n", C.c_uint64), ("digest_out", C.c_void_p),
                 ("count_n", C.c_uint64), ("count_out", C.c_void_p), ("fill_nonces", FILL_NONCES_CB),
                 ("on_chunk", ON_CHUNK_CB),
-                ("user", C.c_void_p)]
+                ("user", C.c_void_p), ("nonces_at", STEP_CB), ("after_step", STEP_CB), ("salts_at", STEP_CB),
+                ("devices", C.c_void_p), ("n_devices", C.c_uint32), ("pad2", C.c_uint32),
+                ("sumdigest_out", C.c_void_p)]
 
 
 class ChainStats(C.Structure):
@@ -137,7 +143,10 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_fill_nonces": ([vp, u64, u64, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch), vp], i32),
         "pvac_hip_fill_random": ([vp, u64, vp, C.c_size_t], i32),
         "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
+        "pvac_hip_batch_sumdigest": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_bucket_count": ([u64], u64),
+        "pvac_hip_chain_partition": ([u64, u64, u32, vp], i32),
+        "pvac_hip_memcpy": ([vp, vp, C.c_size_t, vp], i32),
         "pvac_hip_ctx_set_powg": ([vp, vp, u32], i32),
         "pvac_hip_ctx_set_secret": ([vp, vp, vp, u32, u32, u32, u32], i32),
         "pvac_hip_ctx_set_H_digest": ([vp, vp], i32),
@@ -412,24 +421,36 @@ class Engine:
         return C_
 
     def ct_mul_chain(self, X: DeviceBatch, depth, nonce_seed=0x5EED0040, streams=4, chunk=1024, check_gsum=False,
-                     digest_n=0, canonical=False, fill_nonces=None, on_chunk=None, count_n=None):
+                     digest_n=0, canonical=False, fill_nonces=None, on_chunk=None, count_n=None, sigma=False,
+                     devices=None, stage_inputs=False, nonces_at=None, after_step=None, salts_at=None,
+                     sumdigest=False):
         """c_0 = x, c_k = ct_mul(c_{k-1}, x) to `depth` for every input x of X (tests/test_main.cpp:289-295)
         on `streams` internal worker streams in chunks of `chunk` inputs (pvac_hip_ct_mul_chain).
         Returns a dict of the call's statistics; with digest_n > 0 also the final digests / edge
         counts of inputs [0, digest_n) (numpy u64). fill_nonces / on_chunk: optional ctypes callbacks
         (FILL_NONCES_CB / ON_CHUNK_CB), called from the library's worker threads. count_n: inputs whose
         final edge counts are returned (default digest_n; the FNV-1a digest walks a cipher's edges
-        serially, a count is a copy)."""
+        serially, a count is a copy). sigma: the final step with sigmas (needs H). devices: GPU
+        ordinals, one contiguous range of whole chunks each (stage_inputs: ranges after the first copy
+        their chunks to worker buffers even on this device). nonces_at / after_step / salts_at: STEP_CB
+        hooks (include/pvac_hip.h)."""
         torch = self.torch
         dn = min(int(digest_n), X.n)
         cn = dn if count_n is None else min(int(count_n), X.n)
         dig = torch.zeros(max(dn, 1), dtype=torch.int64, device=self.device)
         cnt = torch.zeros(max(cn, 1), dtype=torch.int64, device=self.device)
+        sdg = torch.zeros(max(cn, 1), dtype=torch.int64, device=self.device) if sumdigest and cn else None
+        devs = (C.c_int * len(devices))(*devices) if devices else None
         o = ChainOpts(depth=depth, streams=streams, chunk=chunk, nonce_seed=nonce_seed,
-                      flags=(CHAIN_CHECK_GSUM if check_gsum else 0) | (MUL_ORDER_CANONICAL if canonical else 0),
+                      flags=(CHAIN_CHECK_GSUM if check_gsum else 0) | (MUL_ORDER_CANONICAL if canonical else 0) |
+                      (MUL_WITH_SIGMA if sigma else 0) | (CHAIN_STAGE_INPUTS if stage_inputs else 0),
                       pad=0, digest_n=dn, digest_out=C.c_void_p(dig.data_ptr()) if dn else None,
                       count_n=cn, count_out=C.c_void_p(cnt.data_ptr()) if cn else None,
-                      fill_nonces=fill_nonces or FILL_NONCES_CB(), on_chunk=on_chunk or ON_CHUNK_CB(), user=None)
+                      fill_nonces=fill_nonces or FILL_NONCES_CB(), on_chunk=on_chunk or ON_CHUNK_CB(), user=None,
+                      nonces_at=nonces_at or STEP_CB(), after_step=after_step or STEP_CB(),
+                      salts_at=salts_at or STEP_CB(), devices=C.cast(devs, C.c_void_p) if devs else None,
+                      n_devices=len(devices) if devices else 0, pad2=0,
+                      sumdigest_out=C.c_void_p(sdg.data_ptr()) if sdg is not None else None)
         st = ChainStats()
         sx = X.struct()
         self._check(self.lib.pvac_hip_ct_mul_chain(self.ctx, C.byref(sx), C.byref(o), C.byref(st)))
@@ -440,6 +461,8 @@ class Engine:
             res["digests"] = dig[:dn].cpu().numpy().view(np.uint64).copy()
         if cn:
             res["counts"] = cnt[:cn].cpu().numpy().view(np.uint64).copy()
+        if sdg is not None:
+            res["sumdigests"] = sdg[:cn].cpu().numpy().view(np.uint64).copy()
         return res
 
     def ct_mul_redo_count(self):
@@ -473,7 +496,11 @@ class Engine:
 
     ISSUE_OPS = ("v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_lshlrev_b32", "v_min_u32", "v_add3_u32",
                  "v_pk_add_u16", "v_fma_f32", "v_mul_lo_u32", "v_mul_hi_u32", "v_cndmask_b32", "v_bfe_u32",
-                 "v_add_co_u32", "v_and_or_b32", "v_pk_min_u16", "v_bitop3_b32", "v_mad_u64_u32")
+                 "v_add_co_u32", "v_and_or_b32", "v_pk_min_u16", "v_bitop3_b32", "v_mad_u64_u32",
+                 "v_cndmask_b32_e64", "v_lshl_add_u32", "v_mov_b32_dpp", "v_perm_b32", "v_mul_u32_u24", "v_sub_u32",
+                 "v_max3_u32", "v_cmp+v_cndmask_vcc", "v_cndmask_b32_e64_vcc", "v_addc_co_u32_vcc",
+                 "v_addc_co_u32_e64_sgpr", "v_cmp_e64+v_cndmask_e64", "v_min_u32_e64", "v_add_u32_e64", "v_and_b32",
+                 "v_or_b32", "v_lshrrev_b32", "v_mov_b32", "v_max_u32")
 
     def issue_probe(self, op, waves_per_simd=8):
         """Per-opcode VALU issue rate (pvac_hip_issue_probe): (wave64 inst/s chip-wide, shader clock Hz
@@ -578,6 +605,13 @@ class Engine:
         self._check(self.lib.pvac_hip_batch_digest(self.ctx, C.byref(sx), C.c_void_p(out.data_ptr())))
         return out[:X.n]
 
+    def sumdigest(self, X: DeviceBatch):
+        """Position-keyed parallel digest per cipher (pvac_hip_batch_sumdigest)."""
+        out = self.torch.empty(max(X.n, 1), dtype=self.torch.int64, device=self.device)
+        sx = X.struct()
+        self._check(self.lib.pvac_hip_batch_sumdigest(self.ctx, C.byref(sx), C.c_void_p(out.data_ptr())))
+        return out[:X.n]
+
     # ---- timing
     def timing(self, on=True):
         self._check(self.lib.pvac_hip_timing_enable(self.ctx, int(on)))
@@ -592,5 +626,5 @@ class Engine:
 
 
 __all__ = ["Engine", "DeviceBatch", "HostCipher", "PvacError", "LAYER_DT", "load_library", "FP_ADD", "FP_SUB",
-           "FP_MUL", "FP_NEG", "FP_SCALE", "FP_INV", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL", "CHAIN_CHECK_GSUM",
+           "FP_MUL", "FP_NEG", "FP_SCALE", "FP_INV", "MUL_WITH_SIGMA", "MUL_ORDER_CANONICAL", "CHAIN_CHECK_GSUM", "CHAIN_STAGE_INPUTS", "STEP_CB",
            "ChainOpts", "ChainStats", "FILL_NONCES_CB", "ON_CHUNK_CB"]

@@ -80,6 +80,7 @@ hipError_t launch_gen_fresh(uint64_t seed, uint64_t first, uint32_t epl, uint32_
 hipError_t launch_fill_nonces(uint64_t seed, uint64_t first, const pvac_ct_batch& A, const pvac_ct_batch& B,
                               const uint64_t* c_l_off, uint64_t* out, hipStream_t st);
 hipError_t launch_batch_digest(const pvac_ct_batch& X, uint64_t* out, hipStream_t st);
+hipError_t launch_batch_sumdigest(const pvac_ct_batch& X, uint64_t* out, hipStream_t st);
 hipError_t launch_ct_scale(const pvac_ct_batch& X, uint64_t slo, uint64_t shi, hipStream_t st);
 
 // x mod d for a runtime divisor d < 2^32 without a 64-bit division: m = floor((2^64-1)/d),
@@ -358,6 +359,7 @@ hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, con
                              const uint64_t* powg, uint32_t Bm, const unsigned int* mx_host, uint32_t* status,
                              unsigned long long* n_bad, int num_cus, hipStream_t st);
 // pvac_hip_ct_mul_chain statistics: out[0] += sum |C.E|, out[1] += sum |A.E| |X.E| (k_check.hip)
+hipError_t launch_stage_rows(const pvac_ct_batch& src, const pvac_ct_batch& dst, hipStream_t st);
 hipError_t launch_chain_stats(const pvac_ct_batch& A, const pvac_ct_batch& X, const pvac_ct_batch& C,
                               unsigned long long* out, hipStream_t st);
 constexpr uint64_t kNoGrp = ~0ull;

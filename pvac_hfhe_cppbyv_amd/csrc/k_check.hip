@@ -247,6 +247,31 @@ __global__ __launch_bounds__(256) void k_chain_stats(const uint64_t* a_cnt, cons
 }
 }  // namespace
 
+// chain worker staging (pvac_hip_ct_mul_chain, a chunk whose inputs live on another device or with
+// PVAC_CHAIN_STAGE_INPUTS): cipher i's rows from src (its own offsets) to dst (offsets scanned from
+// the counts already copied into dst); one workgroup per cipher, coalesced u64 copies; src pointers
+// may be another GPU's memory (peer reads over xGMI)
+__global__ __launch_bounds__(256) void k_stage_rows(pvac_ct_batch src, pvac_ct_batch dst) {
+    const uint64_t i = blockIdx.x;
+    const uint64_t nl = dst.l_cnt[i], ne = dst.e_cnt[i];
+    const uint64_t* sL = (const uint64_t*)(src.layers + src.l_off[i]);
+    uint64_t* dL = (uint64_t*)(dst.layers + dst.l_off[i]);
+    static_assert(sizeof(pvac_layer) == 40, "layer record = 5 u64");
+    for (uint64_t w = threadIdx.x; w < 5 * nl; w += 256) dL[w] = sL[w];
+    const uint64_t se = src.e_off[i], de = dst.e_off[i];
+    for (uint64_t e = threadIdx.x; e < ne; e += 256) {
+        dst.meta[de + e] = src.meta[se + e];
+        dst.w_lo[de + e] = src.w_lo[se + e];
+        dst.w_hi[de + e] = src.w_hi[se + e];
+    }
+}
+
+hipError_t launch_stage_rows(const pvac_ct_batch& src, const pvac_ct_batch& dst, hipStream_t st) {
+    if (!dst.n) return hipSuccess;
+    hipLaunchKernelGGL(k_stage_rows, dim3((unsigned)dst.n), dim3(256), 0, st, src, dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_chain_stats(const pvac_ct_batch& A, const pvac_ct_batch& X, const pvac_ct_batch& C,
                               unsigned long long* out, hipStream_t st) {
     if (!A.n) return hipSuccess;

@@ -197,6 +197,30 @@ __global__ void k_batch_digest(pvac_ct_batch X, uint64_t* out) {
     out[i] = h;
 }
 
+// Position-keyed digest: sum over a cipher's edges e of mix64(e, meta, w_lo, w_hi) (mod 2^64). Order-
+// sensitive through the position e, but a sum, so one workgroup per cipher reduces it in parallel
+// (the FNV digest above walks the edges serially: ~12 ms per depth-8 cipher).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_batch_sumdigest(pvac_ct_batch X, uint64_t* out) {
+    __shared__ uint64_t part[4];
+    const uint64_t i = blockIdx.x;
+    const uint64_t o = X.e_off[i], c = X.e_cnt[i];
+    uint64_t acc = 0;
+    for (uint64_t e = threadIdx.x; e < c; e += 256) {
+        const uint64_t m = X.meta[o + e], lo = X.w_lo[o + e], hi = X.w_hi[o + e];
+        acc += mix64(mix64(mix64(e * 0x9E3779B97F4A7C15ULL ^ m) ^ lo) ^ hi);
+    }
+    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[i] = part[0] + part[1] + part[2] + part[3] + c;
+}
+
 // ct_scale (arithmetic.hpp:33-37), in place: 32 lanes per cipher, eight ciphers per workgroup
 // (fresh ciphers have ~40 edges; a workgroup per cipher left most lanes idle)
 __global__ __launch_bounds__(256) void k_ct_scale(pvac_ct_batch X, uint64_t slo, uint64_t shi) {
@@ -277,6 +301,12 @@ hipError_t launch_gen_fresh(uint64_t seed, uint64_t first, uint32_t epl, uint32_
 hipError_t launch_batch_digest(const pvac_ct_batch& X, uint64_t* out, hipStream_t st) {
     if (!X.n) return hipSuccess;
     hipLaunchKernelGGL(k_batch_digest, dim3((unsigned)((X.n + 255) / 256)), dim3(256), 0, st, X, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_batch_sumdigest(const pvac_ct_batch& X, uint64_t* out, hipStream_t st) {
+    if (!X.n) return hipSuccess;
+    hipLaunchKernelGGL(k_batch_sumdigest, dim3((unsigned)X.n), dim3(256), 0, st, X, out);
     return hipGetLastError();
 }
 

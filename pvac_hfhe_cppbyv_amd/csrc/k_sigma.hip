@@ -839,6 +839,35 @@ void sigma_tables_free(sigma_tables& T) {
     T = sigma_tables{};
 }
 
+// A copy of src's device tables for a context on dst_dev (same or another device: peer copies
+// over xGMI); synchronous on st, which must belong to dst_dev.
+hipError_t sigma_tables_clone(sigma_tables& dst, const sigma_tables& src, int dst_dev, int src_dev, hipStream_t st) {
+    sigma_tables_free(dst);
+    if (!src.ready) return hipSuccess;
+    const size_t nr = (size_t)src.n_cols * src.width * 2, nc = (size_t)src.n_cols * 4,
+                 nd = (size_t)src.n_cols * kDeltaBytes;
+    auto one = [&](void** d, const void* s, size_t bytes) -> hipError_t {
+        if (!s) return hipSuccess;
+        hipError_t e = hipMalloc(d, bytes);
+        if (e == hipSuccess) e = hipMemcpyPeerAsync(*d, dst_dev, s, src_dev, bytes, st);
+        return e;
+    };
+    hipError_t e = one((void**)&dst.rows, src.rows, nr);
+    if (e == hipSuccess) e = one((void**)&dst.counts, src.counts, nc);
+    if (e == hipSuccess) e = one((void**)&dst.rows_fast, src.rows_fast, nr);
+    if (e == hipSuccess) e = one((void**)&dst.rows_delta, src.rows_delta, nd);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        sigma_tables_free(dst);
+        return e;
+    }
+    dst.width = src.width;
+    dst.n_cols = src.n_cols;
+    dst.full = src.full;
+    dst.ready = true;
+    return hipSuccess;
+}
+
 static hipError_t alloc_tables(sigma_tables& T, uint32_t n_cols, uint32_t width) {
     sigma_tables_free(T);
     hipError_t e = hipMalloc(&T.rows, (size_t)n_cols * width * 2);

@@ -201,10 +201,14 @@ __global__ __launch_bounds__(kUB) void k_probe_mfma8(uint64_t* out, uint32_t ite
                    "+v"(r[14]), "+v"(r[15])                                                                  \
                  : "v"(a), "v"(b)                                                                            \
                  : "vcc")
-#define PVAC_IPS(I, T0, T1, T2, T3)                                                                         \
-    I " %0," T0 "\n\t" I " %1," T1 "\n\t" I " %2," T2 "\n\t" I " %3," T3 "\n\t" I " %4," T0 "\n\t" I " %5," \
-    T1 "\n\t" I " %6," T2 "\n\t" I " %7," T3 "\n\t" I " %8," T0 "\n\t" I " %9," T1 "\n\t" I " %10," T2   \
-    "\n\t" I " %11," T3 "\n\t" I " %12," T0 "\n\t" I " %13," T1 "\n\t" I " %14," T2 "\n\t" I " %15," T3
+// 16 instructions; accumulator k is the destination and the first-listed source: "I %k, PRE%kPOST"
+#define PVAC_IPK(I, PRE, POST, k) I " %" #k ", " PRE "%" #k POST "\n\t"
+#define PVAC_IPS(I, PRE, POST)                                                                              \
+    PVAC_IPK(I, PRE, POST, 0) PVAC_IPK(I, PRE, POST, 1) PVAC_IPK(I, PRE, POST, 2) PVAC_IPK(I, PRE, POST, 3)  \
+    PVAC_IPK(I, PRE, POST, 4) PVAC_IPK(I, PRE, POST, 5) PVAC_IPK(I, PRE, POST, 6) PVAC_IPK(I, PRE, POST, 7)  \
+    PVAC_IPK(I, PRE, POST, 8) PVAC_IPK(I, PRE, POST, 9) PVAC_IPK(I, PRE, POST, 10)                           \
+    PVAC_IPK(I, PRE, POST, 11) PVAC_IPK(I, PRE, POST, 12) PVAC_IPK(I, PRE, POST, 13)                         \
+    PVAC_IPK(I, PRE, POST, 14) PVAC_IPK(I, PRE, POST, 15)
 
 template <int OP>
 __global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint32_t seed) {
@@ -219,23 +223,22 @@ __global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint
     }
     for (uint32_t i = 0; i < iters; ++i) {
         // each accumulator's operands: itself and the loop-invariant a / b (16 independent chains)
-        if constexpr (OP == 0) PVAC_IP16(PVAC_IPS("v_add_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 1) PVAC_IP16(PVAC_IPS("v_xor_b32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 2) PVAC_IP16(PVAC_IPS("v_alignbit_b32", "%0,%16,7", "%1,%17,7", "%2,%16,9", "%3,%17,9"));
-        if constexpr (OP == 3) PVAC_IP16(PVAC_IPS("v_lshlrev_b32", "%16,%0", "%17,%1", "%16,%2", "%17,%3"));
-        if constexpr (OP == 4) PVAC_IP16(PVAC_IPS("v_min_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 5) PVAC_IP16(PVAC_IPS("v_add3_u32", "%0,%16,%17", "%1,%17,%16", "%2,%16,%16", "%3,%17,%17"));
-        if constexpr (OP == 6) PVAC_IP16(PVAC_IPS("v_pk_add_u16", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 7) PVAC_IP16(PVAC_IPS("v_fma_f32", "%0,%16,%17", "%1,%17,%16", "%2,%16,%16", "%3,%17,%17"));
-        if constexpr (OP == 8) PVAC_IP16(PVAC_IPS("v_mul_lo_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 9) PVAC_IP16(PVAC_IPS("v_mul_hi_u32", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 10) PVAC_IP16(PVAC_IPS("v_cndmask_b32", "%0,%16,vcc", "%1,%17,vcc", "%2,%16,vcc", "%3,%17,vcc"));
-        if constexpr (OP == 11) PVAC_IP16(PVAC_IPS("v_bfe_u32", "%0,%16,12", "%1,%17,12", "%2,%16,12", "%3,%17,12"));
-        if constexpr (OP == 12) PVAC_IP16(PVAC_IPS("v_add_co_u32", "vcc,%0,%16", "vcc,%1,%17", "vcc,%2,%16", "vcc,%3,%17"));
-        if constexpr (OP == 13) PVAC_IP16(PVAC_IPS("v_and_or_b32", "%0,%16,%17", "%1,%17,%16", "%2,%16,%16", "%3,%17,%17"));
-        if constexpr (OP == 14) PVAC_IP16(PVAC_IPS("v_pk_min_u16", "%0,%16", "%1,%17", "%2,%16", "%3,%17"));
-        if constexpr (OP == 15) PVAC_IP16(PVAC_IPS("v_bitop3_b32", "%0,%16,%17 bitop3:0x96", "%1,%17,%16 bitop3:0x96",
-                                                   "%2,%16,%16 bitop3:0x96", "%3,%17,%17 bitop3:0x96"));
+        if constexpr (OP == 0) PVAC_IP16(PVAC_IPS("v_add_u32", "", ",%16"));
+        if constexpr (OP == 1) PVAC_IP16(PVAC_IPS("v_xor_b32", "", ",%16"));
+        if constexpr (OP == 2) PVAC_IP16(PVAC_IPS("v_alignbit_b32", "", ",%16,7"));
+        if constexpr (OP == 3) PVAC_IP16(PVAC_IPS("v_lshlrev_b32", "%16,", ""));
+        if constexpr (OP == 4) PVAC_IP16(PVAC_IPS("v_min_u32", "", ",%16"));
+        if constexpr (OP == 5) PVAC_IP16(PVAC_IPS("v_add3_u32", "", ",%16,%17"));
+        if constexpr (OP == 6) PVAC_IP16(PVAC_IPS("v_pk_add_u16", "", ",%16"));
+        if constexpr (OP == 7) PVAC_IP16(PVAC_IPS("v_fma_f32", "", ",%16,%17"));
+        if constexpr (OP == 8) PVAC_IP16(PVAC_IPS("v_mul_lo_u32", "", ",%16"));
+        if constexpr (OP == 9) PVAC_IP16(PVAC_IPS("v_mul_hi_u32", "", ",%16"));
+        if constexpr (OP == 10) PVAC_IP16(PVAC_IPS("v_cndmask_b32", "%16,", ",vcc"));
+        if constexpr (OP == 11) PVAC_IP16(PVAC_IPS("v_bfe_u32", "", ",%16,12"));
+        if constexpr (OP == 12) PVAC_IP16(PVAC_IPS("v_add_co_u32", "vcc,", ",%16"));
+        if constexpr (OP == 13) PVAC_IP16(PVAC_IPS("v_and_or_b32", "", ",%16,%17"));
+        if constexpr (OP == 14) PVAC_IP16(PVAC_IPS("v_pk_min_u16", "", ",%16"));
+        if constexpr (OP == 15) PVAC_IP16(PVAC_IPS("v_bitop3_b32", "", ",%16,%17 bitop3:0x96"));
         if constexpr (OP == 16) {
             // v_mad_u64_u32 on 8 64-bit accumulators (register pairs r[2k], r[2k + 1]): 8 per iteration
             uint64_t* x = (uint64_t*)r;
@@ -248,6 +251,54 @@ __global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint
                 : "v"(a), "v"(b)
                 : "vcc");
         }
+        if constexpr (OP == 17) PVAC_IP16(PVAC_IPS("v_cndmask_b32_e64", "%16,", ",s[4:5]"));
+        if constexpr (OP == 18) PVAC_IP16(PVAC_IPS("v_lshl_add_u32", "", ",3,%16"));
+        if constexpr (OP == 19) PVAC_IP16(PVAC_IPS("v_mov_b32_dpp", "", " row_shr:1 row_mask:0xf bank_mask:0xf"));
+        if constexpr (OP == 20) PVAC_IP16(PVAC_IPS("v_perm_b32", "", ",%16,%17"));
+        if constexpr (OP == 21) PVAC_IP16(PVAC_IPS("v_mul_u32_u24", "", ",%16"));
+        if constexpr (OP == 22) PVAC_IP16(PVAC_IPS("v_sub_u32", "%16,", ""));
+        if constexpr (OP == 23) PVAC_IP16(PVAC_IPS("v_max3_u32", "", ",%16,%17"));
+        // VCC readers (the compiler's v_cmp + v_cndmask_b32_e32 / v_addc_co_u32_e32 pattern)
+        if constexpr (OP == 24) {   // 8 x (v_cmp writing vcc, VOP2 v_cndmask reading it): 16 instructions
+            asm volatile(
+                "v_cmp_gt_u32 vcc, %0, %16\n\tv_cndmask_b32 %1, %16, %1, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %2, %16\n\tv_cndmask_b32 %3, %16, %3, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %4, %16\n\tv_cndmask_b32 %5, %16, %5, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %6, %16\n\tv_cndmask_b32 %7, %16, %7, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %8, %16\n\tv_cndmask_b32 %9, %16, %9, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %10, %16\n\tv_cndmask_b32 %11, %16, %11, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %12, %16\n\tv_cndmask_b32 %13, %16, %13, vcc\n\t"
+                "v_cmp_gt_u32 vcc, %14, %16\n\tv_cndmask_b32 %15, %16, %15, vcc"
+                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
+                  "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15])
+                : "v"(a), "v"(b)
+                : "vcc");
+        }
+        if constexpr (OP == 25) PVAC_IP16(PVAC_IPS("v_cndmask_b32_e64", "%16,", ",vcc"));
+        if constexpr (OP == 26) PVAC_IP16(PVAC_IPS("v_addc_co_u32", "vcc,", ",%16,vcc"));
+        if constexpr (OP == 27) PVAC_IP16(PVAC_IPS("v_addc_co_u32_e64", "s[4:5],", ",%16,s[6:7]"));
+        if constexpr (OP == 28) {   // 8 x (v_cmp_e64 writing an SGPR pair, v_cndmask_e64 reading it)
+            asm volatile(
+                "v_cmp_gt_u32_e64 s[4:5], %0, %16\n\tv_cndmask_b32_e64 %1, %16, %1, s[4:5]\n\t"
+                "v_cmp_gt_u32_e64 s[6:7], %2, %16\n\tv_cndmask_b32_e64 %3, %16, %3, s[6:7]\n\t"
+                "v_cmp_gt_u32_e64 s[4:5], %4, %16\n\tv_cndmask_b32_e64 %5, %16, %5, s[4:5]\n\t"
+                "v_cmp_gt_u32_e64 s[6:7], %6, %16\n\tv_cndmask_b32_e64 %7, %16, %7, s[6:7]\n\t"
+                "v_cmp_gt_u32_e64 s[4:5], %8, %16\n\tv_cndmask_b32_e64 %9, %16, %9, s[4:5]\n\t"
+                "v_cmp_gt_u32_e64 s[6:7], %10, %16\n\tv_cndmask_b32_e64 %11, %16, %11, s[6:7]\n\t"
+                "v_cmp_gt_u32_e64 s[4:5], %12, %16\n\tv_cndmask_b32_e64 %13, %16, %13, s[4:5]\n\t"
+                "v_cmp_gt_u32_e64 s[6:7], %14, %16\n\tv_cndmask_b32_e64 %15, %16, %15, s[6:7]"
+                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
+                  "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15])
+                : "v"(a), "v"(b)
+                : "s4", "s5", "s6", "s7");
+        }
+        if constexpr (OP == 29) PVAC_IP16(PVAC_IPS("v_min_u32_e64", "", ",%16"));
+        if constexpr (OP == 30) PVAC_IP16(PVAC_IPS("v_add_u32_e64", "", ",%16"));
+        if constexpr (OP == 31) PVAC_IP16(PVAC_IPS("v_and_b32", "", ",%16"));
+        if constexpr (OP == 32) PVAC_IP16(PVAC_IPS("v_or_b32", "", ",%16"));
+        if constexpr (OP == 33) PVAC_IP16(PVAC_IPS("v_lshrrev_b32", "%16,", ""));
+        if constexpr (OP == 34) PVAC_IP16(PVAC_IPS("v_mov_b32", "", ""));
+        if constexpr (OP == 35) PVAC_IP16(PVAC_IPS("v_max_u32", "", ",%16"));
     }
     uint32_t acc = 0;
 #pragma unroll
@@ -261,8 +312,9 @@ __global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint
 }
 #undef PVAC_IP16
 #undef PVAC_IPS
+#undef PVAC_IPK
 
-constexpr int kIssueOps = 17;
+constexpr int kIssueOps = 36;
 using probe_fn = void (*)(uint64_t*, uint64_t*, uint32_t, uint32_t);
 template <int... I>
 constexpr auto issue_table(std::integer_sequence<int, I...>) {

@@ -49,6 +49,8 @@ struct chain_set {
     uint64_t* w_lo = nullptr;
     uint64_t* w_hi = nullptr;
     size_t e_cap = 0;
+    uint64_t* sigma = nullptr;   // final step with PVAC_MUL_WITH_SIGMA: 1 KiB per edge slot
+    size_t s_cap = 0;            // edge slots of sigma
 };
 
 }  // namespace
@@ -132,11 +134,18 @@ struct pvac_hip_ctx {
     uint64_t arena_cap_words = 0;
     bool large_no_direct = false;   // the redo run: every pair on the full (per-key sums) layout
     // pvac_hip_ct_mul_chain: worker contexts (own stream / arena), and a worker's own buffers
-    std::vector<pvac_hip_ctx*> chain_kids;
+    std::vector<pvac_hip_ctx*> chain_kids;   // [range j * streams + w] of the last call's layout
     chain_set chain_bufs[2];
+    chain_set chain_stage;                   // a worker's staged chunk inputs (another device, or STAGE)
     uint64_t* chain_nonces = nullptr;
     size_t chain_nonce_cap = 0;
+    uint64_t* chain_salts = nullptr;         // final-step salts (WITH_SIGMA)
+    size_t chain_salt_cap = 0;
+    uint64_t* chain_out = nullptr;           // digests / counts of a chunk before the copy to X's device
+    size_t chain_out_cap = 0;
     unsigned long long* chain_stats = nullptr;   // [2 * PVAC_CHAIN_MAX_DEPTH]
+    uint64_t H_gen = 0;                      // bumped whenever H is set (a worker's copy follows it)
+    uint64_t H_from = 0;                     // worker: the parent's H_gen its H copy was taken from
 };
 
 namespace {
@@ -434,11 +443,12 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     c->chain_kids.clear();
     if (c->stream) hipStreamSynchronize(c->stream);
     flush_timers(c);
-    for (chain_set& b : c->chain_bufs)
-        for (void* q : {(void*)b.l_off, (void*)b.l_cnt, (void*)b.e_off, (void*)b.e_cnt, (void*)b.layers, (void*)b.meta,
-                        (void*)b.w_lo, (void*)b.w_hi})
+    for (chain_set* b : {&c->chain_bufs[0], &c->chain_bufs[1], &c->chain_stage})
+        for (void* q : {(void*)b->l_off, (void*)b->l_cnt, (void*)b->e_off, (void*)b->e_cnt, (void*)b->layers,
+                        (void*)b->meta, (void*)b->w_lo, (void*)b->w_hi, (void*)b->sigma})
             if (q) hipFreeAsync(q, c->stream);
-    if (c->chain_nonces) hipFreeAsync(c->chain_nonces, c->stream);
+    for (void* q : {(void*)c->chain_nonces, (void*)c->chain_salts, (void*)c->chain_out})
+        if (q) hipFreeAsync(q, c->stream);
     if (c->stream) hipStreamSynchronize(c->stream);
     hipFree(c->chain_stats);
     hipFree(c->nb_table);
@@ -1130,6 +1140,7 @@ int pvac_hip_ctx_set_H(pvac_hip_ctx* c, const uint64_t* H, uint32_t n_cols, uint
     try {
         const int rc = hip_fail(c, sigma_tables_from_dense(c->H, c->prm, H, c->stream), "set_H");
         if (rc) return rc;
+        ++c->H_gen;
         // H_digest = SHA-256("H|v2" || le64 m || le64 n || le64 wt || column bytes) (matrix.hpp:218-250)
         const size_t colbytes = (c->prm.m_bits + 7) / 8;
         std::vector<uint8_t> msg(28 + (size_t)n_cols * colbytes);
@@ -1155,6 +1166,7 @@ int pvac_hip_ctx_gen_H(pvac_hip_ctx* c, uint8_t digest[32]) {
         uint8_t d[32];
         const int rc = hip_fail(c, sigma_tables_generate(c->H, c->prm, d, c->stream), "gen_H");
         if (rc) return rc;
+        ++c->H_gen;
         std::memcpy(c->H_digest, d, 32);
         c->have_digest = true;
         if (digest) std::memcpy(digest, d, 32);
@@ -1512,6 +1524,11 @@ int pvac_hip_batch_digest(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* out
     return hip_fail(c, launch_batch_digest(*X, out, c->stream), "batch_digest");
 }
 
+int pvac_hip_batch_sumdigest(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* out) {
+    if (!c || !batch_ok(X) || (X->n && !out)) return PVAC_EINVAL;
+    return hip_fail(c, launch_batch_sumdigest(*X, out, c->stream), "batch_sumdigest");
+}
+
 // ---------------------------------------------------------------- depth chains
 }  // extern "C"
 
@@ -1536,11 +1553,17 @@ hipError_t grow_async(T*& p, size_t& cap, size_t need, hipStream_t st) {
     return e;
 }
 
+struct chain_range {
+    uint64_t end = 0;               // last input (exclusive) of this device range
+    std::atomic<uint64_t> next{0};  // next chunk's first input
+};
+
 struct chain_shared {
     const pvac_ct_batch* X = nullptr;
     const pvac_chain_opts* o = nullptr;
     uint64_t chunk = 0;
-    std::atomic<uint64_t> next{0};
+    int x_dev = 0;                  // the device X (and the digest / count outputs) live on
+    chain_range* ranges = nullptr;
     std::atomic<int> stop{0};
     std::mutex mu;
     int rc = PVAC_OK;
@@ -1571,9 +1594,118 @@ pvac_ct_batch chain_view(const pvac_ct_batch& X, uint64_t c0, uint64_t k) {
     return v;
 }
 
-// one worker: chunks in input order from the shared counter, depth steps of plan + exec each on
-// this context's stream, the final c_depth to the digests / on_chunk
-void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
+// the inputs of one chunk copied into the worker's own buffers (compact CSR): counts by peer
+// copy, offsets by an exclusive scan, rows by k_stage_rows (peer reads when X lives elsewhere)
+bool stage_chunk(pvac_hip_ctx* k, chain_shared* sh, const pvac_ct_batch& src, pvac_ct_batch& out) {
+    chain_set& S = k->chain_stage;
+    const uint64_t kk = src.n;
+    auto hipchk = [&](hipError_t e, const char* where) {
+        if (e == hipSuccess) return true;
+        sh->failed(e == hipErrorOutOfMemory ? PVAC_ENOMEM : PVAC_EDEVICE,
+                   std::string("ct_mul_chain: stage ") + where + ": " + hipGetErrorString(e));
+        return false;
+    };
+    if (kk > S.n_cap) {
+        size_t c1 = S.n_cap, c2 = S.n_cap, c3 = S.n_cap, c4 = S.n_cap;
+        if (!hipchk(grow_async(S.l_off, c1, kk, k->stream), "alloc") || !hipchk(grow_async(S.l_cnt, c2, kk, k->stream), "alloc") ||
+            !hipchk(grow_async(S.e_off, c3, kk, k->stream), "alloc") || !hipchk(grow_async(S.e_cnt, c4, kk, k->stream), "alloc"))
+            return false;
+        S.n_cap = std::min(std::min(c1, c2), std::min(c3, c4));
+    }
+    if (ensure_pairs(k, kk)) {
+        sh->failed(PVAC_ENOMEM, "ct_mul_chain: stage scratch: " + k->err);
+        return false;
+    }
+    const int sd = sh->x_dev, dd = k->device;
+    if (!hipchk(hipMemcpyPeerAsync(S.l_cnt, dd, src.l_cnt, sd, kk * 8, k->stream), "counts") ||
+        !hipchk(hipMemcpyPeerAsync(S.e_cnt, dd, src.e_cnt, sd, kk * 8, k->stream), "counts") ||
+        !hipchk(hipMemcpyAsync(S.l_off, S.l_cnt, kk * 8, hipMemcpyDeviceToDevice, k->stream), "offsets") ||
+        !hipchk(hipMemcpyAsync(S.e_off, S.e_cnt, kk * 8, hipMemcpyDeviceToDevice, k->stream), "offsets") ||
+        !hipchk(launch_exclusive_scan_u64(S.l_off, kk, k->scan_scratch, &k->totals[0], k->stream), "scan") ||
+        !hipchk(launch_exclusive_scan_u64(S.e_off, kk, k->scan_scratch, &k->totals[1], k->stream), "scan"))
+        return false;
+    unsigned long long tot[2] = {0, 0};
+    if (!hipchk(hipMemcpyAsync(tot, k->totals, sizeof tot, hipMemcpyDeviceToHost, k->stream), "totals") ||
+        !hipchk(hipStreamSynchronize(k->stream), "totals"))
+        return false;
+    if (tot[0] > S.l_cap && !hipchk(grow_async(S.layers, S.l_cap, tot[0], k->stream), "alloc layers")) return false;
+    if (tot[1] > S.e_cap) {
+        size_t c1 = S.e_cap, c2 = S.e_cap, c3 = S.e_cap;
+        if (!hipchk(grow_async(S.meta, c1, tot[1], k->stream), "alloc edges") ||
+            !hipchk(grow_async(S.w_lo, c2, tot[1], k->stream), "alloc edges") ||
+            !hipchk(grow_async(S.w_hi, c3, tot[1], k->stream), "alloc edges"))
+            return false;
+        S.e_cap = std::min(c1, std::min(c2, c3));
+    }
+    out = pvac_ct_batch{};
+    out.n = kk;
+    out.l_off = S.l_off;
+    out.l_cnt = S.l_cnt;
+    out.layers = S.layers;
+    out.e_off = S.e_off;
+    out.e_cnt = S.e_cnt;
+    out.meta = S.meta;
+    out.w_lo = S.w_lo;
+    out.w_hi = S.w_hi;
+    return hipchk(launch_stage_rows(src, out, k->stream), "rows");
+}
+
+// the final step's sigmas (PVAC_MUL_WITH_SIGMA): salts from salts_at (or splitmix), then sigma_from_H
+// per edge over the finished hash-order output; a pair the exec put in the canonical order
+// (guard_budget / ORDER_CANONICAL) makes the step run once more with the salts mapped (exec's salt
+// positions), as pvac_hip_ct_mul_exec does for a batch
+bool chain_final_sigma(pvac_hip_ctx* k, chain_shared* sh, uint32_t d, uint64_t c0, pvac_hip_plan& plan,
+                       const pvac_ct_batch& A, const pvac_ct_batch& Xv, pvac_ct_batch& C, chain_set& S,
+                       uint32_t mflags) {
+    const pvac_chain_opts& o = *sh->o;
+    auto hipchk = [&](hipError_t e, const char* where) {
+        if (e == hipSuccess) return true;
+        sh->failed(e == hipErrorOutOfMemory ? PVAC_ENOMEM : PVAC_EDEVICE,
+                   std::string("ct_mul_chain: sigma ") + where + ": " + hipGetErrorString(e));
+        return false;
+    };
+    const uint64_t slots = std::max<uint64_t>(plan.total_edge_slots, 1);
+    const uint32_t sw = k->prm.m_bits / 64;
+    if (slots > S.s_cap) {
+        if (S.sigma) hipFreeAsync(S.sigma, k->stream);
+        S.sigma = nullptr;
+        S.s_cap = 0;
+        if (!hipchk(hipMallocAsync((void**)&S.sigma, slots * sw * 8, k->stream), "alloc (1 KiB per edge: a smaller chunk?)"))
+            return false;
+        S.s_cap = slots;
+    }
+    if (!hipchk(grow_async(k->chain_salts, k->chain_salt_cap, slots, k->stream), "alloc salts")) return false;
+    if (o.salts_at) {
+        if (o.salts_at(o.user, d, c0, &A, &Xv, &C, k->chain_salts, plan.total_edge_slots, (void*)k->stream) != 0) {
+            sh->failed(PVAC_EINVAL, "ct_mul_chain: salts_at callback failed");
+            return false;
+        }
+    } else if (!hipchk(launch_fill_random(o.nonce_seed ^ 0x5A175A175A175A17ull ^ (97ull * c0 + d), k->chain_salts, slots,
+                                          k->stream),
+                       "fill salts")) {
+        return false;
+    }
+    C.sigma = S.sigma;
+    C.sigma_words = sw;
+    bool hash_order = (mflags & PVAC_MUL_ORDER_CANONICAL) == 0;
+    if (hash_order) {
+        std::vector<uint32_t> stv(C.n);
+        if (!hipchk(hipMemcpyAsync(stv.data(), k->pair_status, C.n * 4, hipMemcpyDeviceToHost, k->stream), "status") ||
+            !hipchk(hipStreamSynchronize(k->stream), "status"))
+            return false;
+        for (uint32_t v : stv) hash_order &= v != 1u;
+    }
+    if (hash_order) return hipchk(launch_sigma(k->H, k->prm, C, k->chain_salts, nullptr, k->num_cus, k->stream), "launch");
+    if (pvac_hip_ct_mul_exec(k, &plan, &A, &Xv, k->chain_nonces, k->chain_salts, &C, mflags | PVAC_MUL_WITH_SIGMA)) {
+        sh->failed(PVAC_EDEVICE, "ct_mul_chain: sigma exec: " + k->err);
+        return false;
+    }
+    return true;
+}
+
+// one worker: chunks of its device range in input order from the range's counter, depth steps of
+// plan + exec each on this context's stream, the final c_depth to the digests / on_chunk
+void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage, chain_wstats* ws) {
     if (hipSetDevice(k->device) != hipSuccess) {
         sh->failed(PVAC_EDEVICE, "ct_mul_chain: hipSetDevice");
         return;
@@ -1582,6 +1714,8 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
     const pvac_ct_batch& X = *sh->X;
     const uint32_t mflags = o.flags & PVAC_MUL_ORDER_CANONICAL;
     const bool check = (o.flags & PVAC_CHAIN_CHECK_GSUM) != 0;
+    const bool sigma = (o.flags & PVAC_MUL_WITH_SIGMA) != 0;
+    const bool remote = k->device != sh->x_dev;
     auto hipchk = [&](hipError_t e, const char* where) {
         if (e == hipSuccess) return true;
         sh->failed(e == hipErrorOutOfMemory ? PVAC_ENOMEM : PVAC_EDEVICE,
@@ -1595,10 +1729,11 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
     };
     for (;;) {
         if (sh->stop.load()) return;
-        const uint64_t c0 = sh->next.fetch_add(1) * sh->chunk;
-        if (c0 >= X.n) return;
-        const uint64_t kk = std::min<uint64_t>(sh->chunk, X.n - c0);
-        const pvac_ct_batch Xv = chain_view(X, c0, kk);
+        const uint64_t c0 = rg->next.fetch_add(sh->chunk);
+        if (c0 >= rg->end) return;
+        const uint64_t kk = std::min<uint64_t>(sh->chunk, rg->end - c0);
+        pvac_ct_batch Xv = chain_view(X, c0, kk);
+        if ((stage || remote) && !stage_chunk(k, sh, chain_view(X, c0, kk), Xv)) return;
         pvac_ct_batch A = Xv;
         int cur = 0;
         for (uint32_t d = 0; d < o.depth; ++d) {
@@ -1638,7 +1773,12 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
             C.meta = S.meta;
             C.w_lo = S.w_lo;
             C.w_hi = S.w_hi;
-            if (o.fill_nonces) {
+            if (o.nonces_at) {
+                if (o.nonces_at(o.user, d, c0, &A, &Xv, &C, k->chain_nonces, nw, (void*)k->stream) != 0) {
+                    sh->failed(PVAC_EINVAL, "ct_mul_chain: nonces_at callback failed");
+                    return;
+                }
+            } else if (o.fill_nonces) {
                 if (o.fill_nonces(o.user, d, c0, nw, k->chain_nonces, (void*)k->stream) != 0) {
                     sh->failed(PVAC_EINVAL, "ct_mul_chain: fill_nonces callback failed");
                     return;
@@ -1656,19 +1796,34 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
                 ws->gsum_pairs += kk;
                 ws->gsum_failed += bad;
             }
+            if (o.after_step && o.after_step(o.user, d, c0, &A, &Xv, &C, nullptr, 0, (void*)k->stream) != 0) {
+                sh->failed(PVAC_EINVAL, "ct_mul_chain: after_step callback failed");
+                return;
+            }
+            if (sigma && d + 1 == o.depth && !chain_final_sigma(k, sh, d, c0, plan, A, Xv, C, S, mflags)) return;
             A = C;
             cur ^= 1;
         }
-        if (o.digest_n > c0 && o.digest_out) {
+        // digests / counts land in the caller's arrays on X's device (through the worker's own
+        // buffer and a peer copy when this worker runs on another device)
+        auto out_words = [&](uint64_t n_out, uint64_t* dst, int kind) {   // 0 counts, 1 FNV, 2 sum digests
+            if (n_out <= c0 || !dst) return true;
+            const uint64_t m = std::min<uint64_t>(kk, n_out - c0);
             pvac_ct_batch H = A;
-            H.n = std::min<uint64_t>(kk, o.digest_n - c0);
-            if (!hipchk(launch_batch_digest(H, o.digest_out + c0, k->stream), "digest")) return;
-        }
-        if (o.count_n > c0 && o.count_out) {
-            const uint64_t m = std::min<uint64_t>(kk, o.count_n - c0);
-            if (!hipchk(hipMemcpyAsync(o.count_out + c0, A.e_cnt, m * 8, hipMemcpyDeviceToDevice, k->stream), "counts"))
-                return;
-        }
+            H.n = m;
+            auto put = [&](uint64_t* to) {
+                if (kind == 1) return hipchk(launch_batch_digest(H, to, k->stream), "digest");
+                if (kind == 2) return hipchk(launch_batch_sumdigest(H, to, k->stream), "sum digest");
+                return hipchk(hipMemcpyAsync(to, A.e_cnt, m * 8, hipMemcpyDeviceToDevice, k->stream), "counts");
+            };
+            if (!remote) return put(dst + c0);
+            if (!hipchk(grow_async(k->chain_out, k->chain_out_cap, m, k->stream), "alloc outputs") || !put(k->chain_out))
+                return false;
+            return hipchk(hipMemcpyPeerAsync(dst + c0, sh->x_dev, k->chain_out, k->device, m * 8, k->stream), "peer copy");
+        };
+        if (!out_words(o.digest_n, o.digest_out, 1) || !out_words(o.count_n, o.count_out, 0) ||
+            !out_words(o.count_n, o.sumdigest_out, 2))
+            return;
         if (o.on_chunk && o.on_chunk(o.user, c0, &A, (void*)k->stream) != 0) {
             sh->failed(PVAC_EINVAL, "ct_mul_chain: on_chunk callback failed");
             return;
@@ -1681,64 +1836,143 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_wstats* ws) {
 
 extern "C" {
 
+int pvac_hip_memcpy(void* dst, const void* src, size_t bytes, void* stream) {
+    if (!bytes) return PVAC_OK;
+    if (!dst || !src) return PVAC_EINVAL;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return e == hipSuccess ? PVAC_OK : PVAC_EDEVICE;
+}
+
+int pvac_hip_chain_partition(uint64_t n, uint64_t chunk, uint32_t parts, uint64_t* first) {
+    if (!first || parts == 0 || parts > PVAC_CHAIN_MAX_DEVICES) return PVAC_EINVAL;
+    if (!chunk) chunk = 1024;
+    const uint64_t nch = (n + chunk - 1) / chunk;   // whole chunks, dealt as evenly as possible
+    for (uint32_t j = 0; j <= parts; ++j) first[j] = std::min<uint64_t>(n, (nch * j / parts) * chunk);
+    return PVAC_OK;
+}
+
 int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_chain_opts* o, pvac_chain_stats* st) {
     if (!c || !o || !st || !batch_ok(X)) return fail(c, PVAC_EINVAL, "ct_mul_chain: bad arguments");
     if (o->depth < 1 || o->depth > PVAC_CHAIN_MAX_DEPTH) return fail(c, PVAC_EINVAL, "ct_mul_chain: depth");
-    if (o->flags & ~(PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM))
-        return fail(c, PVAC_EINVAL, "ct_mul_chain: flags (WITH_SIGMA is not supported on chains)");
+    if (o->flags & ~(PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM | PVAC_MUL_WITH_SIGMA | PVAC_CHAIN_STAGE_INPUTS))
+        return fail(c, PVAC_EINVAL, "ct_mul_chain: flags");
     if ((o->flags & PVAC_CHAIN_CHECK_GSUM) && !c->powg)
         return fail(c, PVAC_EINVAL, "ct_mul_chain: CHECK_GSUM needs pvac_hip_ctx_set_powg");
+    if ((o->flags & PVAC_MUL_WITH_SIGMA) && !c->H.ready)
+        return fail(c, PVAC_EINVAL, "ct_mul_chain: WITH_SIGMA needs H (pvac_hip_ctx_set_H / gen_H)");
+    if (o->n_devices > PVAC_CHAIN_MAX_DEVICES || (o->n_devices && !o->devices))
+        return fail(c, PVAC_EINVAL, "ct_mul_chain: devices");
     if (X->n && (!X->layers || !X->meta || !X->w_lo || !X->w_hi)) return fail(c, PVAC_EINVAL, "ct_mul_chain: input arrays");
     std::memset(st, 0, sizeof *st);
     const auto t0 = std::chrono::steady_clock::now();
     if (!X->n) return PVAC_OK;
     const uint32_t S = o->streams ? std::min<uint32_t>(o->streams, 64) : 4u;
     const uint64_t chunk = o->chunk ? o->chunk : 1024;
+    const uint32_t D = o->n_devices ? o->n_devices : 1u;
+    std::vector<int> devs(D, c->device);
+    for (uint32_t j = 0; j < o->n_devices; ++j) devs[j] = o->devices[j];
     // inputs already enqueued on the caller's stream must be complete before other streams read them
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain (caller stream)");
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
-    // each worker's general-path scratch: its share of half the HBM free now (the other half holds
-    // the workers' ping-pong outputs and the caller's data)
-    const uint64_t cap_words = std::max<uint64_t>((uint64_t)(free_b / 2) / S / 4, 1ull << 24);
-    while (c->chain_kids.size() < S) {
-        pvac_hip_ctx* k = nullptr;
-        const int rc = pvac_hip_ctx_create(c->device, &c->prm, &k);
-        if (rc) return fail(c, rc, "ct_mul_chain: worker context");
-        c->chain_kids.push_back(k);
-        e = hipMalloc(&k->chain_stats, 2 * PVAC_CHAIN_MAX_DEPTH * sizeof(unsigned long long));
-        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain: worker statistics");
+    // worker contexts: [range j * S + w] on devs[j]; a layout change rebuilds the ones that differ
+    if (c->chain_kids.size() > (size_t)D * S) {
+        for (size_t w = (size_t)D * S; w < c->chain_kids.size(); ++w) pvac_hip_ctx_destroy(c->chain_kids[w]);
+        c->chain_kids.resize((size_t)D * S);
     }
-    for (uint32_t w = 0; w < S; ++w) {
-        pvac_hip_ctx* k = c->chain_kids[w];
-        k->arena_cap_words = cap_words;
-        k->prm = c->prm;
-        if (c->powg && (k->powg_n != c->powg_n || !k->powg)) {
-            hipFree(k->powg);
-            k->powg = nullptr;
-            e = hipMalloc(&k->powg, (size_t)c->powg_n * 16);
-            if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain: worker powg");
-            k->powg_n = c->powg_n;
+    for (uint32_t j = 0; j < D; ++j) {
+        // each worker's general-path scratch: its share of half the HBM free now on its device (the
+        // other half holds the workers' ping-pong outputs and the caller's data)
+        size_t free_b = 0, total_b = 0;
+        if (hipSetDevice(devs[j]) != hipSuccess) {
+            hipSetDevice(c->device);
+            return fail(c, PVAC_EDEVICE, "ct_mul_chain: device " + std::to_string(devs[j]));
         }
-        if (c->powg) e = hipMemcpy(k->powg, c->powg, (size_t)c->powg_n * 16, hipMemcpyDeviceToDevice);
-        if (e == hipSuccess) e = hipMemsetAsync(k->chain_stats, 0, 2 * PVAC_CHAIN_MAX_DEPTH * 8, k->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(k->stream);
-        if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain: worker setup");
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 8ull << 30;
+        const uint32_t same = (uint32_t)std::count(devs.begin(), devs.end(), devs[j]);
+        const uint64_t cap_words = std::max<uint64_t>((uint64_t)(free_b / 2) / ((uint64_t)S * same) / 4, 1ull << 24);
+        if (devs[j] != c->device) {   // peer reads of X / peer writes of the outputs
+            const hipError_t pe = hipDeviceEnablePeerAccess(c->device, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+                hipSetDevice(c->device);
+                return hip_fail(c, pe, "ct_mul_chain: peer access");
+            }
+            (void)hipGetLastError();
+        }
+        for (uint32_t w = 0; w < S; ++w) {
+            const size_t slot = (size_t)j * S + w;
+            if (slot < c->chain_kids.size() && c->chain_kids[slot]->device != devs[j]) {
+                pvac_hip_ctx_destroy(c->chain_kids[slot]);
+                c->chain_kids[slot] = nullptr;
+            }
+            if (slot >= c->chain_kids.size()) c->chain_kids.push_back(nullptr);
+            pvac_hip_ctx*& k = c->chain_kids[slot];
+            if (!k) {
+                const int rc = pvac_hip_ctx_create(devs[j], &c->prm, &k);
+                if (rc) {
+                    hipSetDevice(c->device);
+                    return fail(c, rc, "ct_mul_chain: worker context");
+                }
+                e = hipMalloc(&k->chain_stats, 2 * PVAC_CHAIN_MAX_DEPTH * sizeof(unsigned long long));
+                if (e != hipSuccess) {
+                    hipSetDevice(c->device);
+                    return hip_fail(c, e, "ct_mul_chain: worker statistics");
+                }
+            }
+            k->arena_cap_words = cap_words;
+            k->prm = c->prm;
+            if (c->powg && (k->powg_n != c->powg_n || !k->powg)) {
+                hipFree(k->powg);
+                k->powg = nullptr;
+                e = hipMalloc(&k->powg, (size_t)c->powg_n * 16);
+                if (e != hipSuccess) {
+                    hipSetDevice(c->device);
+                    return hip_fail(c, e, "ct_mul_chain: worker powg");
+                }
+                k->powg_n = c->powg_n;
+            }
+            e = hipSuccess;
+            if (c->powg) e = hipMemcpyPeer(k->powg, k->device, c->powg, c->device, (size_t)c->powg_n * 16);
+            if (e == hipSuccess && (o->flags & PVAC_MUL_WITH_SIGMA) && (!k->H.ready || k->H_from != c->H_gen)) {
+                e = sigma_tables_clone(k->H, c->H, k->device, c->device, k->stream);
+                k->H_from = c->H_gen;
+            }
+            if (e == hipSuccess) e = hipMemsetAsync(k->chain_stats, 0, 2 * PVAC_CHAIN_MAX_DEPTH * 8, k->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(k->stream);
+            if (e != hipSuccess) {
+                hipSetDevice(c->device);
+                return hip_fail(c, e, "ct_mul_chain: worker setup");
+            }
+        }
+    }
+    hipSetDevice(c->device);
+    std::vector<uint64_t> first(D + 1);
+    pvac_hip_chain_partition(X->n, chunk, D, first.data());
+    std::vector<chain_range> ranges(D);
+    for (uint32_t j = 0; j < D; ++j) {
+        ranges[j].next.store(first[j]);
+        ranges[j].end = first[j + 1];
     }
     chain_shared sh;
     sh.X = X;
     sh.o = o;
     sh.chunk = chunk;
-    std::vector<chain_wstats> ws(S);
-    std::vector<uint64_t> redo0(S);
-    for (uint32_t w = 0; w < S; ++w) redo0[w] = c->chain_kids[w]->redo_total;
+    sh.x_dev = c->device;
+    sh.ranges = ranges.data();
+    const size_t nk = (size_t)D * S;
+    std::vector<chain_wstats> ws(nk);
+    std::vector<uint64_t> redo0(nk);
+    for (size_t w = 0; w < nk; ++w) redo0[w] = c->chain_kids[w]->redo_total;
     std::vector<std::thread> th;
-    th.reserve(S);
-    for (uint32_t w = 0; w < S; ++w) th.emplace_back(chain_worker, c->chain_kids[w], &sh, &ws[w]);
+    th.reserve(nk);
+    for (uint32_t j = 0; j < D; ++j)
+        for (uint32_t w = 0; w < S; ++w)
+            th.emplace_back(chain_worker, c->chain_kids[(size_t)j * S + w], &sh, &ranges[j],
+                            j > 0 && (o->flags & PVAC_CHAIN_STAGE_INPUTS) != 0, &ws[(size_t)j * S + w]);
     for (std::thread& t : th) t.join();
-    for (uint32_t w = 0; w < S; ++w) {
+    for (size_t w = 0; w < nk; ++w) {
         pvac_hip_ctx* k = c->chain_kids[w];
+        hipSetDevice(k->device);
         e = hipStreamSynchronize(k->stream);
         if (e != hipSuccess && sh.rc == PVAC_OK) sh.failed(PVAC_EDEVICE, std::string("ct_mul_chain: ") + hipGetErrorString(e));
         unsigned long long v[2 * PVAC_CHAIN_MAX_DEPTH];
@@ -1752,6 +1986,7 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
         st->chunks += ws[w].chunks;
         st->redo += k->redo_total - redo0[w];
     }
+    hipSetDevice(c->device);
     st->pair_steps = X->n * o->depth;
     st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (sh.rc != PVAC_OK) return fail(c, sh.rc, sh.err);
@@ -1759,3 +1994,4 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
 }
 
 }  // extern "C"
+

@@ -24,6 +24,8 @@ struct sigma_tables {
 };
 
 void sigma_tables_free(sigma_tables& T);
+// device copy of src for a context on dst_dev (peer copies when the devices differ); synchronous
+hipError_t sigma_tables_clone(sigma_tables& dst, const sigma_tables& src, int dst_dev, int src_dev, hipStream_t st);
 // host SHA-256 over a contiguous buffer
 void sha256_host(const uint8_t* p, size_t n, uint8_t out[32]);
 // from a HOST dense H (n_bits columns x ceil(m_bits/64) words); synchronous

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -192,6 +193,59 @@ struct replay {
         return s[k++];
     }
 };
+
+// FIPS 180-4 SHA-256 (test side only: per-edge sigma digests of the fixtures, first 8 bytes LE of the
+// hash of the sigma words as little-endian bytes, as the harness's sigma_digests writes them)
+static uint64_t sigma_digest(const std::vector<uint64_t>& words) {
+    static const uint32_t K[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
+        0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+        0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8,
+        0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+        0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819,
+        0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+        0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+        0xc67178f2};
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    std::vector<uint8_t> m(words.size() * 8);
+    for (size_t i = 0; i < words.size(); ++i)
+        for (int b = 0; b < 8; ++b) m[8 * i + b] = (uint8_t)(words[i] >> (8 * b));
+    const uint64_t bits = (uint64_t)m.size() * 8;
+    m.push_back(0x80);
+    while (m.size() % 64 != 56) m.push_back(0);
+    for (int b = 7; b >= 0; --b) m.push_back((uint8_t)(bits >> (8 * b)));
+    auto rotr = [](uint32_t x, int r) { return (x >> r) | (x << (32 - r)); };
+    for (size_t o = 0; o < m.size(); o += 64) {
+        uint32_t w[64];
+        for (int t = 0; t < 16; ++t)
+            w[t] = (uint32_t)m[o + 4 * t] << 24 | (uint32_t)m[o + 4 * t + 1] << 16 | (uint32_t)m[o + 4 * t + 2] << 8 |
+                   m[o + 4 * t + 3];
+        for (int t = 16; t < 64; ++t)
+            w[t] = (rotr(w[t - 2], 17) ^ rotr(w[t - 2], 19) ^ (w[t - 2] >> 10)) + w[t - 7] +
+                   (rotr(w[t - 15], 7) ^ rotr(w[t - 15], 18) ^ (w[t - 15] >> 3)) + w[t - 16];
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+        for (int t = 0; t < 64; ++t) {
+            const uint32_t t1 = hh + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K[t] + w[t];
+            const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+    }
+    uint64_t r = 0;   // digest bytes 0..7, read little-endian
+    for (int b = 0; b < 8; ++b) r |= (uint64_t)(uint8_t)(h[b / 4] >> (24 - 8 * (b % 4))) << (8 * b);
+    return r;
+}
+
+// a seeded splitmix64 word source (reproducible randomness for the multi-device comparisons)
+static pvac_hip::RandomSource os_splitmix(uint64_t seed) {
+    auto st = std::make_shared<uint64_t>(seed);
+    return [st] {
+        uint64_t z = (*st += 0x9e3779b97f4a7c15ULL);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+        return z ^ (z >> 31);
+    };
+}
 
 // replays an enc_value getrandom log; the adapter draws a whole stride per value, so reads
 // past the log return 0 (they are never consumed by the kernels) and are counted
@@ -416,6 +470,56 @@ int main(int argc, char** argv) {
             for (size_t l = 0; l < full.size(); ++l) MUST(c.L[l].seed.ztag == full[l].seed.ztag, "ztag %zu", l);
             cur = c;
         }
+    }
+
+    // the chain entry point (pvac_hip_ct_mul_chain) with a final-step WITH_SIGMA, replaying the
+    // reference's stream of c_k = ct_mul(c_{k-1}, x), k = 1..4 (harness cmd_chainx): every step's
+    // nonces placed, the intermediate salts skipped, the final salts placed; c_4 byte-identical
+    // (weights-only .ct, full layer table) and every sigma's digest equal to the reference's
+    {
+        const Cipher x = read_ct(ref + "/chainx_x.ct")[0];
+        const auto stream = read_u64(ref + "/chainx_stream.u64");
+        auto rp = std::make_shared<replay>(replay{stream});
+        std::vector<pvac_hip::RandomSource> rnds{[rp] { return (*rp)(); }};
+        const Cipher c = pvac_hip::ct_mul_chain(pk, std::vector<Cipher>{x}, 4, true, rnds)[0];
+        MUST(rp->k == stream.size(), "chain consumed %zu of %zu random words", rp->k, stream.size());
+        Cipher w = c;
+        for (auto& E : w.E) E.s = mirror::BitVec{};   // the fixture is the weights-only .ct
+        MUST(write_ct({w}) == slurp(ref + "/chainx_final.ct"), "chainx c_4 weights .ct bytes");
+        const auto lay = read_u64(ref + "/chainx_final_layers.u64");
+        MUST(c.L.size() * 6 == lay.size(), "chainx layers %zu", c.L.size());
+        for (size_t l = 0; l < c.L.size(); ++l)
+            MUST((uint64_t)c.L[l].rule == lay[6 * l] && c.L[l].seed.ztag == lay[6 * l + 3] &&
+                     c.L[l].seed.nonce.lo == lay[6 * l + 4] && c.L[l].seed.nonce.hi == lay[6 * l + 5],
+                 "chainx layer %zu", l);
+        const auto dig = read_u64(ref + "/chainx_final_sigdig.u64");
+        MUST(dig.size() == c.E.size(), "chainx sigma digests");
+        for (size_t e = 0; e < c.E.size(); ++e) MUST(sigma_digest(c.E[e].s.w) == dig[e], "chainx sigma %zu", e);
+        // two device ranges on this GPU (devices {0, 0}): the same bytes and sigmas
+        auto rp2 = std::make_shared<replay>(replay{stream});
+        std::vector<Cipher> xs{x, x, x};
+        std::vector<pvac_hip::RandomSource> r3{[rp2] { return (*rp2)(); }, os_splitmix(11), os_splitmix(12)};
+        const auto c3 = pvac_hip::ct_mul_chain(pk, xs, 4, true, r3, std::vector<int>{0, 0});
+        MUST(write_ct({ct_view(c3[0])}) == write_ct({ct_view(c)}) && same_edges(c3[0], c, true), "chain 2-range c_4");
+        MUST(same_edges(c3[1], c3[2], false) && same_edges(c3[1], c, false), "chain 2-range weights");
+    }
+
+    // multi-device batch ct_mul (devices {0, 0}: two ranges, two contexts, one GPU) with sigma from one
+    // seeded source: the bytes of the one-device batch (draw order preserved)
+    {
+        std::vector<Cipher> A, B;
+        for (int p = 0; p < 8; ++p) {
+            A.push_back(read_ct(ref + "/pair" + std::to_string(p) + "_x.ct")[0]);
+            B.push_back(read_ct(ref + "/pair" + std::to_string(p) + "_y.ct")[0]);
+        }
+        const auto one = pvac_hip::ct_mul_batch(pk, A, B, true, os_splitmix(7), std::vector<int>{});
+        const auto two = pvac_hip::ct_mul_batch(pk, A, B, true, os_splitmix(7), std::vector<int>{0, 0});
+        const auto three = pvac_hip::ct_mul_batch(pk, A, B, true, os_splitmix(7), std::vector<int>{0, 0, 0});
+        MUST(one.size() == 8 && two.size() == 8 && three.size() == 8, "multi-device batch sizes");
+        for (int p = 0; p < 8; ++p)
+            MUST(write_ct({ct_view(one[p])}) == write_ct({ct_view(two[p])}) && same_edges(one[p], two[p], true) &&
+                     same_edges(one[p], three[p], true),
+                 "multi-device batch pair %d", p);
     }
 
     // fp_binop through the adapter on the golden vectors (core/field.hpp:50-213)

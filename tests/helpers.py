@@ -423,31 +423,30 @@ def pack_device_batch(X, k):
             cs(u(X.w_hi[ei])))
 
 
-_HIP = None
+def _lib():
+    """libpvac_hip.so (already loaded by the engine); its pvac_hip_memcpy does the hook-side copies
+    (a second HIP runtime loaded by ctypes would clash with torch's)."""
+    from pvac_hfhe_cppbyv_amd import load_library
+    global _LIB
+    if "_LIB" not in globals() or _LIB is None:
+        _LIB = load_library()
+    return _LIB
 
 
-def _hip():
-    global _HIP
-    if _HIP is None:
-        _HIP = C.CDLL("/opt/rocm/lib/libamdhip64.so")
-        _HIP.hipStreamSynchronize.argtypes = [C.c_void_p]
-        _HIP.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    return _HIP
+def _copy(dst, src, nbytes, stream):
+    assert _lib().pvac_hip_memcpy(C.c_void_p(dst), C.c_void_p(src), nbytes, C.c_void_p(stream)) == 0
 
 
 def hip_batch_to_host(b, stream, sigma_words=0):
-    """Copy a device pvac_ct_batch (a CtBatch struct handed to a chain's on_chunk callback, whose
-    arrays live only during the callback) to host ciphers: synchronises `stream`, then plain
-    hipMemcpy device-to-host of the counts/offsets and each cipher's rows. Test helper."""
-    hip = _hip()
-    assert hip.hipStreamSynchronize(C.c_void_p(stream)) == 0
+    """Copy a device pvac_ct_batch (a CtBatch struct handed to a chain hook / on_chunk callback,
+    whose arrays live only during the callback) to host ciphers: counts/offsets, then each cipher's
+    rows, through pvac_hip_memcpy on the callback's stream. Test helper."""
     n = int(b.n)
 
     def d2h(ptr, count, dtype, off=0, width=1):
         out = np.zeros(count * width, dtype)
         if count:
-            assert hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr + off * width * out.itemsize),
-                                 out.nbytes, 2) == 0   # hipMemcpyDeviceToHost
+            _copy(out.ctypes.data, ptr + off * width * out.itemsize, out.nbytes, stream)
         return out
 
     lo, lc = d2h(b.l_off, n, np.uint64), d2h(b.l_cnt, n, np.uint64)
@@ -461,3 +460,30 @@ def hip_batch_to_host(b, stream, sigma_words=0):
             sg = d2h(b.sigma, int(ec[i]), np.uint64, int(eo[i]), sigma_words).reshape(-1, sigma_words)
         out.append(Cipher(L, *args, sg))
     return out
+
+
+def hip_h2d(dev_ptr, arr, stream=None):
+    """Host numpy array -> device pointer (pvac_hip_memcpy on `stream`). Test helper."""
+    a = np.ascontiguousarray(arr)
+    if a.nbytes:
+        _copy(dev_ptr, a.ctypes.data, a.nbytes, stream or 0)
+
+
+def hip_d2h_u64(dev_ptr, n, stream=None):
+    out = np.zeros(n, np.uint64)
+    if n:
+        _copy(out.ctypes.data, dev_ptr, out.nbytes, stream or 0)
+    return out
+
+
+def sumdigest(c):
+    """pvac_hip_batch_sumdigest restated in numpy (uint64 wrap-around): |E| + sum over edges e of
+    m(m(m(e * golden ^ meta) ^ w_lo) ^ w_hi), m = the splitmix64 finaliser."""
+    def m(z):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
+    with np.errstate(over="ignore"):
+        e = np.arange(c.nE, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        v = m(m(m(e ^ c.meta) ^ c.w_lo) ^ c.w_hi)
+        return int((v.sum(dtype=np.uint64) + np.uint64(c.nE)) & np.uint64(2**64 - 1))

@@ -616,3 +616,19 @@ def test_ct_mul_api_errors_leave_context_usable(oracle):
         base = int(loff[p]) + x.nL + y.nL
         ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0x55)
         _assert_same(out[p], ref, layers_view=False)
+
+
+def test_sumdigest_matches_numpy_restatement():
+    """pvac_hip_batch_sumdigest (the parallel position-keyed digest the chain's timed pass uses) equals
+    its numpy restatement on ragged ciphers (0, 1, 255, 256, 257 and thousands of edges)."""
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine, HostCipher
+    from helpers import LAYER_DT, sumdigest
+    eng = Engine(device=0)
+    rng = np.random.default_rng(0x5D16)
+    cs = []
+    for ne in (0, 1, 255, 256, 257, 4099):
+        L = np.zeros(2, LAYER_DT)
+        cs.append(HostCipher(L, rng.integers(0, 2**63, ne, dtype=np.uint64), rng.integers(0, 2**64, ne, dtype=np.uint64),
+                             rng.integers(0, 2**64, ne, dtype=np.uint64)))
+    got = eng.sumdigest(DeviceBatch.from_host(cs, eng.device)).cpu().numpy().view(np.uint64)
+    assert [int(g) for g in got] == [sumdigest(c) for c in cs]

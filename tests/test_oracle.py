@@ -289,3 +289,43 @@ def test_add_batch_timed_equals_ct_add(oracle):
                                           P_(cnt), P_(dig))
         assert [int(v) for v in cnt] == [r.nE for r in refs]
         assert [int(v) for v in dig] == [_fnv(r) for r in refs]
+
+
+def test_chainx_fixture_replay(oracle, manifest, H_dense):
+    """The chain entry point's fixture (ref_harness chainx): x = enc_value(2), c_k = ct_mul(c_{k-1}, x),
+    k = 1..4, one getrandom stream. The oracle replays it step by step (each step's nonces, then its
+    salts: skipped for steps 1..3, used for step 4's sigmas), reproducing every step's edge / layer /
+    stream counts, c_4's weights-only .ct bytes, its full layer table, every sigma digest, and its
+    decryption (x^5 = 32)."""
+    import hashlib
+    import json
+    with open(os.path.join(REF, "chainx_manifest.json")) as f:
+        man = json.load(f)
+    x = read_ct(os.path.join(REF, "chainx_x.ct"))[0]
+    xw = Cipher(x.layers, x.meta, x.w_lo, x.w_hi)
+    stream = read_u64("chainx_stream.u64")
+    pos, c = 0, xw
+    depth = man["depth"]
+    for k in range(depth):
+        nn = 2 * c.nL * x.nL
+        nz = stream[pos:pos + nn]
+        w = oracle.ct_mul(c, xw, nz, canon_tag=man["canon_tag"])   # weights: the salt count
+        rec = man["steps"][k]
+        assert w.nE == rec["edges"] and w.nL == rec["layers"] and nn + w.nE == rec["stream"]
+        if k + 1 == depth:
+            c = oracle.ct_mul(c, xw, nz, salts=stream[pos + nn:pos + nn + w.nE], H=H_dense, canon_tag=man["canon_tag"])
+        else:
+            c = w
+        pos += nn + w.nE
+    assert pos == len(stream) == man["stream"]
+    with open(os.path.join(REF, "chainx_final.ct"), "rb") as f:
+        assert write_ct([Cipher(c.layers, c.meta, c.w_lo, c.w_hi)]) == f.read()
+    full = read_layers_u64("chainx_final_layers.u64")
+    for fld in ("rule", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(c.layers[fld], full[fld])
+    dig = read_u64("chainx_final_sigdig.u64")
+    got = np.array([int.from_bytes(hashlib.sha256(s.astype("<u8").tobytes()).digest()[:8], "little")
+                    for s in c.sigma], np.uint64)
+    assert np.array_equal(got, dig)
+    R = R_for(c, [(x, read_u64("chainx_x_R.u64"))])
+    assert list(oracle.dec(c, read_u64("powg_B.u64"), R)) == man["dec"] == [32, 0]
