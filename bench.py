@@ -469,6 +469,18 @@ def self_checks(eng, args, A, B, out, nonces, n, first, seed, world, rank):
             del Aw, Bw, Cw, ow, nw
         res["shard_windows"] = {"pairs_per_rank": K, "ranks": world, "recomputed_on": "rank 0", "match": match}
         res["shard_digests_ok"] = bool(match and failed == 0)
+    # the optional result concat (shard.gather_batch: RCCL all_gather of compacted shards) on each
+    # rank's last 8 pairs: the gathered ciphers' digests equal the window digests every rank sent
+    from pvac_hfhe_cppbyv_amd import DeviceBatch
+    from pvac_hfhe_cppbyv_amd.shard import gather_batch
+    k8 = min(8, K)
+    tail = DeviceBatch(k8, out.l_off[n - k8:n], out.l_cnt[n - k8:n], out.layers, out.e_off[n - k8:n],
+                       out.e_cnt[n - k8:n], out.meta, out.w_lo, out.w_hi)
+    G = gather_batch(tail)
+    gd = eng.digest(G).cpu().numpy().view(np.uint64)
+    want = np.concatenate([w[len(w) - k8:] for w in wins])
+    res["result_gather"] = {"pairs_per_rank": k8, "ranks": world, "ciphers": int(G.n),
+                            "match": bool(G.n == k8 * world and np.array_equal(gd, want))}
     return res
 
 

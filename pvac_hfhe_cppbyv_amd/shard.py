@@ -103,3 +103,71 @@ def all_gather_u64(values, device=None):
     dist.all_gather_into_tensor(allt, mine)
     a = allt.cpu().numpy().view(np.uint64)
     return [a[r * len(v):(r + 1) * len(v)].copy() for r in range(world)]
+
+
+def compact_rows(X, n=None):
+    """The used rows of a (capacity-padded) DeviceBatch as flat int64 tensors on its device:
+    (l_cnt, e_cnt, layers [sum l_cnt, 5], meta, w_lo, w_hi, sigma or None), ciphers in order."""
+    import torch
+    n = X.n if n is None else n
+
+    def rows(off, cnt):
+        cnt = cnt[:n].to(torch.int64)
+        start = torch.repeat_interleave(off[:n].to(torch.int64) - (torch.cumsum(cnt, 0) - cnt), cnt)
+        return start + torch.arange(start.numel(), device=start.device)
+
+    li, ei = rows(X.l_off, X.l_cnt), rows(X.e_off, X.e_cnt)
+    sig = None if X.sigma is None else X.sigma[ei]
+    return (X.l_cnt[:n].to(torch.int64), X.e_cnt[:n].to(torch.int64), X.layers[li], X.meta[ei], X.w_lo[ei], X.w_hi[ei],
+            sig)
+
+
+def gather_batch(X, n=None, device=None):
+    """Result concat of a sharded run for SMALL batches (BASELINE cfg 5's optional gather over xGMI):
+    every rank's ciphers (compacted, in rank order = global pair order) on every rank, as one
+    DeviceBatch with a compact CSR. Two collectives: an all_gather of the per-rank row counts, then
+    one all_gather_into_tensor of each rank's payload padded to the largest (RCCL on device
+    tensors; gloo on CPU copies). No process group: the compacted X itself. At cfg 5's sizes
+    (~490 GB of output) this is not meant to run: results stay sharded (global_edge_offsets)."""
+    import torch
+    import torch.distributed as dist
+    from . import DeviceBatch
+    lc, ec, lay, meta, wlo, whi, sig = compact_rows(X, n)
+    on = dist.is_available() and dist.is_initialized()
+    dev = lc.device
+    if on and dist.get_backend() == "gloo":
+        dev = torch.device("cpu")
+    elif device is not None:
+        dev = torch.device(device)
+    sw = 0 if sig is None else int(sig.shape[1])
+    parts = [lc, ec, lay.reshape(-1), meta, wlo, whi] + ([sig.reshape(-1)] if sw else [])
+    payload = torch.cat([p.to(dev).reshape(-1) for p in parts])
+    head = torch.tensor([lc.numel(), int(lay.shape[0]), int(meta.numel()), payload.numel()], dtype=torch.int64,
+                        device=dev)
+    if on:
+        world = dist.get_world_size()
+        heads = torch.zeros(world * 4, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(heads, head)
+        heads = heads.reshape(world, 4).cpu().tolist()
+        width = max(h[3] for h in heads)
+        buf = torch.zeros(width, dtype=torch.int64, device=dev)
+        buf[:payload.numel()] = payload
+        allp = torch.zeros(world * width, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allp, buf)
+        chunks = [allp[r * width:r * width + heads[r][3]] for r in range(world)]
+    else:
+        heads, chunks = [head.cpu().tolist()], [payload]
+    fields = [[] for _ in range(7)]
+    for (nc, nl, ne, _), p in zip(heads, chunks):
+        sizes = [nc, nc, 5 * nl, ne, ne, ne] + ([ne * sw] if sw else [])
+        segs = torch.split(p, sizes)
+        for k, t in enumerate(segs):
+            fields[k].append(t)
+    cat = [torch.cat(f) if f else None for f in fields]
+    l_cnt, e_cnt = cat[0], cat[1]
+    l_off = torch.cumsum(l_cnt, 0) - l_cnt
+    e_off = torch.cumsum(e_cnt, 0) - e_cnt
+    out_dev = lc.device if device is None else torch.device(device)
+    mv = lambda t: None if t is None else t.to(out_dev)
+    return DeviceBatch(int(l_cnt.numel()), mv(l_off), mv(l_cnt), mv(cat[2].reshape(-1, 5)), mv(e_off), mv(e_cnt),
+                       mv(cat[3]), mv(cat[4]), mv(cat[5]), mv(cat[6].reshape(-1, sw)) if sw else None)

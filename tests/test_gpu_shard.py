@@ -69,6 +69,7 @@ def test_bench_world2_shard_digests_equal_one_gpu():
     assert two["n_gpus"] == 1 and two["ranks"] == 2 and two["dist"] == {"world_size": 2, "backend": "gloo"}
     assert one["n_gpus"] == 1 and one["ranks"] == 1
     assert c2["shard_digests_ok"] and c2["shard_windows"]["ranks"] == 2
+    assert c2["result_gather"]["match"] and c2["result_gather"]["ciphers"] == 16
     assert c2["gsum_invariant"]["ok"] and c2["gsum_invariant"]["pairs"] == 8192
     assert c1["shard_digests_ok"] and c1["gsum_invariant"]["pairs"] == 8192
     assert c2["global_digest"] == c1["global_digest"]
@@ -89,6 +90,7 @@ def test_bench_rccl_one_rank_collectives():
     c, c0 = rccl["checks"], plain["checks"]
     assert c["collective_backend"] == "nccl" and c0["collective_backend"] is None
     assert c["shard_digests_ok"] and c["gsum_invariant"]["ok"] and c["gsum_invariant"]["pairs"] == 4096
+    assert c["result_gather"]["match"]   # shard.gather_batch over RCCL (one rank)
     assert c["global_digest"] == c0["global_digest"]
     assert c["global_output_edges"] == c0["global_output_edges"]
 

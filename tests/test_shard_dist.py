@@ -76,3 +76,62 @@ def test_gloo_world2_global_offsets():
         assert [h[2] for h in heads] == [2**64 - 1, 2**64 - 2] and [h[1] for h in heads] == [res[0][2], res[1][2]]
         assert combine_digests(h[0] for h in heads) == shard_digest(dig_all, 0)
     assert res[0][1] == 0 and res[1][1] == res[0][2]
+
+
+def _gather_worker(rank, world, port, q):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, HostCipher, LAYER_DT
+    from pvac_hfhe_cppbyv_amd.shard import gather_batch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(100 + rank)
+    cs = []
+    for i in range(3 + rank):   # ragged shards: 3 and 4 ciphers, one of them empty
+        ne = 0 if (rank, i) == (1, 2) else int(rng.integers(1, 60))
+        L = np.zeros(int(rng.integers(1, 5)), LAYER_DT)
+        L["ztag"] = rng.integers(0, 2**63, len(L), dtype=np.uint64)
+        cs.append(HostCipher(L, rng.integers(0, 2**63, ne, dtype=np.uint64), rng.integers(0, 2**63, ne, dtype=np.uint64),
+                             rng.integers(0, 2**63, ne, dtype=np.uint64)))
+    X = DeviceBatch.from_host(cs, "cpu")
+    # capacity padding as engine outputs have it: 3 unused rows after every cipher's rows
+    gap = lambda cnt: torch.cumsum(cnt, 0) - cnt + 3 * torch.arange(X.n, dtype=torch.int64)
+
+    def spread(a, off_old, off_new, cnt, width=None):
+        out = torch.full((int(off_new[-1] + cnt[-1]) + 3,) + tuple(a.shape[1:]), -1, dtype=a.dtype)
+        for i in range(X.n):
+            out[int(off_new[i]):int(off_new[i] + cnt[i])] = a[int(off_old[i]):int(off_old[i] + cnt[i])]
+        return out
+
+    lo2, eo2 = gap(X.l_cnt), gap(X.e_cnt)
+    X = DeviceBatch(X.n, lo2, X.l_cnt, spread(X.layers, X.l_off, lo2, X.l_cnt), eo2, X.e_cnt,
+                    spread(X.meta, X.e_off, eo2, X.e_cnt), spread(X.w_lo, X.e_off, eo2, X.e_cnt),
+                    spread(X.w_hi, X.e_off, eo2, X.e_cnt))
+    G = gather_batch(X)
+    got = G.to_host()
+    q.put((rank, [(c.layers.tobytes(), c.meta.tobytes(), c.w_lo.tobytes(), c.w_hi.tobytes()) for c in got],
+           [(c.layers.tobytes(), c.meta.tobytes(), c.w_lo.tobytes(), c.w_hi.tobytes()) for c in cs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_batch():
+    """shard.gather_batch (the optional result concat of cfg 5) on world size 2 over gloo: every rank
+    receives both shards' ciphers in rank order, byte-identical, ragged shards and an empty cipher."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = res[0][2] + res[1][2]
+    assert len(want) == 7
+    for _, got, _ in res:
+        assert got == want
