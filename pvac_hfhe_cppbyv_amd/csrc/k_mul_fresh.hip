@@ -198,12 +198,19 @@ struct fresh_pref {
     uint32_t rule, pa, pb;
 };
 
+#ifndef PVAC_F3_PF_WAVES   // A/B builds: 0 = every wave prefetches (round 4)
+#define PVAC_F3_PF_WAVES 1
+#endif
 __device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h, uint32_t t = threadIdx.x) {
-    // branch-free and unconditional: every lane loads a valid address (a clamped index, or the
-    // argument block itself when there is no pair / no edge), so the waitcnt pass never has to
-    // drain earlier loads (or the previous pair's output stores) before issuing these; lanes past
-    // the counts ignore what they loaded
+    // every lane of a loading wave loads a valid address (a clamped index, or the argument block
+    // itself when there is no pair / no edge), so the waitcnt pass never has to drain earlier loads
+    // (or the previous pair's output stores) before issuing these; lanes past the counts ignore what
+    // they loaded. Waves past the pair's edges and layers (wave-uniform: 7 of 8 for 40-edge
+    // ciphers) load nothing.
     const bool live = h.pr != kNoPair;
+#if PVAC_F3_PF_WAVES
+    if ((t & ~63u) >= max(max(h.nA, h.nB), h.LA + h.LB)) return fresh_pref{};
+#endif
     using gp64 = const __attribute__((address_space(1))) uint64_t*;   // global: never a flat load
     using gpl = const __attribute__((address_space(1))) uint32_t*;
     const gp64 dummy = (gp64)(uint64_t)g;
