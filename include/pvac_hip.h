@@ -147,7 +147,8 @@ int pvac_hip_alu_ceiling(pvac_hip_ctx* ctx, int kind, double* per_s);
  * 21 v_mul_u32_u24, 22 v_sub_u32, 23 v_max3_u32, 24 v_cmp (VCC) + VOP2 v_cndmask_b32 pairs, 25 v_cndmask_b32_e64
  * reading VCC, 26 VOP2 v_addc_co_u32 (VCC carry), 27 v_addc_co_u32_e64 (SGPR carry), 28 v_cmp_e64 + v_cndmask_b32_e64
  * (SGPR mask) pairs, 29 v_min_u32_e64, 30 v_add_u32_e64, 31 v_and_b32, 32 v_or_b32, 33 v_lshrrev_b32,
- * 34 v_mov_b32, 35 v_max_u32.
+ * 34 v_mov_b32, 35 v_max_u32, 36 v_add_u32_sdwa (byte source), 37 / 38 v_lshlrev_b32_sdwa (byte shifted / byte
+ * shift count), 39 v_xor_b32_e64, 40 v_mad_u32_u24.
  * Measurement only (never used by an op). Synchronous. */
 int pvac_hip_issue_probe(pvac_hip_ctx* ctx, int op, int waves_per_simd, double* per_s, double* clock_hz);
 /* Per-kernel device timing (HIP events on the ctx stream) for the roofline report. */

@@ -500,7 +500,8 @@ class Engine:
                  "v_cndmask_b32_e64", "v_lshl_add_u32", "v_mov_b32_dpp", "v_perm_b32", "v_mul_u32_u24", "v_sub_u32",
                  "v_max3_u32", "v_cmp+v_cndmask_vcc", "v_cndmask_b32_e64_vcc", "v_addc_co_u32_vcc",
                  "v_addc_co_u32_e64_sgpr", "v_cmp_e64+v_cndmask_e64", "v_min_u32_e64", "v_add_u32_e64", "v_and_b32",
-                 "v_or_b32", "v_lshrrev_b32", "v_mov_b32", "v_max_u32")
+                 "v_or_b32", "v_lshrrev_b32", "v_mov_b32", "v_max_u32", "v_add_u32_sdwa", "v_lshlrev_b32_sdwa_src1",
+                 "v_lshlrev_b32_sdwa_src0", "v_xor_b32_e64", "v_mad_u32_u24")
 
     def issue_probe(self, op, waves_per_simd=8):
         """Per-opcode VALU issue rate (pvac_hip_issue_probe): (wave64 inst/s chip-wide, shader clock Hz

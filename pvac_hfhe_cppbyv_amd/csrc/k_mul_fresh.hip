@@ -659,6 +659,14 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
         //      bits of each slot, its bucket's first-insert time t_bkt, its rank in the bucket
         //      (edges of later keys) and the bucket's edge count G[t_bkt]
         uint32_t ordA[KR], ordB[KR];   // t_bkt of slots 0, 1 | t_bkt of slot 2, rank 3 bits x 3, emit 2 bits x 3
+#if PVAC_REP_P2 == 0   // experiment builds: no P2 (no emits, every bucket time "none")
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            ordA[k] = kT16 | (kT16 << 16);
+            ordB[k] = kT16;
+        }
+        if (lane == 0) wave_lp[wave] = 0;
+#endif
         for (int rep_ = 0; rep_ < PVAC_REP_P2; ++rep_) {   // experiment builds only (tools/exp_fresh3.py)
         {
             uint64_t myor = 0;
@@ -891,6 +899,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
 
         M3(5);
         // ---- P5: products into the limb accumulators of their emit positions
+#ifndef PVAC_EXP_SKIP_P5   // experiment builds only: no products (outputs wrong; the phase's cost)
         {
             const uint32_t tid = opaque(threadIdx.x);
             auto accumulate = [&](const ulonglong2& x, const ulonglong2& y, uint32_t p) {
@@ -933,6 +942,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 accumulate(x, y, p);
             }
         }
+#endif
         STAMP3_SYNC(9);
         __syncthreads();
         STAMP3(10);
@@ -957,7 +967,11 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
             const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(cm, 0, 0x7FFFFFF8, 0x00020000);
             const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(cl, 0, 0x7FFFFFF8, 0x00020000);
             const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(chh, 0, 0x7FFFFFF8, 0x00020000);
+#ifdef PVAC_EXP_SKIP_W   // experiment builds only: no writer (outputs wrong; the phase's cost)
+            for (uint32_t p = tid; p < 0u; p += BS - 64) {
+#else
             for (uint32_t p = tid; p < total && wave != NW - 1; p += BS - 64) {
+#endif
                 unsigned long long* q = lim + 3u * p;
                 const uint64_t l0 = q[0], l1 = q[1], l2c = q[2];
                 q[0] = 0;

@@ -299,6 +299,14 @@ __global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint
         if constexpr (OP == 33) PVAC_IP16(PVAC_IPS("v_lshrrev_b32", "%16,", ""));
         if constexpr (OP == 34) PVAC_IP16(PVAC_IPS("v_mov_b32", "", ""));
         if constexpr (OP == 35) PVAC_IP16(PVAC_IPS("v_max_u32", "", ",%16"));
+        // SDWA forms (k_sigma's column flips use them)
+        if constexpr (OP == 36)
+            PVAC_IP16(PVAC_IPS("v_add_u32_sdwa", "", ",%16 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"));
+        if constexpr (OP == 37)
+            PVAC_IP16(PVAC_IPS("v_lshlrev_b32_sdwa", "%16,", " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"));
+        if constexpr (OP == 38) PVAC_IP16(PVAC_IPS("v_lshlrev_b32_sdwa", "", ",%16 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"));
+        if constexpr (OP == 39) PVAC_IP16(PVAC_IPS("v_xor_b32_e64", "", ",%16"));
+        if constexpr (OP == 40) PVAC_IP16(PVAC_IPS("v_mad_u32_u24", "", ",%16,%17"));
     }
     uint32_t acc = 0;
 #pragma unroll
@@ -314,7 +322,7 @@ __global__ void k_probe_issue(uint64_t* out, uint64_t* clk, uint32_t iters, uint
 #undef PVAC_IPS
 #undef PVAC_IPK
 
-constexpr int kIssueOps = 36;
+constexpr int kIssueOps = 41;
 using probe_fn = void (*)(uint64_t*, uint64_t*, uint32_t, uint32_t);
 template <int... I>
 constexpr auto issue_table(std::integer_sequence<int, I...>) {
