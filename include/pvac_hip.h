@@ -283,7 +283,8 @@ typedef struct pvac_chain_opts {
     const int* devices;              /* HOST [n_devices] GPU ordinals; null / 0 = ctx's device */
     uint32_t n_devices;              /* 0 .. PVAC_CHAIN_MAX_DEVICES */
     uint32_t pad2;
-    uint64_t* sumdigest_out;         /* DEVICE [count_n], nullable: pvac_hip_batch_sumdigest of c_depth */
+    uint64_t* sumdigest_out;         /* DEVICE [sumdigest_n], nullable: pvac_hip_batch_sumdigest of c_depth */
+    uint64_t sumdigest_n;            /* leading inputs whose sum digests are written (reads their whole c_depth) */
 } pvac_chain_opts;
 typedef struct pvac_chain_stats {
     uint64_t pair_steps;                        /* inputs x depth */

@@ -91,7 +91,7 @@ class ChainOpts(C.Structure):
                 ("on_chunk", ON_CHUNK_CB),
                 ("user", C.c_void_p), ("nonces_at", STEP_CB), ("after_step", STEP_CB), ("salts_at", STEP_CB),
                 ("devices", C.c_void_p), ("n_devices", C.c_uint32), ("pad2", C.c_uint32),
-                ("sumdigest_out", C.c_void_p)]
+                ("sumdigest_out", C.c_void_p), ("sumdigest_n", C.c_uint64)]
 
 
 class ChainStats(C.Structure):
@@ -433,13 +433,15 @@ class Engine:
         serially, a count is a copy). sigma: the final step with sigmas (needs H). devices: GPU
         ordinals, one contiguous range of whole chunks each (stage_inputs: ranges after the first copy
         their chunks to worker buffers even on this device). nonces_at / after_step / salts_at: STEP_CB
-        hooks (include/pvac_hip.h)."""
+        hooks (include/pvac_hip.h). sumdigest: True (every input) or the number of leading inputs
+        whose pvac_hip_batch_sumdigest is returned."""
         torch = self.torch
         dn = min(int(digest_n), X.n)
         cn = dn if count_n is None else min(int(count_n), X.n)
         dig = torch.zeros(max(dn, 1), dtype=torch.int64, device=self.device)
         cnt = torch.zeros(max(cn, 1), dtype=torch.int64, device=self.device)
-        sdg = torch.zeros(max(cn, 1), dtype=torch.int64, device=self.device) if sumdigest and cn else None
+        sn = min(X.n if sumdigest is True else int(sumdigest or 0), X.n)   # True: every input
+        sdg = torch.zeros(max(sn, 1), dtype=torch.int64, device=self.device) if sn else None
         devs = (C.c_int * len(devices))(*devices) if devices else None
         o = ChainOpts(depth=depth, streams=streams, chunk=chunk, nonce_seed=nonce_seed,
                       flags=(CHAIN_CHECK_GSUM if check_gsum else 0) | (MUL_ORDER_CANONICAL if canonical else 0) |
@@ -450,7 +452,7 @@ class Engine:
                       nonces_at=nonces_at or STEP_CB(), after_step=after_step or STEP_CB(),
                       salts_at=salts_at or STEP_CB(), devices=C.cast(devs, C.c_void_p) if devs else None,
                       n_devices=len(devices) if devices else 0, pad2=0,
-                      sumdigest_out=C.c_void_p(sdg.data_ptr()) if sdg is not None else None)
+                      sumdigest_out=C.c_void_p(sdg.data_ptr()) if sdg is not None else None, sumdigest_n=sn)
         st = ChainStats()
         sx = X.struct()
         self._check(self.lib.pvac_hip_ct_mul_chain(self.ctx, C.byref(sx), C.byref(o), C.byref(st)))
@@ -462,7 +464,7 @@ class Engine:
         if cn:
             res["counts"] = cnt[:cn].cpu().numpy().view(np.uint64).copy()
         if sdg is not None:
-            res["sumdigests"] = sdg[:cn].cpu().numpy().view(np.uint64).copy()
+            res["sumdigests"] = sdg[:sn].cpu().numpy().view(np.uint64).copy()
         return res
 
     def ct_mul_redo_count(self):

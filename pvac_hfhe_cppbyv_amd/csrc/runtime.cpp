@@ -1822,7 +1822,7 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
             return hipchk(hipMemcpyPeerAsync(dst + c0, sh->x_dev, k->chain_out, k->device, m * 8, k->stream), "peer copy");
         };
         if (!out_words(o.digest_n, o.digest_out, 1) || !out_words(o.count_n, o.count_out, 0) ||
-            !out_words(o.count_n, o.sumdigest_out, 2))
+            !out_words(o.sumdigest_n, o.sumdigest_out, 2))
             return;
         if (o.on_chunk && o.on_chunk(o.user, c0, &A, (void*)k->stream) != 0) {
             sh->failed(PVAC_EINVAL, "ct_mul_chain: on_chunk callback failed");

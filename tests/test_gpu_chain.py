@@ -222,10 +222,11 @@ def test_chain_two_device_ranges_equal_one_device():
     eng = Engine(device=0, canon_tag=0xD0D0)
     n, depth, chunk = 37, 4, 5
     X = eng.gen_fresh(n, 0xD0D1, 20)
-    one = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n, nonce_seed=0xD0D2)
+    one = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n, nonce_seed=0xD0D2, sumdigest=True)
     two = eng.ct_mul_chain(X, depth, streams=2, chunk=chunk, digest_n=n, nonce_seed=0xD0D2, devices=[0, 0],
-                           stage_inputs=True)
+                           stage_inputs=True, sumdigest=23)
     assert np.array_equal(one["digests"], two["digests"]) and np.array_equal(one["counts"], two["counts"])
+    assert len(one["sumdigests"]) == n and np.array_equal(one["sumdigests"][:23], two["sumdigests"])
     assert one["edges"] == two["edges"] and one["products"] == two["products"]
     assert two["chunks"] == one["chunks"] == (n + chunk - 1) // chunk
     three = eng.ct_mul_chain(X, depth, streams=1, chunk=chunk, digest_n=n, nonce_seed=0xD0D2, devices=[0, 0, 0])
