@@ -390,15 +390,21 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
 #ifndef PVAC_F3_BS   // A/B builds only: workgroup size of k_ct_mul_fresh3
 #define PVAC_F3_BS 512
 #endif
+#ifndef PVAC_F3_WPE   // A/B builds only: waves per SIMD the kernel is compiled for (6: <= 80 VGPRs)
+#define PVAC_F3_WPE 6
+#endif
+#ifndef PVAC_F3_U     // A/B builds only: product rounds per thread kept in registers from P1 to P5
+#define PVAC_F3_U 4
+#endif
 constexpr uint32_t kF3Threads = PVAC_F3_BS;
 template <int BS>
-__global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* __restrict__ gp, fresh3_layout Ls) {
+__global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fresh_args* __restrict__ gp, fresh3_layout Ls) {
     constexpr int KI = (kFreshKeysMax + BS - 1) / BS;    // key slots per thread (rebuild)
     // bins per thread: a bin holds 2 or 3 slots except when size-2 buckets are left without a
     // size-1 partner, so there are at most kFreshKeysMax / 2 bins
     constexpr int KR = (kFreshKeysMax / 2 + BS - 1) / BS;
     constexpr int NW = BS / 64;
-    constexpr int U = 4;                                 // product rounds per pass
+    constexpr int U = PVAC_F3_U;                         // product rounds per pass
     constexpr uint32_t kT16 = 0xFFFFu;                   // no first-insert time
     static_assert(BS % 64 == 0 && BS >= (int)kFreshEdgesMax && NW <= 16, "fresh geometry");
     static_assert(kFreshProdMax <= 16u * 256u, "16 scan segments of 256 product times");
@@ -924,6 +930,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 uint32_t p[2];
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
+                    if (u0 + v >= U) break;   // odd U (A/B builds)
                     const uint32_t pk = prod[u0 + v] == ~0u ? 0u : prod[u0 + v];
                     x[v] = a_w[pk & 0xFFu];
                     y[v] = b_w[(pk >> 8) & 0xFFu];
@@ -931,7 +938,7 @@ __global__ __launch_bounds__(BS, 6) void k_ct_mul_fresh3(const mul_fresh_args* _
                 }
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
-                    if (prod[u0 + v] != ~0u) accumulate(x[v], y[v], p[v]);
+                    if (u0 + v < U && prod[u0 + v] != ~0u) accumulate(x[v], y[v], p[v]);
             }
             // further passes (n > U * BS): recompute
             for (uint32_t t = tid + U * BS; t < n; t += BS) {
