@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PVAC_HIP_ABI_VERSION 1
+#define PVAC_HIP_ABI_VERSION 2
 
 /* status codes */
 #define PVAC_OK 0
@@ -295,6 +295,9 @@ typedef struct pvac_chain_stats {
     uint64_t redo;                              /* pairs re-run on the general path (ct_mul_exec) */
     uint64_t chunks;
     double seconds;                             /* wall time of the call */
+    uint64_t image_steps;                       /* pair-steps whose C went to the next step as a dense
+                                                   image (intermediate steps, no after_step hook or
+                                                   gsum check): the layout the next step reads back */
 } pvac_chain_stats;
 int pvac_hip_ct_mul_chain(pvac_hip_ctx* ctx, const pvac_ct_batch* X, const pvac_chain_opts* opts,
                           pvac_chain_stats* stats);

@@ -97,7 +97,8 @@ class ChainOpts(C.Structure):
 class ChainStats(C.Structure):
     _fields_ = [("pair_steps", C.c_uint64), ("edges", C.c_uint64 * CHAIN_MAX_DEPTH),
                 ("products", C.c_uint64 * CHAIN_MAX_DEPTH), ("gsum_pairs", C.c_uint64), ("gsum_failed", C.c_uint64),
-                ("redo", C.c_uint64), ("chunks", C.c_uint64), ("seconds", C.c_double)]
+                ("redo", C.c_uint64), ("chunks", C.c_uint64), ("seconds", C.c_double),
+                ("image_steps", C.c_uint64)]
 
 
 def load_library(path: str = _LIB_PATH) -> C.CDLL:
@@ -458,7 +459,8 @@ class Engine:
         self._check(self.lib.pvac_hip_ct_mul_chain(self.ctx, C.byref(sx), C.byref(o), C.byref(st)))
         res = {"pair_steps": st.pair_steps, "edges": [st.edges[d] for d in range(depth)],
                "products": [st.products[d] for d in range(depth)], "gsum_pairs": st.gsum_pairs,
-               "gsum_failed": st.gsum_failed, "redo": st.redo, "chunks": st.chunks, "seconds": st.seconds}
+               "gsum_failed": st.gsum_failed, "redo": st.redo, "chunks": st.chunks, "seconds": st.seconds,
+               "image_steps": st.image_steps}
         if dn:
             res["digests"] = dig[:dn].cpu().numpy().view(np.uint64).copy()
         if cn:

@@ -338,6 +338,12 @@ struct mul_large_args {
     uint32_t pad4;
     uint64_t* redo_ids;          // pairs the host re-runs on the full layout (shared with the fresh kernel)
     unsigned int* redo_cnt;
+    // chain steps (pvac_hip_ct_mul_chain): a pair whose A_img flag is set holds A as a dense image
+    // (k_large_products_direct's image writer) instead of hash-order records; a direct pair of a
+    // step with C_img writes C that way when it is dense, and k_large_direct_redo sets its flag
+    uint32_t* A_img;             // nullable, [n pairs]
+    uint32_t* C_img;             // nullable, [n pairs]
+    unsigned long long* img_count;   // nullable: += 1 per pair written as an image
     // launch sizing (maxima over the nl descriptors; max_tasks over the per-task class, max_tasks_all
     // over all, max_la_wg = ceil(|A.L| / kLaPerWG) over the A-layer-major class)
     uint64_t max_S, max_zero, max_tasks, max_capE, max_lay, max_tasks_all, max_la_wg, max_nA;
@@ -347,6 +353,10 @@ struct mul_large_args {
 constexpr uint32_t kLaPerWG = 4;
 constexpr uint32_t kLaMaxLB = 4;
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
+// dense chain images back to hash-order records for the listed pairs whose flag is set (the flag is
+// cleared): tmp holds 3 words per edge of every listed pair (sum of their |A.E|)
+hipError_t launch_image_to_records(const pvac_ct_batch& A, uint32_t* img, const uint64_t* pairs, uint32_t n_pairs,
+                                   uint64_t* tmp, uint32_t Bm, hipStream_t st);
 // LDS of k_large_products_direct for B and nbl staged B layers (the direct mode needs it <= 160 KB)
 uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl);
 // measured integer-ALU ceilings (k_ubench.hip)
@@ -368,6 +378,7 @@ constexpr uint32_t kCntIFail = 8;     // cnt word: an iblk pair uses the block m
 constexpr uint32_t kCntIShared = 9;   // cnt word: an iblk pair has keys sharing a bucket (order probes)
 constexpr uint32_t kCntDirect = 10;   // cnt word: a direct pair's positions are final (k_large_scan_direct)
 constexpr uint32_t kCntRedo = 11;     // cnt word: a direct pair was handed to the host's redo
+constexpr uint32_t kCntImg = 12;      // cnt word: a direct pair writes C as a dense image (k_large_scan_direct)
 constexpr uint32_t kIblkMaxNB = 63;   // iblk: |B.E| <= 63 (a 64-bit mask per A edge, bit 63 a flag)
 // static bucket groups of key slots [0, S) for one bucket count: head[s] = 0 when s is alone in
 // its bucket, else the first slot + 1 of the bucket's chain; next[s] = the following slot + 1

@@ -136,6 +136,18 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     for (uint32_t l = tid; l < LA + LB; l += kLBig) hist[l] = 0;
     if (tid == 0) flag = 0;
     __syncthreads();
+    // A as a dense chain image (mul_large_args::A_img, written by the previous step's
+    // k_large_products_direct): layer l >= first holds the 2B edges [(l - first) 2B, (l - first + 1) 2B)
+    // in cell order, each meta's low word already this kernel's direct id (hash-order edge | cell << 21):
+    // the lists are the slabs themselves, nothing to validate or bucket
+    const bool aimg = g.A_img && g.A_img[pr];
+    const uint32_t slab = 2u * Bm;
+    const uint32_t nslab = aimg ? nA / slab : 0u;
+    const uint32_t first = aimg && nslab <= LA ? LA - nslab : 0u;
+    if (aimg) {
+        for (uint32_t l = first + tid; l < LA; l += kLBig) hist[l] = slab;
+        if (tid == 0 && (nslab > LA || nslab * slab != nA || !d.direct)) flag = 1;
+    }
     // four edges per thread and round, loads first; the first kListRegRounds rounds keep each edge's
     // layer and cell in registers for the scatter pass (layer < 2^15, cell < 2^11), later rounds
     // load their metas again
@@ -156,12 +168,14 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
             else atomicAdd(&hist[la], 1u);
         }
     };
+    if (!aimg) {
 #pragma unroll
-    for (uint32_t r = 0; r < kListRegRounds; ++r)
-        if (tid + r * 4u * kLBig < nA) hist_round(tid + r * 4u * kLBig, pk[r]);
-    for (uint32_t i0 = tid + kListRegRounds * 4u * kLBig; i0 < nA; i0 += 4u * kLBig) {
-        uint32_t pr[4];
-        hist_round(i0, pr);
+        for (uint32_t r = 0; r < kListRegRounds; ++r)
+            if (tid + r * 4u * kLBig < nA) hist_round(tid + r * 4u * kLBig, pk[r]);
+        for (uint32_t i0 = tid + kListRegRounds * 4u * kLBig; i0 < nA; i0 += 4u * kLBig) {
+            uint32_t pr[4];
+            hist_round(i0, pr);
+        }
     }
     for (uint32_t j = tid; j < nB; j += kLBig) {
         const uint64_t m = g.B.meta[beo + j];
@@ -190,6 +204,7 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
         uint32_t start = 0;
         if (c) {
             start = atomicAdd(&cnt[a ? 5 : 6], c);
+            if (aimg && a) start = (ll - first) * slab;   // the layer's slab
             const uint32_t k = atomicAdd(&cnt[a ? 0 : 1], 1u);
             (S + (a ? d.o_neA : d.o_neB))[k] = ll;
         }
@@ -216,10 +231,12 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
             idsA[atomicAdd(&hist[pr[u] & 0x7FFFu], 1u)] = i | (uint32_t)((cell << dsh) & 0xFFFFFFFFull);
         }
     };
+    if (!aimg) {   // (an image's ids are the low words of its metas: the direct kernels read them there)
 #pragma unroll
-    for (uint32_t r = 0; r < kListRegRounds; ++r)
-        if (tid + r * 4u * kLBig < nA) scatter_round(tid + r * 4u * kLBig, pk[r]);
-    for (uint32_t i0 = tid + kListRegRounds * 4u * kLBig; i0 < nA; i0 += 4u * kLBig) {
+        for (uint32_t r = 0; r < kListRegRounds; ++r)
+            if (tid + r * 4u * kLBig < nA) scatter_round(tid + r * 4u * kLBig, pk[r]);
+    }
+    for (uint32_t i0 = tid + kListRegRounds * 4u * kLBig; i0 < nA && !aimg; i0 += 4u * kLBig) {
         uint64_t m[4];
         uint32_t pr[4];
 #pragma unroll
@@ -250,6 +267,7 @@ struct layer_src {
     uint64_t eo;          // the pair's edge offset in X
     const uint32_t* ids;
     uint32_t n;
+    uint32_t ish = 0;     // 1: id k is ids[2 k] (the low words of a dense chain image's metas)
 };
 __device__ __forceinline__ edge_rec load_edge(const layer_src& L, uint32_t k) {
     const uint32_t e = L.ids[k];
@@ -965,7 +983,7 @@ __device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint32_t k = k0 + (uint32_t)v * BS;
-            e[v] = k0 == tid ? pre[v] : D.ids[k < D.n ? k : 0u];   // A edge | dense cell << 21 (k_large_lists)
+            e[v] = k0 == tid ? pre[v] : D.ids[(k < D.n ? k : 0u) << D.ish];   // A edge | dense cell << 21 (k_large_lists)
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -1028,15 +1046,17 @@ __global__ __launch_bounds__(BS, PVAC_CNT_MINB) void k_large_count_la(mul_large_
     }
     uint32_t st_c = S[d.o_lstA + la_c], n_c = S[d.o_lstA + LA + la_c];
     const uint64_t mbj = tid < nB ? g.B.meta[beo + tid] : 0ull;   // bjt below
-    // level 3
-    const uint32_t* idsA = S + d.o_lstA + 2u * LA;
+    // level 3 (A as a dense chain image: its ids are the low words of its metas, k_large_lists)
+    const bool aimg = g.A_img && g.A_img[d.pair];
+    const uint32_t ish = aimg ? 1u : 0u;
+    const uint32_t* idsA = aimg ? (const uint32_t*)(g.A.meta + g.A.e_off[d.pair]) : S + d.o_lstA + 2u * LA;
     const uint32_t* idsB = S + d.o_lstB + 2u * LB;
     uint32_t pre[4];
     auto load_ids = [&](uint32_t st, uint32_t n) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint32_t k = tid + (uint32_t)v * BS;
-            pre[v] = idsA[st + (k < n ? k : 0u)];
+            pre[v] = idsA[(st + (k < n ? k : 0u)) << ish];
         }
     };
     load_ids(st_c, n_c);
@@ -1084,7 +1104,7 @@ __global__ __launch_bounds__(BS, PVAC_CNT_MINB) void k_large_count_la(mul_large_
     for (uint32_t i = i0; i < i1; ++i) {
         DSTAMP(0);
         const uint32_t la = late(la_c);
-        const layer_src srcA{&g.A, 0, idsA + late(st_c), late(n_c)};
+        const layer_src srcA{&g.A, 0, idsA + (late(st_c) << ish), late(n_c), ish};
         bool ok = srcA.n >= kLargeDenseMin;
 #pragma unroll
         for (uint32_t k = 0; k < kLaMaxLB; ++k) ok &= k >= neB || (nbv[k] <= kMxMaxSparse && nbv[k] <= srcA.n);
@@ -1255,6 +1275,13 @@ __global__ __launch_bounds__(kLBig) void k_large_scan_direct(mul_large_args g) {
         cnt[3] = total;
         cnt[4] = 0;
         cnt[kCntDirect] = 1;
+        // a chain step writes C as a dense image when every cell of every product layer (la, lb) with
+        // edges on both sides holds a key (and the hash positions fit the 21-bit ids the next step's
+        // lists carry)
+        cnt[kCntImg] = g.C_img && !g.salt_pos && (uint64_t)total == (uint64_t)cnt[0] * cnt[1] * 2u * g.Bm &&
+                               total < (1u << 21)
+                           ? 1u
+                           : 0u;
         g.C.e_cnt[d.pair] = total;
         g.pair_status[d.pair] = 0;
     }
@@ -1268,7 +1295,14 @@ __global__ __launch_bounds__(64) void k_large_direct_redo(mul_large_args g) {
     const large_desc& d = g.desc[q];
     if (!d.direct) return;
     const uint32_t* cnt = g.scratch + d.o_cnt;
-    if (cnt[2] || !cnt[kCntRedo]) return;
+    if (cnt[2]) return;
+    if (!cnt[kCntRedo]) {   // finished here: its C is a dense image when the image writer ran
+        if (g.C_img && cnt[kCntDirect] && cnt[kCntImg]) {
+            g.C_img[d.pair] = 1u;
+            if (g.img_count) atomicAdd(g.img_count, 1ull);
+        }
+        return;
+    }
     g.pair_status[d.pair] = kPairRedo;
     g.redo_ids[atomicAdd(g.redo_cnt, 1u)] = d.pair;
 }
@@ -1417,8 +1451,10 @@ __host__ __device__ inline uint32_t dir_lds_bytes(uint32_t Bm, uint32_t nbl) {
 
 // the dense side (an A layer) as digits, one copy per channel (k_large_count_la checked for
 // duplicate cells). Barriers inside; every thread calls it.
+// slab: kInf, or (A held as a dense chain image) the layer's first edge slot: list entry k's weight
+// sits at slab + k instead of at its hash-order edge (a contiguous read instead of a gather)
 template <int BS>
-__device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D) {
+__device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D, uint32_t slab) {
     constexpr uint32_t kV = 3;   // a dense A layer (<= 2 B = 674 edges) in one round of loads
     const uint32_t tid = threadIdx.x;
     uint32_t c[kV];
@@ -1427,10 +1463,12 @@ __device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D) {
 #pragma unroll
         for (uint32_t v = 0; v < kV; ++v) {
             const uint32_t k = k0 + v * BS;
-            const uint32_t id = D.ids[k < D.n ? k : 0u];   // D.n >= kLargeDenseMin
+            const uint32_t kc = k < D.n ? k : 0u;   // D.n >= kLargeDenseMin
+            const uint32_t id = D.ids[kc << D.ish];
             c[v] = id >> 21;
-            lo[v] = D.X->w_lo[D.eo + (id & 0x1FFFFFu)];
-            hi[v] = D.X->w_hi[D.eo + (id & 0x1FFFFFu)];
+            const uint32_t e = slab != kInf ? slab + kc : (id & 0x1FFFFFu);
+            lo[v] = D.X->w_lo[D.eo + e];
+            hi[v] = D.X->w_hi[D.eo + e];
         }
     };
     auto put = [&](uint32_t k0) {
@@ -1596,18 +1634,24 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     const __amdgpu_buffer_rsrc_t rlo = __builtin_amdgcn_make_buffer_rsrc(g.C.w_lo + ceo, 0, 0x7FFFFFF8, 0x00020000);
     const __amdgpu_buffer_rsrc_t rhi = __builtin_amdgcn_make_buffer_rsrc(g.C.w_hi + ceo, 0, 0x7FFFFFF8, 0x00020000);
     const uint32_t i1 = min(neA, i0 + g.la_per_wg);
+    const bool aimg = g.A_img && g.A_img[d.pair];   // A as dense images (k_large_lists made its lists the slabs)
+    const bool cimg = cnt[kCntImg] != 0;             // C as dense images (k_large_scan_direct)
+    // image slabs: C's kept product layers are exactly those with keys, last in C's layer order and in
+    // (la, lb) order, one slab of 2B cells each: C layer lid's slab starts at (lid - nbase) 2B
+    const uint32_t nbase = cimg ? (uint32_t)g.C.l_cnt[d.pair] - cnt[0] * cnt[1] : 0u;   // k_large_layers set l_cnt
     // layer headers one layer ahead: the next layer's id loads during this layer's staging, its
     // list range and writer-list length during this layer's writer
     uint32_t la = S[d.o_neA + i0];
     uint32_t a_start = S[d.o_lstA + la], a_n = S[d.o_lstA + LA + la], a_nw = S[d.o_wln + la];
     for (uint32_t ia = i0; ia < i1; ++ia) {
-        const layer_src srcA{&g.A, aeo, S + d.o_lstA + 2u * LA + a_start, a_n};
+        const layer_src srcA = aimg ? layer_src{&g.A, aeo, (const uint32_t*)(g.A.meta + aeo) + 2u * a_start, a_n, 1u}
+                                    : layer_src{&g.A, aeo, S + d.o_lstA + 2u * LA + a_start, a_n};
         uint32_t lid[kLaMaxLB];
 #pragma unroll
         for (uint32_t k = 0; k < kLaMaxLB; ++k) lid[k] = k < neB ? remap[LA + LB + la * LB + lbv[k]] : 0u;
         const uint32_t la_nx = ia + 1u < i1 ? S[d.o_neA + ia + 1u] : 0u;
         DSTAMP(0);
-        dir_stage_dense<BS>(dig, Bm, srcA);   // barriers inside (they also publish the B staging)
+        dir_stage_dense<BS>(dig, Bm, srcA, aimg ? a_start : kInf);   // barriers inside (they also publish the B staging)
         DSTAMP(1);
         for (uint32_t k = 0; k < neB; ++k) {
             const uint4* prec = (const uint4*)(sreg + k * kMxSparseBytes);
@@ -1635,7 +1679,81 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
         ulonglong2* omk = (ulonglong2*)(oexc + BS);            // [BS] the entry's P / M masks
         uint32_t* part = (uint32_t*)(omk + BS);                // [BS / 64] scan partials
         const uint32_t lane = tid & 63u, wave = tid >> 6;
-        for (uint32_t b0 = 0; b0 < nw; b0 += BS) {   // workgroup-uniform
+        if (cimg) {
+            // dense image writer (a chain step whose C the next step reads): C layer lid (a product
+            // layer with keys) owns the 2B slots from (lid - nbase) 2B, cell c = ch B + r at slot + c:
+            // meta = (hash-order position | c << 21) | C layer << 32 (the next step's list id), the weights
+            // in cell order. One wave per writer-list entry, one lane per B edge j: key (j, P) sits after
+            // the entry's keys of larger j, (j, M) right after (j, P). With at most two B layers (chain
+            // steps) the positions go to an LDS table by cell (the dead okey region, 8 B x 2B) and every
+            // store is coalesced; otherwise each key's meta is stored where it is found.
+            const bool ptab_ok = neB <= 2u;   // workgroup-uniform
+            uint32_t* ptab = (uint32_t*)plds;   // [k][2B] position of cell c of staged B layer k
+            for (uint32_t b0 = 0; b0 < nw; b0 += BS) {   // workgroup-uniform
+                const uint32_t kq = b0 + tid;
+                const bool lv = kq < nw;
+                const uint32_t we = lv ? wle[lbase + kq] : 0u;
+                const ulonglong2 mk = lv ? wlm[lbase + kq] : make_ulonglong2(0ull, 0ull);
+                obase[tid] = lv ? dir_edge_off(c8, wo, we & 0x1FFFFFu) : 0u;
+                oidx[tid] = we >> 21;
+                omk[tid] = make_ulonglong2(mk.x & ~(1ull << 63), mk.y);
+                __syncthreads();
+                const uint32_t ne = min(nw - b0, (uint32_t)BS);
+                for (uint32_t l = wave; l < ne; l += BS / 64) {   // wave-uniform
+                    const ulonglong2 m2 = omk[l];
+                    const uint32_t hp = (uint32_t)(m2.x >> lane) & 1u, hm = (uint32_t)(m2.y >> lane) & 1u;
+                    if (!(hp | hm)) continue;
+                    const uint32_t above =
+                        lane == 63u ? 0u : (uint32_t)__popcll(m2.x >> (lane + 1u)) + (uint32_t)__popcll(m2.y >> (lane + 1u));
+                    const uint32_t pos = obase[l] + above;
+                    const uint32_t bj = bjt[lane];
+                    const uint32_t kb = (bj >> 12) & 15u;
+                    const uint32_t r = mod_small(oidx[l] + (bj & 0xFFFu), Bm);
+                    const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
+                    const uint32_t sbase = (lidk - nbase) * 2u * Bm;   // < 2^21 (k_large_scan_direct)
+                    if (ptab_ok) {
+                        if (hp) ptab[kb * 2u * Bm + r] = pos;
+                        if (hm) ptab[kb * 2u * Bm + Bm + r] = pos + hp;
+                        continue;
+                    }
+                    if (hp) {
+                        const ulonglong2 w = stg[(kb * Bm + r) * 2u];
+                        if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
+                        const uint64_t mv = (uint64_t)(pos | r << 21) | (uint64_t)lidk << 32;
+                        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta,
+                                                              (sbase + r) * 8u, 0, PVAC_DIR_STORE_AUX);
+                    }
+                    if (hm) {
+                        const ulonglong2 w = stg[(kb * Bm + r) * 2u + 1u];
+                        if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;
+                        const uint64_t mv = (uint64_t)((pos + hp) | (Bm + r) << 21) | (uint64_t)lidk << 32;
+                        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta,
+                                                              (sbase + Bm + r) * 8u, 0, PVAC_DIR_STORE_AUX);
+                    }
+                }
+                if (b0 + BS < nw) __syncthreads();   // the next round rewrites obase / oidx / omk
+            }
+            if (ptab_ok) __syncthreads();   // every position in the table
+#pragma unroll
+            for (uint32_t k = 0; k < kLaMaxLB; ++k) {   // the weights of every cell, coalesced
+                if (k >= neB) break;
+                const uint32_t sbase = (lid[k] - nbase) * 2u * Bm;
+                for (uint32_t c = tid; c < 2u * Bm; c += BS) {
+                    const uint32_t ch = c >= Bm ? 1u : 0u, r = c - ch * Bm;
+                    const ulonglong2 w = stg[(k * Bm + r) * 2u + ch];
+                    const uint32_t bo = (sbase + c) * 8u;
+                    if (ptab_ok) {   // every cell is a key (the image is dense)
+                        if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
+                        const uint64_t mv = (uint64_t)(ptab[k * 2u * Bm + c] | c << 21) | (uint64_t)lid[k] << 32;
+                        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta, bo, 0,
+                                                              PVAC_DIR_STORE_AUX);
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.x, (uint32_t)(w.x >> 32)}, rlo, bo, 0, PVAC_DIR_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.y, (uint32_t)(w.y >> 32)}, rhi, bo, 0, PVAC_DIR_STORE_AUX);
+                }
+            }
+        }
+        for (uint32_t b0 = 0; b0 < nw && !cimg; b0 += BS) {   // workgroup-uniform
             const uint32_t kq = b0 + tid;
             const bool lv = kq < nw;
             const uint32_t we = lv ? wle[lbase + kq] : 0u;
@@ -2288,6 +2406,55 @@ hipError_t launch_grp_build(fastmod64 nbm, uint32_t Bm, uint64_t S, uint32_t hbi
 }
 
 uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl) { return dir_lds_bytes(Bm, nbl); }
+
+// ---------------------------------------------------------------- dense chain images -> records
+// (k_large_products_direct's image writer; see mul_large_args::A_img) Listed pair y (pairs[y], its
+// edges at tmp + 3 pairs[n + y]): the image is copied out, then every slot's edge is written back at
+// its hash-order position as (meta, w_lo, w_hi); the flags are cleared last.
+__global__ __launch_bounds__(256) void k_img_copy(pvac_ct_batch A, const uint32_t* img, const uint64_t* pairs, uint32_t n,
+                                                  uint64_t* tmp) {
+    const uint64_t pr = pairs[blockIdx.y];
+    if (!img[pr]) return;
+    const uint64_t eo = A.e_off[pr], ne = A.e_cnt[pr];
+    uint64_t* t = tmp + 3u * pairs[n + blockIdx.y];
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < ne; k += (uint64_t)gridDim.x * 256u) {
+        t[3u * k] = A.meta[eo + k];
+        t[3u * k + 1u] = A.w_lo[eo + k];
+        t[3u * k + 2u] = A.w_hi[eo + k];
+    }
+}
+__global__ __launch_bounds__(256) void k_img_scatter(pvac_ct_batch A, const uint32_t* img, const uint64_t* pairs, uint32_t n,
+                                                     const uint64_t* tmp, uint32_t Bm) {
+    const uint64_t pr = pairs[blockIdx.y];
+    if (!img[pr]) return;
+    const uint64_t eo = A.e_off[pr], ne = A.e_cnt[pr];
+    const uint64_t* t = tmp + 3u * pairs[n + blockIdx.y];
+    for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < ne; k += (uint64_t)gridDim.x * 256u) {
+        const uint64_t m = t[3u * k];
+        const uint32_t pos = (uint32_t)m & 0x1FFFFFu, cell = ((uint32_t)m >> 21) & 0x7FFu;
+        if (pos >= ne) continue;   // not an image slot (never written by the image writer)
+        const uint32_t ch = cell >= Bm ? 1u : 0u;
+        A.meta[eo + pos] = make_meta((uint32_t)(m >> 32), cell - ch * Bm, ch);
+        A.w_lo[eo + pos] = t[3u * k + 1u];
+        A.w_hi[eo + pos] = t[3u * k + 2u];
+    }
+}
+__global__ __launch_bounds__(64) void k_img_clear(uint32_t* img, const uint64_t* pairs, uint32_t n) {
+    const uint32_t y = blockIdx.x * 64u + threadIdx.x;
+    if (y < n) img[pairs[y]] = 0u;
+}
+hipError_t launch_image_to_records(const pvac_ct_batch& A, uint32_t* img, const uint64_t* pairs, uint32_t n_pairs,
+                                   uint64_t* tmp, uint32_t Bm, hipStream_t st) {
+    if (!n_pairs) return hipSuccess;
+    for (uint32_t y0 = 0; y0 < n_pairs; y0 += 65535u) {   // grid y limit
+        const uint32_t ny = std::min<uint32_t>(n_pairs - y0, 65535u);
+        hipLaunchKernelGGL(k_img_copy, dim3(64, ny), dim3(256), 0, st, A, img, pairs + y0, n_pairs - y0, tmp);
+        hipLaunchKernelGGL(k_img_scatter, dim3(64, ny), dim3(256), 0, st, A, img, pairs + y0, n_pairs - y0, tmp, Bm);
+    }
+    hipLaunchKernelGGL(k_img_clear, dim3((n_pairs + 63u) / 64u), dim3(64), 0, st, img, pairs, n_pairs);
+    return hipGetLastError();
+}
+
 
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st) {
     if (!a.nl) return hipSuccess;

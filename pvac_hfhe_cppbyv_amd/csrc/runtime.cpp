@@ -51,6 +51,8 @@ struct chain_set {
     size_t e_cap = 0;
     uint64_t* sigma = nullptr;   // final step with PVAC_MUL_WITH_SIGMA: 1 KiB per edge slot
     size_t s_cap = 0;            // edge slots of sigma
+    uint32_t* img = nullptr;     // per pair: 1 = this step's C is a dense image (mul_large_args::C_img)
+    size_t img_cap = 0;
 };
 
 }  // namespace
@@ -133,6 +135,15 @@ struct pvac_hip_ctx {
     // general-path scratch cap in words (0 = half the free HBM): chain workers share the device
     uint64_t arena_cap_words = 0;
     bool large_no_direct = false;   // the redo run: every pair on the full (per-key sums) layout
+    // chain steps: per-pair dense-image flags of A (read; cleared where A is turned back into records)
+    // and of C (written) for the next exec (mul_large_args::A_img / C_img); null outside the chain
+    uint32_t* img_in = nullptr;
+    uint32_t* img_out = nullptr;
+    unsigned long long* img_count = nullptr;   // chain: pair-steps written as images (chain_stats' last word)
+    uint64_t* img_tmp = nullptr;       // image -> records: 3 words per edge of the pairs converted
+    size_t img_tmp_cap = 0;
+    uint64_t* img_pairs = nullptr;     // [2 n]: pair ids, then their offsets in img_tmp
+    size_t img_pairs_cap = 0;
     // pvac_hip_ct_mul_chain: worker contexts (own stream / arena), and a worker's own buffers
     std::vector<pvac_hip_ctx*> chain_kids;   // [range j * streams + w] of the last call's layout
     chain_set chain_bufs[2];
@@ -143,7 +154,7 @@ struct pvac_hip_ctx {
     size_t chain_salt_cap = 0;
     uint64_t* chain_out = nullptr;           // digests / counts of a chunk before the copy to X's device
     size_t chain_out_cap = 0;
-    unsigned long long* chain_stats = nullptr;   // [2 * PVAC_CHAIN_MAX_DEPTH]
+    unsigned long long* chain_stats = nullptr;   // [2 * PVAC_CHAIN_MAX_DEPTH + 1]: edges / products, image pair-steps
     uint64_t H_gen = 0;                      // bumped whenever H is set (a worker's copy follows it)
     uint64_t H_from = 0;                     // worker: the parent's H_gen its H copy was taken from
 };
@@ -445,7 +456,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     flush_timers(c);
     for (chain_set* b : {&c->chain_bufs[0], &c->chain_bufs[1], &c->chain_stage})
         for (void* q : {(void*)b->l_off, (void*)b->l_cnt, (void*)b->e_off, (void*)b->e_cnt, (void*)b->layers,
-                        (void*)b->meta, (void*)b->w_lo, (void*)b->w_hi, (void*)b->sigma})
+                        (void*)b->meta, (void*)b->w_lo, (void*)b->w_hi, (void*)b->sigma, (void*)b->img})
             if (q) hipFreeAsync(q, c->stream);
     for (void* q : {(void*)c->chain_nonces, (void*)c->chain_salts, (void*)c->chain_out})
         if (q) hipFreeAsync(q, c->stream);
@@ -460,6 +471,8 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->large_info);
     hipFree(c->redo_ids);
     hipFree(c->redo_cnt);
+    hipFree(c->img_tmp);
+    hipFree(c->img_pairs);
     hipFree(c->desc_dev);
     hipFree(c->sel_dev);
     hipFree(c->arena);
@@ -739,6 +752,29 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
 
 namespace {
 
+// A chain step's input held as dense images (ctx img_in, pvac_hip_ct_mul_chain) turned back into
+// hash-order records for the pairs given as (pair, |A.E|) before a path that reads A's records (the
+// non-direct kernels, the redo run). The device skips pairs whose flag is clear and clears the flags
+// of the pairs it converts.
+int images_to_records(pvac_hip_ctx* c, const pvac_ct_batch* A, const std::vector<std::pair<uint64_t, uint64_t>>& pn) {
+    if (!c->img_in || pn.empty()) return PVAC_OK;
+    std::vector<uint64_t> h(2 * pn.size());
+    uint64_t tot = 0;
+    for (size_t k = 0; k < pn.size(); ++k) {
+        h[k] = pn[k].first;
+        h[pn.size() + k] = tot;
+        tot += pn[k].second;
+    }
+    int rc = ensure_dev(c, c->img_pairs, c->img_pairs_cap, h.size(), "alloc image pairs");
+    if (!rc) rc = ensure_dev(c, c->img_tmp, c->img_tmp_cap, 3 * std::max<uint64_t>(tot, 1), "alloc image scratch");
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(c->img_pairs, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = launch_image_to_records(*A, c->img_in, c->img_pairs, (uint32_t)pn.size(), c->img_tmp, c->prm.B, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // h is read from the host stack
+    return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "chain images to records");
+}
+
 // Runs the general path over the plan's large pairs in sub-batches that fit the scratch budget.
 int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, const uint64_t* nonces,
               pvac_ct_batch* C, uint32_t flags, uint32_t* salt_pos) {
@@ -867,6 +903,9 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
         a.dir_lb = std::max<uint32_t>(mLBd, 1u);
         a.redo_ids = c->redo_ids;
         a.redo_cnt = c->redo_cnt;
+        a.A_img = c->img_in;
+        a.C_img = c->img_out;
+        a.img_count = c->img_out ? c->img_count : nullptr;
         a.la_per_wg = la_per_wg;
         a.la_xcd = la_xcd;
         e = launch_ct_mul_large(a, c->stream);
@@ -904,6 +943,22 @@ int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batc
         if (rc) return fail(c, rc, why);
     }
     std::sort(redo.begin(), redo.end(), [](const large_desc& x, const large_desc& y) { return x.pair < y.pair; });
+    // a chain step's image inputs become records first; the redo run reads and writes records only
+    uint32_t* const img_in = c->img_in;
+    uint32_t* const img_out = c->img_out;
+    if (img_in) {
+        std::vector<std::pair<uint64_t, uint64_t>> pn;
+        for (const large_desc& d : redo) pn.emplace_back(d.pair, d.nA);
+        const int rc = images_to_records(c, A, pn);
+        if (rc) return rc;
+    }
+    c->img_in = nullptr;
+    c->img_out = nullptr;
+    struct img_restore {
+        pvac_hip_ctx* c;
+        uint32_t *in, *out;
+        ~img_restore() { c->img_in = in; c->img_out = out; }
+    } img_guard{c, img_in, img_out};
     // run them as the context's large-pair set, then restore the plan's own set and its tables
     std::vector<large_desc> plan_set;
     plan_set.swap(c->large_host);
@@ -1002,6 +1057,13 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
             ++c->plan_stamp;
             return rc;
         }
+    }
+    if (plan->n_large && c->img_in) {   // chain step: image inputs of pairs off the direct mode -> records
+        std::vector<std::pair<uint64_t, uint64_t>> pn;
+        for (const large_desc& d : c->large_host)
+            if (!d.direct) pn.emplace_back(d.pair, d.nA);
+        const int rc = images_to_records(c, A, pn);
+        if (rc) return rc;
     }
     if (plan->n_large) {
         scoped_timer t(c, "ct_mul_large");
@@ -1553,6 +1615,11 @@ hipError_t grow_async(T*& p, size_t& cap, size_t need, hipStream_t st) {
     return e;
 }
 
+// intermediate chain steps as dense images (A/B builds: -DPVAC_CHAIN_IMAGE=0 keeps records throughout)
+#ifndef PVAC_CHAIN_IMAGE
+#define PVAC_CHAIN_IMAGE 1
+#endif
+
 struct chain_range {
     uint64_t end = 0;               // last input (exclusive) of this device range
     std::atomic<uint64_t> next{0};  // next chunk's first input
@@ -1716,6 +1783,10 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
     const bool check = (o.flags & PVAC_CHAIN_CHECK_GSUM) != 0;
     const bool sigma = (o.flags & PVAC_MUL_WITH_SIGMA) != 0;
     const bool remote = k->device != sh->x_dev;
+    // intermediate steps hand their C to the next step as dense images (mul_large_args::C_img) unless
+    // a caller hook or the gsum check reads every step's records; an image A never meets the fresh
+    // kernel, whose pairs have at most kFreshEdgesMax < 2B edges a side
+    const bool use_img = PVAC_CHAIN_IMAGE && !check && !o.after_step && 2u * k->prm.B > kFreshEdgesMax;
     auto hipchk = [&](hipError_t e, const char* where) {
         if (e == hipSuccess) return true;
         sh->failed(e == hipErrorOutOfMemory ? PVAC_ENOMEM : PVAC_EDEVICE,
@@ -1736,6 +1807,11 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
         if ((stage || remote) && !stage_chunk(k, sh, chain_view(X, c0, kk), Xv)) return;
         pvac_ct_batch A = Xv;
         int cur = 0;
+        uint32_t* a_img = nullptr;   // the previous step's image flags (A's)
+        struct img_reset {
+            pvac_hip_ctx* k;
+            ~img_reset() { k->img_in = k->img_out = nullptr; }
+        } img_guard{k};
         for (uint32_t d = 0; d < o.depth; ++d) {
             if (sh->stop.load()) return;
             chain_set& S = k->chain_bufs[cur];
@@ -1787,7 +1863,17 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
                                "fill nonces")) {
                 return;
             }
+            uint32_t* c_img = nullptr;
+            if (use_img && d + 1 < o.depth) {
+                if (kk > S.img_cap && !hipchk(grow_async(S.img, S.img_cap, kk, k->stream), "alloc image flags")) return;
+                if (!hipchk(hipMemsetAsync(S.img, 0, kk * 4, k->stream), "image flags")) return;
+                c_img = S.img;
+            }
+            k->img_in = a_img;
+            k->img_out = c_img;
+            k->img_count = k->chain_stats + 2 * PVAC_CHAIN_MAX_DEPTH;
             if (!rcchk(pvac_hip_ct_mul_exec(k, &plan, &A, &Xv, k->chain_nonces, nullptr, &C, mflags), "exec")) return;
+            k->img_out = nullptr;   // the final-step sigma re-run below reads A (img_in), writes records
             if (!hipchk(launch_chain_stats(A, Xv, C, k->chain_stats + 2 * d, k->stream), "stats")) return;
             if (check) {
                 uint64_t bad = 0;
@@ -1801,6 +1887,8 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
                 return;
             }
             if (sigma && d + 1 == o.depth && !chain_final_sigma(k, sh, d, c0, plan, A, Xv, C, S, mflags)) return;
+            k->img_in = nullptr;
+            a_img = c_img;
             A = C;
             cur ^= 1;
         }
@@ -1913,7 +2001,7 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
                     hipSetDevice(c->device);
                     return fail(c, rc, "ct_mul_chain: worker context");
                 }
-                e = hipMalloc(&k->chain_stats, 2 * PVAC_CHAIN_MAX_DEPTH * sizeof(unsigned long long));
+                e = hipMalloc(&k->chain_stats, (2 * PVAC_CHAIN_MAX_DEPTH + 1) * sizeof(unsigned long long));
                 if (e != hipSuccess) {
                     hipSetDevice(c->device);
                     return hip_fail(c, e, "ct_mul_chain: worker statistics");
@@ -1937,7 +2025,7 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
                 e = sigma_tables_clone(k->H, c->H, k->device, c->device, k->stream);
                 k->H_from = c->H_gen;
             }
-            if (e == hipSuccess) e = hipMemsetAsync(k->chain_stats, 0, 2 * PVAC_CHAIN_MAX_DEPTH * 8, k->stream);
+            if (e == hipSuccess) e = hipMemsetAsync(k->chain_stats, 0, (2 * PVAC_CHAIN_MAX_DEPTH + 1) * 8, k->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(k->stream);
             if (e != hipSuccess) {
                 hipSetDevice(c->device);
@@ -1975,12 +2063,14 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
         hipSetDevice(k->device);
         e = hipStreamSynchronize(k->stream);
         if (e != hipSuccess && sh.rc == PVAC_OK) sh.failed(PVAC_EDEVICE, std::string("ct_mul_chain: ") + hipGetErrorString(e));
-        unsigned long long v[2 * PVAC_CHAIN_MAX_DEPTH];
-        if (hipMemcpy(v, k->chain_stats, sizeof v, hipMemcpyDeviceToHost) == hipSuccess)
+        unsigned long long v[2 * PVAC_CHAIN_MAX_DEPTH + 1];
+        if (hipMemcpy(v, k->chain_stats, sizeof v, hipMemcpyDeviceToHost) == hipSuccess) {
             for (uint32_t d = 0; d < o->depth; ++d) {
                 st->edges[d] += v[2 * d];
                 st->products[d] += v[2 * d + 1];
             }
+            st->image_steps += v[2 * PVAC_CHAIN_MAX_DEPTH];
+        }
         st->gsum_pairs += ws[w].gsum_pairs;
         st->gsum_failed += ws[w].gsum_failed;
         st->chunks += ws[w].chunks;

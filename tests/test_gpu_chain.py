@@ -297,3 +297,74 @@ def test_chain_final_step_sigma_vs_oracle(oracle, manifest, H_dense):
             assert np.array_equal(out.w_lo, ref.w_lo) and np.array_equal(out.w_hi, ref.w_hi)
             assert np.array_equal(out.layers["ztag"], ref.layers["ztag"])
             assert np.array_equal(out.sigma, ref.sigma)
+
+
+def _enc_inputs(eng, n, seed):
+    sk, man, em = fixture_secret()
+    assert eng.gen_H().hex() == man["H_digest"]
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    eng.set_powg(read_u64("powg_B.u64"))
+    rng = np.random.default_rng(seed)
+    X, st = eng.enc_value(rng.integers(0, 2**64, n, dtype=np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+    assert not st.any()
+    return X, man
+
+
+def _oracle_chain(oracle, X, n, depth, canon_tag, edge_budget=1200000):
+    px = pack_device_batch(X, n)
+    P_ = lambda a: a.ctypes.data_as(C.c_void_p)
+    ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
+    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(canon_tag, edge_budget=edge_budget)), n,
+                                      *(P_(a) for a in px), depth, 8, P_(ocnt), P_(odig), P_(se))
+    return ocnt, odig
+
+
+def test_chain_dense_images_equal_records(oracle):
+    """Intermediate chain steps hand their C to the next step as dense images (k_large_products_direct's
+    image writer: cell c of product layer lp at slot lp 2B + c with its hash-order position; the next
+    step's k_large_lists takes the slabs as its A lists and the dense staging reads the weights in
+    slab order). enc_value inputs to depth 7 without hooks (steps 3-6 write images) give the same final
+    digests, edge counts and per-step edge sums as the same chains with an after_step hook (records
+    at every step), as the step-by-step engine run and as the CPU port."""
+    from pvac_hfhe_cppbyv_amd import STEP_CB, Engine
+    eng = Engine(device=0, canon_tag=fixture_secret()[1]["canon_tag"])
+    n, depth, chunk, seed = 5, 7, 3, 0x1A6E
+    X, man = _enc_inputs(eng, n, 0x1A6D)
+    img = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=2, chunk=chunk, digest_n=n)
+
+    def after(user, step, first, A, Xb, Cb, words, nw, stream):
+        return 0
+
+    rec = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=2, chunk=chunk, digest_n=n, after_step=STEP_CB(after))
+    assert img["redo"] == 0 and rec["redo"] == 0
+    assert img["image_steps"] == 4 * n and rec["image_steps"] == 0   # steps 3-6 handed on as images
+    assert np.array_equal(img["digests"], rec["digests"]) and np.array_equal(img["counts"], rec["counts"])
+    assert img["edges"] == rec["edges"] and img["edges"][5] == n * 128 * 674   # step 6: 128 dense product layers
+    dig, cnt, edges = _stepwise(eng, X, depth, seed, chunk)
+    assert np.array_equal(img["digests"], dig) and np.array_equal(img["counts"], cnt) and img["edges"] == edges
+    ocnt, odig = _oracle_chain(oracle, X, n, depth, man["canon_tag"])
+    assert np.array_equal(ocnt, cnt) and np.array_equal(odig, dig)
+
+
+def test_chain_image_inputs_redone_on_records(oracle):
+    """edge_budget between step 4's and step 5's output sizes (21,568 and 43,136 edges): step 4 writes
+    its C as dense images, and every step-5 pair exceeds the budget, so guard_budget's canonical order
+    sends it to the redo, which first turns its image input back into hash-order records
+    (k_img_copy / k_img_scatter). Final digests and counts equal the record-only run (after_step hook)
+    and the CPU port's chain with the same edge_budget."""
+    from pvac_hfhe_cppbyv_amd import STEP_CB, Engine
+    man = fixture_secret()[1]
+    eng = Engine(device=0, canon_tag=man["canon_tag"], edge_budget=30000)
+    n, depth, chunk, seed = 4, 6, 2, 0x1A6F
+    X, _ = _enc_inputs(eng, n, 0x1A70)
+    img = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=2, chunk=chunk, digest_n=n)
+    assert img["redo"] >= 2 * n and img["image_steps"] == 2 * n   # images: steps 3, 4; redone: steps 5, 6
+
+    def after(user, step, first, A, Xb, Cb, words, nw, stream):
+        return 0
+
+    rec = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=2, chunk=chunk, digest_n=n, after_step=STEP_CB(after))
+    assert np.array_equal(img["digests"], rec["digests"]) and np.array_equal(img["counts"], rec["counts"])
+    ocnt, odig = _oracle_chain(oracle, X, n, depth, man["canon_tag"], edge_budget=30000)
+    assert np.array_equal(ocnt, img["counts"]) and np.array_equal(odig, img["digests"])

@@ -1,6 +1,6 @@
 """cfg-4 chain A/B (GPU box): the chain call (pvac_hip_ct_mul_chain) on the same GPU enc_value inputs through
 each library given, alternating, with 1 and with 4 worker streams; final digests must agree between
-libraries. Usage: python tools/chain_ab.py [--inputs N] lib1.so [lib2.so ...]"""
+libraries. Usage: python tools/chain_ab.py [--inputs N] [--streams 1,4] lib1.so [lib2.so ...]"""
 import json
 import os
 import sys
@@ -18,8 +18,12 @@ from pvac_hfhe_cppbyv_amd import Engine, load_library  # noqa: E402
 def main():
     argv = sys.argv[1:]
     n = 16384
-    if argv and argv[0] == "--inputs":
-        n = int(argv[1])
+    streams = (1, 4)
+    while argv and argv[0] in ("--inputs", "--streams"):
+        if argv[0] == "--inputs":
+            n = int(argv[1])
+        else:
+            streams = tuple(int(x) for x in argv[1].split(","))
         argv = argv[2:]
     res = {}
     ref = None
@@ -33,7 +37,7 @@ def main():
         X, st = eng.enc_value(vals, rnd)
         del rnd
         name = os.path.basename(path)
-        for s in (1, 4):
+        for s in streams:
             eng.ct_mul_chain(X, 8, streams=s, chunk=1024)   # warm: arenas, buffers
             torch.cuda.synchronize()
             t = time.perf_counter()
@@ -45,7 +49,8 @@ def main():
             same = ref is None or bool(np.array_equal(ref, r["digests"]))
             if ref is None:
                 ref = r["digests"]
-            print(k, res[k], "ct_mul/s", "same" if same else "DIFFERENT", "redo", r["redo"], flush=True)
+            print(k, res[k], "ct_mul/s", "same" if same else "DIFFERENT", "redo", r["redo"], "image_steps",
+                  r.get("image_steps"), flush=True)
         del X, eng
         torch.cuda.empty_cache()
     print(json.dumps(res))
