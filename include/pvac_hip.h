@@ -247,6 +247,14 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  *              edge slots): dev_words[C.e_off[i] + k] is the salt of pair i's k-th emitted edge in
  *              the reference's emit order (hash order; a pair in the canonical order still takes its
  *              salts in hash order, as pvac_hip_ct_mul_exec does).
+ * Intermediate layout: without an after_step hook or the gsum check, a step from the third on whose
+ * C is dense (every cell of every product layer present, under 2^21 edges) hands C to the next step
+ * as a dense image instead of hash-order records: C's counts, offsets and layer records are final,
+ * but edge slot s of pair i holds cell s mod 2B of its s / 2B-th product layer with the edge's
+ * hash-order position in the meta's low 21 bits (stats.image_steps counts such pair-steps). The
+ * next step reads it in place (no per-layer edge gathers); a pair that leaves the direct mode gets
+ * its records back first. So nonces_at / salts_at may see A in that layout: read its counts and
+ * layers only. c_depth (on_chunk, digests) is always records.
  * Devices: with n_devices > 0 the inputs are split into n_devices contiguous ranges of whole chunks
  * (by global input index; a range never splits a chunk, so every chunk, its nonce seeds and its
  * results are those of a one-device run) and each range runs on `streams` worker threads on
