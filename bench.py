@@ -928,7 +928,7 @@ def chain_bench(eng, args):
         return {"inputs": n, "depth": depth, "chunk": chunk, "streams": S, "chain_seconds": chain_s,
                 "ct_mul_per_s": n * depth / chain_s, "timed_window_monotonic_ns": [w0, w1],
                 "edges_per_input_by_step": [e / n for e in r["edges"]], "products": float(sum(r["products"])),
-                "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak}
+                "redo_pairs": r["redo"], "image_pair_steps": r["image_steps"], "peak_hbm_reserved_gb": peak}
     # check pass (untimed): same nonces, gsum invariant on every pair-step, every final digest
     t2 = time.perf_counter()
     rc = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, check_gsum=True, digest_n=n_chk,
@@ -950,7 +950,11 @@ def chain_bench(eng, args):
            "enc_status_nonzero": bad, "input_edges_per_value": in_edges / n,
            "products": products, "Gfp_mul_per_s": products / chain_s / 1e9,
            "edges_per_input_by_step": [e / n for e in r["edges"]],
-           "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak, "timed_window_monotonic_ns": [w0, w1]}
+           "redo_pairs": r["redo"], "peak_hbm_reserved_gb": peak, "timed_window_monotonic_ns": [w0, w1],
+           "image_pair_steps": r["image_steps"],
+           "intermediate_layout": "dense images between steps 3..depth-1 (include/pvac_hip.h): the timed pass; "
+                                  "the check pass (gsum on every step) keeps records throughout, and its final "
+                                  "counts and sum digests must equal the timed pass's"}
     gf, gp = rc["gsum_failed"], rc["gsum_pairs"]
     out["invariant"] = {"check": "check_mul_gsum_all (reference utils/metrics.hpp:88-113) on every pair of every "
                                  "step, on the device (second, untimed pass with the same nonces)", "pair_steps": gp,

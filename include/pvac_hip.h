@@ -250,8 +250,9 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * Intermediate layout: without an after_step hook or the gsum check, a step from the third on whose
  * C is dense (every cell of every product layer present, under 2^21 edges) hands C to the next step
  * as a dense image instead of hash-order records: C's counts, offsets and layer records are final,
- * but edge slot s of pair i holds cell s mod 2B of its s / 2B-th product layer with the edge's
- * hash-order position in the meta's low 21 bits (stats.image_steps counts such pair-steps). The
+ * but edge slot s of pair i holds the weight of cell s mod 2B of its s / 2B-th product layer, and
+ * 32-bit word s of the pair's meta region holds that edge's hash-order position | cell << 21
+ * (stats.image_steps counts such pair-steps). The
  * next step reads it in place (no per-layer edge gathers); a pair that leaves the direct mode gets
  * its records back first. So nonces_at / salts_at may see A in that layout: read its counts and
  * layers only. c_depth (on_chunk, digests) is always records.

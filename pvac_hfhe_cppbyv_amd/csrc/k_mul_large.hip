@@ -138,8 +138,8 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
     __syncthreads();
     // A as a dense chain image (mul_large_args::A_img, written by the previous step's
     // k_large_products_direct): layer l >= first holds the 2B edges [(l - first) 2B, (l - first + 1) 2B)
-    // in cell order, each meta's low word already this kernel's direct id (hash-order edge | cell << 21):
-    // the lists are the slabs themselves, nothing to validate or bucket
+    // in cell order, and 32-bit word s of the pair's meta region is slot s's direct id (hash-order
+    // edge | cell << 21): the lists are the slabs themselves, nothing to validate or bucket
     const bool aimg = g.A_img && g.A_img[pr];
     const uint32_t slab = 2u * Bm;
     const uint32_t nslab = aimg ? nA / slab : 0u;
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kLBig) void k_large_lists(mul_large_args g) {
             idsA[atomicAdd(&hist[pr[u] & 0x7FFFu], 1u)] = i | (uint32_t)((cell << dsh) & 0xFFFFFFFFull);
         }
     };
-    if (!aimg) {   // (an image's ids are the low words of its metas: the direct kernels read them there)
+    if (!aimg) {   // (an image's ids sit in its meta region: the direct kernels read them there)
 #pragma unroll
         for (uint32_t r = 0; r < kListRegRounds; ++r)
             if (tid + r * 4u * kLBig < nA) scatter_round(tid + r * 4u * kLBig, pk[r]);
@@ -267,7 +267,6 @@ struct layer_src {
     uint64_t eo;          // the pair's edge offset in X
     const uint32_t* ids;
     uint32_t n;
-    uint32_t ish = 0;     // 1: id k is ids[2 k] (the low words of a dense chain image's metas)
 };
 __device__ __forceinline__ edge_rec load_edge(const layer_src& L, uint32_t k) {
     const uint32_t e = L.ids[k];
@@ -983,7 +982,7 @@ __device__ bool stage_tt(uint8_t* lds, uint32_t Bm, const layer_src& D, uint32_t
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint32_t k = k0 + (uint32_t)v * BS;
-            e[v] = k0 == tid ? pre[v] : D.ids[(k < D.n ? k : 0u) << D.ish];   // A edge | dense cell << 21 (k_large_lists)
+            e[v] = k0 == tid ? pre[v] : D.ids[k < D.n ? k : 0u];   // A edge | dense cell << 21 (k_large_lists)
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -1046,9 +1045,8 @@ __global__ __launch_bounds__(BS, PVAC_CNT_MINB) void k_large_count_la(mul_large_
     }
     uint32_t st_c = S[d.o_lstA + la_c], n_c = S[d.o_lstA + LA + la_c];
     const uint64_t mbj = tid < nB ? g.B.meta[beo + tid] : 0ull;   // bjt below
-    // level 3 (A as a dense chain image: its ids are the low words of its metas, k_large_lists)
+    // level 3 (A as a dense chain image: its ids are the 32-bit words of its meta region, k_large_lists)
     const bool aimg = g.A_img && g.A_img[d.pair];
-    const uint32_t ish = aimg ? 1u : 0u;
     const uint32_t* idsA = aimg ? (const uint32_t*)(g.A.meta + g.A.e_off[d.pair]) : S + d.o_lstA + 2u * LA;
     const uint32_t* idsB = S + d.o_lstB + 2u * LB;
     uint32_t pre[4];
@@ -1056,7 +1054,7 @@ __global__ __launch_bounds__(BS, PVAC_CNT_MINB) void k_large_count_la(mul_large_
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint32_t k = tid + (uint32_t)v * BS;
-            pre[v] = idsA[(st + (k < n ? k : 0u)) << ish];
+            pre[v] = idsA[st + (k < n ? k : 0u)];
         }
     };
     load_ids(st_c, n_c);
@@ -1104,7 +1102,7 @@ __global__ __launch_bounds__(BS, PVAC_CNT_MINB) void k_large_count_la(mul_large_
     for (uint32_t i = i0; i < i1; ++i) {
         DSTAMP(0);
         const uint32_t la = late(la_c);
-        const layer_src srcA{&g.A, 0, idsA + (late(st_c) << ish), late(n_c), ish};
+        const layer_src srcA{&g.A, 0, idsA + late(st_c), late(n_c)};
         bool ok = srcA.n >= kLargeDenseMin;
 #pragma unroll
         for (uint32_t k = 0; k < kLaMaxLB; ++k) ok &= k >= neB || (nbv[k] <= kMxMaxSparse && nbv[k] <= srcA.n);
@@ -1464,7 +1462,7 @@ __device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D, uin
         for (uint32_t v = 0; v < kV; ++v) {
             const uint32_t k = k0 + v * BS;
             const uint32_t kc = k < D.n ? k : 0u;   // D.n >= kLargeDenseMin
-            const uint32_t id = D.ids[kc << D.ish];
+            const uint32_t id = D.ids[kc];
             c[v] = id >> 21;
             const uint32_t e = slab != kInf ? slab + kc : (id & 0x1FFFFFu);
             lo[v] = D.X->w_lo[D.eo + e];
@@ -1644,8 +1642,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     uint32_t la = S[d.o_neA + i0];
     uint32_t a_start = S[d.o_lstA + la], a_n = S[d.o_lstA + LA + la], a_nw = S[d.o_wln + la];
     for (uint32_t ia = i0; ia < i1; ++ia) {
-        const layer_src srcA = aimg ? layer_src{&g.A, aeo, (const uint32_t*)(g.A.meta + aeo) + 2u * a_start, a_n, 1u}
-                                    : layer_src{&g.A, aeo, S + d.o_lstA + 2u * LA + a_start, a_n};
+        const layer_src srcA{&g.A, aeo, (aimg ? (const uint32_t*)(g.A.meta + aeo) : S + d.o_lstA + 2u * LA) + a_start, a_n};
         uint32_t lid[kLaMaxLB];
 #pragma unroll
         for (uint32_t k = 0; k < kLaMaxLB; ++k) lid[k] = k < neB ? remap[LA + LB + la * LB + lbv[k]] : 0u;
@@ -1682,8 +1679,8 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
         if (cimg) {
             // dense image writer (a chain step whose C the next step reads): C layer lid (a product
             // layer with keys) owns the 2B slots from (lid - nbase) 2B, cell c = ch B + r at slot + c:
-            // meta = (hash-order position | c << 21) | C layer << 32 (the next step's list id), the weights
-            // in cell order. One wave per writer-list entry, one lane per B edge j: key (j, P) sits after
+            // 32-bit word s of C's meta region = hash-order position | c << 21 (the next step's list id),
+            // the weights in cell order. One wave per writer-list entry, one lane per B edge j: key (j, P) sits after
             // the entry's keys of larger j, (j, M) right after (j, P). With at most two B layers (chain
             // steps) the positions go to an LDS table by cell (the dead okey region, 8 B x 2B) and every
             // store is coalesced; otherwise each key's meta is stored where it is found.
@@ -1719,16 +1716,13 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                     if (hp) {
                         const ulonglong2 w = stg[(kb * Bm + r) * 2u];
                         if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
-                        const uint64_t mv = (uint64_t)(pos | r << 21) | (uint64_t)lidk << 32;
-                        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta,
-                                                              (sbase + r) * 8u, 0, PVAC_DIR_STORE_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(pos | r << 21, rmeta, (sbase + r) * 4u, 0, PVAC_DIR_STORE_AUX);
                     }
                     if (hm) {
                         const ulonglong2 w = stg[(kb * Bm + r) * 2u + 1u];
                         if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;
-                        const uint64_t mv = (uint64_t)((pos + hp) | (Bm + r) << 21) | (uint64_t)lidk << 32;
-                        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta,
-                                                              (sbase + Bm + r) * 8u, 0, PVAC_DIR_STORE_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b32((pos + hp) | (Bm + r) << 21, rmeta, (sbase + Bm + r) * 4u, 0,
+                                                              PVAC_DIR_STORE_AUX);
                     }
                 }
                 if (b0 + BS < nw) __syncthreads();   // the next round rewrites obase / oidx / omk
@@ -1744,8 +1738,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                     const uint32_t bo = (sbase + c) * 8u;
                     if (ptab_ok) {   // every cell is a key (the image is dense)
                         if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
-                        const uint64_t mv = (uint64_t)(ptab[k * 2u * Bm + c] | c << 21) | (uint64_t)lid[k] << 32;
-                        __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)mv, (uint32_t)(mv >> 32)}, rmeta, bo, 0,
+                        __builtin_amdgcn_raw_buffer_store_b32(ptab[k * 2u * Bm + c] | c << 21, rmeta, (sbase + c) * 4u, 0,
                                                               PVAC_DIR_STORE_AUX);
                     }
                     __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.x, (uint32_t)(w.x >> 32)}, rlo, bo, 0, PVAC_DIR_STORE_AUX);
@@ -2417,8 +2410,9 @@ __global__ __launch_bounds__(256) void k_img_copy(pvac_ct_batch A, const uint32_
     if (!img[pr]) return;
     const uint64_t eo = A.e_off[pr], ne = A.e_cnt[pr];
     uint64_t* t = tmp + 3u * pairs[n + blockIdx.y];
+    const uint32_t* ids = (const uint32_t*)(A.meta + eo);
     for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < ne; k += (uint64_t)gridDim.x * 256u) {
-        t[3u * k] = A.meta[eo + k];
+        t[3u * k] = ids[k];
         t[3u * k + 1u] = A.w_lo[eo + k];
         t[3u * k + 2u] = A.w_hi[eo + k];
     }
@@ -2428,13 +2422,14 @@ __global__ __launch_bounds__(256) void k_img_scatter(pvac_ct_batch A, const uint
     const uint64_t pr = pairs[blockIdx.y];
     if (!img[pr]) return;
     const uint64_t eo = A.e_off[pr], ne = A.e_cnt[pr];
+    const uint64_t slab = 2u * Bm, first = A.l_cnt[pr] - ne / slab;   // the slabs are the last layers
     const uint64_t* t = tmp + 3u * pairs[n + blockIdx.y];
     for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < ne; k += (uint64_t)gridDim.x * 256u) {
-        const uint64_t m = t[3u * k];
-        const uint32_t pos = (uint32_t)m & 0x1FFFFFu, cell = ((uint32_t)m >> 21) & 0x7FFu;
+        const uint32_t id = (uint32_t)t[3u * k];
+        const uint32_t pos = id & 0x1FFFFFu, cell = id >> 21;
         if (pos >= ne) continue;   // not an image slot (never written by the image writer)
         const uint32_t ch = cell >= Bm ? 1u : 0u;
-        A.meta[eo + pos] = make_meta((uint32_t)(m >> 32), cell - ch * Bm, ch);
+        A.meta[eo + pos] = make_meta((uint32_t)(first + k / slab), cell - ch * Bm, ch);
         A.w_lo[eo + pos] = t[3u * k + 1u];
         A.w_hi[eo + pos] = t[3u * k + 2u];
     }
