@@ -362,12 +362,26 @@ __device__ __forceinline__ void fp_digits8(const fp& v, uint64_t& dl, uint64_t& 
 // k(i + 8) = k(i) + 16: 256^16 = 2^128 == 2 (mod p), so d[i] = c[i] + 2 c[i + 8] (32-bit, |d| < 2^24
 // for <= 20 sparse edges) leaves positions 4h..4h+3 (d[0..3]) and 8+4h..11+4h (d[4..7]), i.e. the
 // 32-bit words h and 2 + h of the row's value: ga, gb (|g| < 2^48.1).
+// acc + (int64) x * m in one v_mad_i64_i32 (sign extension, shift and 64-bit add: the compiler's
+// form of a power-of-two multiple is a sign-extending shift plus a 64-bit shift-add per term)
+#ifndef PVAC_MX_MAD
+#define PVAC_MX_MAD 1
+#endif
+__device__ __forceinline__ int64_t mad_i64_i32(int32_t x, uint32_t m, int64_t acc) {
+#if PVAC_MX_MAD
+    int64_t r;
+    asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(acc) : "vcc");
+    return r;
+#else
+    return acc + (int64_t)x * (int64_t)m;
+#endif
+}
 __device__ __forceinline__ void mx_groups(const mx_v16& c, int64_t& ga, int64_t& gb) {
     int32_t d[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) d[i] = c[i] + 2 * c[i + 8];
-    ga = (int64_t)d[0] + (int64_t)d[1] * 256 + (int64_t)d[2] * 65536 + (int64_t)d[3] * 16777216;
-    gb = (int64_t)d[4] + (int64_t)d[5] * 256 + (int64_t)d[6] * 65536 + (int64_t)d[7] * 16777216;
+    ga = mad_i64_i32(d[3], 16777216u, mad_i64_i32(d[2], 65536u, mad_i64_i32(d[1], 256u, (int64_t)d[0])));
+    gb = mad_i64_i32(d[7], 16777216u, mad_i64_i32(d[6], 65536u, mad_i64_i32(d[5], 256u, (int64_t)d[4])));
 }
 
 // Z = H0 + H1 2^32 + H2 2^64 + H3 2^96 mod p (|H| < 2^56), canonical. 2^128 == 2, 2^127 == 1 (mod p).
@@ -1474,7 +1488,8 @@ __device__ void dir_stage_dense(uint4* dig, uint32_t Bm, const layer_src& D, uin
         for (uint32_t v = 0; v < kV; ++v) {
             if (k0 + v * BS >= D.n) break;
             uint64_t dl, dh;
-            fp_digits8(fp_canon(lo[v], hi[v]), dl, dh);
+            // an image's weights are the previous step's folded sums, canonical already
+            fp_digits8(slab != kInf ? fp{lo[v], hi[v]} : fp_canon(lo[v], hi[v]), dl, dh);
             dig[c[v]] = make_uint4((uint32_t)dl, (uint32_t)(dl >> 32), (uint32_t)dh, (uint32_t)(dh >> 32));
         }
     };
@@ -1512,6 +1527,9 @@ __device__ __forceinline__ void dir_stage_sparse(uint4* prec, uint4* pinf, uint3
 }
 
 // one task's products, each row's P (half 0) / M (half 1) sum into stg[(r) 2 + h]
+#ifndef PVAC_DIR_PINF_REG   // A/B builds: 1 = the k-steps' sparse-edge offsets held in registers for every block
+#define PVAC_DIR_PINF_REG 0   // (177 instead of 187 VALU per block, but 21 spill ops: 428-429 K against 430-431 K)
+#endif
 template <int BS, int NKS>
 __device__ void dir_rows_n(const uint4* dig, const uint4* prec, const uint4* pinf, uint32_t Bm, ulonglong2* stg) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -1528,18 +1546,43 @@ __device__ void dir_rows_n(const uint4* dig, const uint4* prec, const uint4* pin
                             (int)__builtin_amdgcn_alignbyte(w3, w2, sh), (int)__builtin_amdgcn_alignbyte(w4, w3, sh)};
         }
     }
+#if PVAC_DIR_PINF_REG
+    // the k-steps' sparse-edge words, byte offsets into the digit table packed as
+    // (B - idx) 16 | (P table base) 16 << 16, held in registers for every block: the digit reads of a
+    // block depend on no LDS read of their own (the M table base is B 16 minus the P one)
+    uint32_t pk[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const uint4 in = pinf[2u * (uint32_t)s + h];
+        pk[s] = (in.x << 4) | (in.y << 20);
+    }
+    const uint32_t B16 = Bm << 4;
+#endif
     const uint32_t nblk = (Bm + 31u) >> 5;
     for (uint32_t blk = wave; blk < nblk; blk += BS / 64) {
         const uint32_t r = blk * 32u + n;
         const bool live = r < Bm;
         const uint32_t rr = live ? r : 0u;
         mx_v16 aP{}, aM{};
+#if PVAC_DIR_PINF_REG
+        const uint32_t rr16 = rr << 4;
+        const uint8_t* dg = (const uint8_t*)dig;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) asm volatile("" : "+v"(pk[s]));   // unpacked per block: 10 registers, not 20
+#endif
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
+#if PVAC_DIR_PINF_REG
+            uint32_t x = rr16 + (pk[s] & 0xFFFFu);   // 16 ((r - idx) mod B)
+            x = min(x, x - B16);
+            const uint4 dp = *(const uint4*)(dg + x + (pk[s] >> 16));
+            const uint4 dm = *(const uint4*)(dg + (x + B16) - (pk[s] >> 16));
+#else
             const uint4 in = pinf[2u * (uint32_t)s + h];
             uint32_t x = rr + in.x;   // (r - idx) mod B
             x = min(x, x - Bm);
             const uint4 dp = dig[in.y + x], dm = dig[in.z + x];
+#endif
             aP = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dp.x, (int)dp.y, (int)dp.z, (int)dp.w}, aP, 0, 0, 0);
             aM = __builtin_amdgcn_mfma_i32_32x32x32_i8(frag[s], mx_v4{(int)dm.x, (int)dm.y, (int)dm.z, (int)dm.w}, aM, 0, 0, 0);
         }
