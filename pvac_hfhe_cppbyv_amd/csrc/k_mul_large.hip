@@ -39,11 +39,11 @@
 #include <cstring>
 
 #ifdef PVAC_DIR_STAMPS   // diagnostic build only: k_large_products_direct's wave 0 s_memtime per phase
-__device__ unsigned long long g_dir_stamps[16];
+__device__ unsigned long long g_dir_stamps[24];
 extern "C" int pvac_hip_diag_dir_stamps(unsigned long long* host, int reset) {
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dir_stamps), sizeof(g_dir_stamps)) != hipSuccess) return -5;
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[24] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_dir_stamps), z, sizeof(z)) != hipSuccess) return -5;
     }
     return 0;
@@ -1636,7 +1636,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
     static_assert(BS <= 256, "dir_lds_base holds the writer's per-entry words for 256 entries");
     const uint32_t tid = threadIdx.x;
 #ifdef PVAC_DIR_STAMPS
-    unsigned long long st_acc[4] = {0, 0, 0, 0}, t_prev = dir_stamp();
+    unsigned long long st_acc[9] = {}, t_prev = dir_stamp();
 #endif
     uint4* dig = (uint4*)plds;
     uint8_t* sreg = plds + dir_lds_base(Bm);                           // per B layer: prec | pinf
@@ -1729,6 +1729,10 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
             // store is coalesced; otherwise each key's meta is stored where it is found.
             const bool ptab_ok = neB <= 2u;   // workgroup-uniform
             uint32_t* ptab = (uint32_t*)plds;   // [k][2B] position of cell c of staged B layer k
+            // lane j's B edge (the same for every entry): its idx, staged layer and position row
+            const uint32_t bjl = bjt[lane];
+            const uint32_t kbl = (bjl >> 12) & 15u, idxl = bjl & 0xFFFu;
+            uint32_t* const ptl = ptab + kbl * 2u * Bm;
             for (uint32_t b0 = 0; b0 < nw; b0 += BS) {   // workgroup-uniform
                 const uint32_t kq = b0 + tid;
                 const bool lv = kq < nw;
@@ -1738,6 +1742,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                 oidx[tid] = we >> 21;
                 omk[tid] = make_ulonglong2(mk.x & ~(1ull << 63), mk.y);
                 __syncthreads();
+                DSTAMP(4);
                 const uint32_t ne = min(nw - b0, (uint32_t)BS);
                 for (uint32_t l = wave; l < ne; l += BS / 64) {   // wave-uniform
                     const ulonglong2 m2 = omk[l];
@@ -1746,16 +1751,15 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                     const uint32_t above =
                         lane == 63u ? 0u : (uint32_t)__popcll(m2.x >> (lane + 1u)) + (uint32_t)__popcll(m2.y >> (lane + 1u));
                     const uint32_t pos = obase[l] + above;
-                    const uint32_t bj = bjt[lane];
-                    const uint32_t kb = (bj >> 12) & 15u;
-                    const uint32_t r = mod_small(oidx[l] + (bj & 0xFFFu), Bm);
-                    const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
-                    const uint32_t sbase = (lidk - nbase) * 2u * Bm;   // < 2^21 (k_large_scan_direct)
+                    const uint32_t r = mod_small(oidx[l] + idxl, Bm);
                     if (ptab_ok) {
-                        if (hp) ptab[kb * 2u * Bm + r] = pos;
-                        if (hm) ptab[kb * 2u * Bm + Bm + r] = pos + hp;
+                        if (hp) ptl[r] = pos;
+                        if (hm) ptl[Bm + r] = pos + hp;
                         continue;
                     }
+                    const uint32_t kb = kbl;
+                    const uint32_t lidk = kb == 0 ? lid[0] : kb == 1 ? lid[1] : kb == 2 ? lid[2] : lid[3];
+                    const uint32_t sbase = (lidk - nbase) * 2u * Bm;   // < 2^21 (k_large_scan_direct)
                     if (hp) {
                         const ulonglong2 w = stg[(kb * Bm + r) * 2u];
                         if ((w.x | w.y) == 0ull) cnt[kCntRedo] = 1u;   // a present cell whose products cancel
@@ -1771,6 +1775,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                 if (b0 + BS < nw) __syncthreads();   // the next round rewrites obase / oidx / omk
             }
             if (ptab_ok) __syncthreads();   // every position in the table
+            DSTAMP(5);
 #pragma unroll
             for (uint32_t k = 0; k < kLaMaxLB; ++k) {   // the weights of every cell, coalesced
                 if (k >= neB) break;
@@ -1788,6 +1793,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                     __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.y, (uint32_t)(w.y >> 32)}, rhi, bo, 0, PVAC_DIR_STORE_AUX);
                 }
             }
+            DSTAMP(8);
         }
         for (uint32_t b0 = 0; b0 < nw && !cimg; b0 += BS) {   // workgroup-uniform
             const uint32_t kq = b0 + tid;
@@ -1804,6 +1810,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
             oexc[tid] = excl;
             omk[tid] = make_ulonglong2(mp, mm);
             __syncthreads();
+            DSTAMP(6);
             // key expansion, one wave per entry and one lane per B edge j: the range's keys in emit
             // order (j DESC, P before M at one j), so key (j, P) sits at the keys above j
             const uint32_t ne = min(nw - b0, (uint32_t)BS);
@@ -1817,6 +1824,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
                 if (hm) okey[x0 + above + hp] = (uint16_t)(lane | 64u | l << 7);
             }
             __syncthreads();
+            DSTAMP(7);
             for (uint32_t q = tid; q < T; q += BS) {
                 const uint32_t v = okey[q];
                 const uint32_t l = v >> 7, jj = v & 63u, ch = (v >> 6) & 1u;
@@ -1846,6 +1854,7 @@ __global__ __launch_bounds__(BS, PVAC_LA_MINB) void k_large_products_direct(mul_
 #ifdef PVAC_DIR_STAMPS
     if (tid == 0) {
         for (int p = 0; p < 4; ++p) atomicAdd(&g_dir_stamps[p], st_acc[p]);
+        for (int p = 4; p < 9; ++p) atomicAdd(&g_dir_stamps[12 + p], st_acc[p]);   // writer parts: [16, 21)
         atomicAdd(&g_dir_stamps[4], (unsigned long long)(i1 - i0));
         atomicAdd(&g_dir_stamps[5], 1ull);
     }

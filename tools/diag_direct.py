@@ -29,17 +29,22 @@ def main():
     X, st = eng.enc_value(vals, rnd)
     eng.ct_mul_chain(X, 8, streams=1, chunk=1024)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     lib.pvac_hip_diag_dir_stamps(buf, 1)
     eng.ct_mul_chain(X, 8, streams=1, chunk=1024)
     torch.cuda.synchronize()
     assert lib.pvac_hip_diag_dir_stamps(buf, 1) == 0
     v = list(buf)
-    tot = sum(v[:4])
+    tot = sum(v[:4]) + sum(v[16:21])
     names = ["setup", "stage_dense", "mfma_rows", "writer"]
     out = {"a_layers": v[4], "workgroups": v[5], "cycles_total": tot}
     for i, nm in enumerate(names):
         out[nm] = {"frac": round(v[i] / max(tot, 1), 4), "cycles_per_a_layer": round(v[i] / max(v[4], 1))}
+    # the writer's parts (phase 3 above is the record writer's output loop plus the layer's last wait):
+    # image steps (intermediate): entries + offsets, key expansion into the LDS position table, the
+    # coalesced cell pass; record steps (final): entries + offsets + scan, key expansion
+    for i, nm in enumerate(["img_entries", "img_expand", "rec_entries", "rec_expand", "img_cells"]):
+        out["writer_" + nm] = {"frac": round(v[16 + i] / max(tot, 1), 4), "cycles_per_a_layer": round(v[16 + i] / max(v[4], 1))}
     tc = sum(v[8:12])
     out["count_la"] = {"a_layers": v[12], "cycles_total": tc, "list_entries_per_a_layer": round(v[13] / max(v[12], 1), 1)}
     for i, nm in enumerate(["setup", "stage_tt", "keys", "iblk_list"]):
