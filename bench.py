@@ -50,9 +50,10 @@ def parse():
                     help="cfg 4: chains (first inputs of the first chunk) whose final outputs are digest-compared "
                          "with the pinned CPU port, which is also timed on them (cpu_baseline)")
     ap.add_argument("--chain-ref", type=int, default=2, help="cfg 4: reference chains (oracle/_ref) timed, depth 4")
-    ap.add_argument("--chain-streams", type=int, default=4,
+    ap.add_argument("--chain-streams", type=int, default=6,
                     help="cfg 4: worker streams of the engine's chain call (pvac_hip_ct_mul_chain): one chunk's "
-                         "host planning and dependent launches overlap the other chunks' kernels")
+                         "host planning and dependent launches overlap the other chunks' kernels (6: +1.5%% over 4, "
+                         "profiles/r05/rows/chain_streams2.log)")
     ap.add_argument("--chain-no-check", action="store_true",
                     help="cfg 4: skip the checked second pass and the CPU sample (kernel-trace profiling)")
     ap.add_argument("--chain-compare-streams", action="store_true",
@@ -917,7 +918,7 @@ def chain_bench(eng, args):
     # worker, S x chunk inputs: a sum digest reads the whole c_depth, ~1.4 ms of HBM per 1024 depth-8
     # chains, so all of them would add ~6% to the chain's kernel time; the serial FNV-1a digests come
     # from the check pass, which must reproduce every count and these sum digests)
-    n_sd = min(n, S * chunk)
+    n_sd = min(n, 4 * chunk)   # a fixed prefix: the timed pass digests 4 chunks whatever the stream count
     r = eng.ct_mul_chain(X_all, depth, nonce_seed=seed, streams=S, chunk=chunk, count_n=n, sumdigest=n_sd)
     torch.cuda.synchronize(dev)
     chain_s = time.perf_counter() - t1
