@@ -350,7 +350,7 @@ struct mul_large_args {
 };
 // k_large_products_la: A layers per workgroup (default; PVAC_LA_PER_WG); pairs with at most
 // kLaMaxLB B layers take it
-constexpr uint32_t kLaPerWG = 4;
+constexpr uint32_t kLaPerWG = 8;
 constexpr uint32_t kLaMaxLB = 4;
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
 // dense chain images back to hash-order records for the listed pairs whose flag is set (the flag is
