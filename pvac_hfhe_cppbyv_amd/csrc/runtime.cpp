@@ -155,6 +155,7 @@ struct pvac_hip_ctx {
     uint64_t* chain_out = nullptr;           // digests / counts of a chunk before the copy to X's device
     size_t chain_out_cap = 0;
     unsigned long long* chain_stats = nullptr;   // [2 * PVAC_CHAIN_MAX_DEPTH + 1]: edges / products, image pair-steps
+    uint64_t chain_layout[3] = {0, 0, 0};       // the last call's (streams, devices, chunk)
     uint64_t H_gen = 0;                      // bumped whenever H is set (a worker's copy follows it)
     uint64_t H_from = 0;                     // worker: the parent's H_gen its H copy was taken from
 };
@@ -447,6 +448,16 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
     return PVAC_OK;
 }
 
+// a chain worker's output batches (stream-ordered frees on its stream; the caller synchronises)
+static void free_chain_sets(pvac_hip_ctx* c) {
+    for (chain_set* b : {&c->chain_bufs[0], &c->chain_bufs[1], &c->chain_stage}) {
+        for (void* q : {(void*)b->l_off, (void*)b->l_cnt, (void*)b->e_off, (void*)b->e_cnt, (void*)b->layers,
+                        (void*)b->meta, (void*)b->w_lo, (void*)b->w_hi, (void*)b->sigma, (void*)b->img})
+            if (q) hipFreeAsync(q, c->stream);
+        *b = chain_set{};
+    }
+}
+
 int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     if (!c) return PVAC_OK;
     hipSetDevice(c->device);
@@ -454,10 +465,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     c->chain_kids.clear();
     if (c->stream) hipStreamSynchronize(c->stream);
     flush_timers(c);
-    for (chain_set* b : {&c->chain_bufs[0], &c->chain_bufs[1], &c->chain_stage})
-        for (void* q : {(void*)b->l_off, (void*)b->l_cnt, (void*)b->e_off, (void*)b->e_cnt, (void*)b->layers,
-                        (void*)b->meta, (void*)b->w_lo, (void*)b->w_hi, (void*)b->sigma, (void*)b->img})
-            if (q) hipFreeAsync(q, c->stream);
+    free_chain_sets(c);
     for (void* q : {(void*)c->chain_nonces, (void*)c->chain_salts, (void*)c->chain_out})
         if (q) hipFreeAsync(q, c->stream);
     if (c->stream) hipStreamSynchronize(c->stream);
@@ -1963,6 +1971,26 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
     // inputs already enqueued on the caller's stream must be complete before other streams read them
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain (caller stream)");
+    // a layout change (streams, devices, chunk) first returns the workers' grown buffers and scratch
+    // arenas, so the HBM shares below are taken over the device's memory, not over what the previous
+    // layout's workers left free
+    const uint64_t layout[3] = {S, D, chunk};
+    if (!c->chain_kids.empty() && !std::equal(layout, layout + 3, c->chain_layout)) {
+        for (pvac_hip_ctx* k : c->chain_kids) {
+            hipSetDevice(k->device);
+            free_chain_sets(k);
+            e = hipStreamSynchronize(k->stream);
+            if (e != hipSuccess) {
+                hipSetDevice(c->device);
+                return hip_fail(c, e, "ct_mul_chain: worker release");
+            }
+            hipFree(k->arena);
+            k->arena = nullptr;
+            k->arena_words = 0;
+        }
+        hipSetDevice(c->device);
+    }
+    std::copy(layout, layout + 3, c->chain_layout);
     // worker contexts: [range j * S + w] on devs[j]; a layout change rebuilds the ones that differ
     if (c->chain_kids.size() > (size_t)D * S) {
         for (size_t w = (size_t)D * S; w < c->chain_kids.size(); ++w) pvac_hip_ctx_destroy(c->chain_kids[w]);

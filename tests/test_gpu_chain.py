@@ -236,6 +236,30 @@ def test_chain_two_device_ranges_equal_one_device():
     assert list(f) == [0, 10, 25, 37]   # 8 chunks dealt 2 / 3 / 3
 
 
+def test_chain_layout_changes_release_worker_memory():
+    """Calls with different (streams, chunk) layouts on one context: a layout change returns the
+    workers' grown output buffers and scratch arenas before the new HBM shares are taken (without it
+    a larger-chunk call followed by more streams ran out of memory on the 2^16-input bench shape).
+    Every layout gives the same digests and counts; the device's free memory after a small-chunk call
+    is not below what it was after the large-chunk call."""
+    import torch
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0xD0D5)
+    n, depth = 41, 4
+    X = eng.gen_fresh(n, 0xD0D6, 20)
+    base = eng.ct_mul_chain(X, depth, streams=2, chunk=5, digest_n=n, nonce_seed=0xD0D7)
+    big = eng.ct_mul_chain(X, depth, streams=1, chunk=41, digest_n=n, nonce_seed=0xD0D7)
+    torch.cuda.synchronize()
+    free_big = torch.cuda.mem_get_info()[0]
+    for streams, chunk in ((3, 2), (4, 7), (2, 5)):
+        r = eng.ct_mul_chain(X, depth, streams=streams, chunk=chunk, digest_n=n, nonce_seed=0xD0D7)
+        assert np.array_equal(base["digests"], r["digests"]) and np.array_equal(base["counts"], r["counts"])
+        assert r["chunks"] == (n + chunk - 1) // chunk
+    assert np.array_equal(base["digests"], big["digests"])
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info()[0] + (64 << 20) >= free_big
+
+
 def test_chain_final_step_sigma_vs_oracle(oracle, manifest, H_dense):
     """PVAC_MUL_WITH_SIGMA on the chain entry point: the final step's edges get sigma_from_H with
     the salts the salts_at hook writes (hash-order position per edge), intermediate steps stay

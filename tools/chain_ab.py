@@ -1,6 +1,6 @@
 """cfg-4 chain A/B (GPU box): the chain call (pvac_hip_ct_mul_chain) on the same GPU enc_value inputs through
 each library given, alternating, with 1 and with 4 worker streams; final digests must agree between
-libraries. Usage: python tools/chain_ab.py [--inputs N] [--streams 1,4] lib1.so [lib2.so ...]"""
+libraries. Usage: python tools/chain_ab.py [--inputs N] [--streams 1,4] [--chunks 1024] lib1.so [lib2.so ...]"""
 import json
 import os
 import sys
@@ -19,9 +19,12 @@ def main():
     argv = sys.argv[1:]
     n = 16384
     streams = (1, 4)
-    while argv and argv[0] in ("--inputs", "--streams"):
+    chunks = (1024,)
+    while argv and argv[0] in ("--inputs", "--streams", "--chunks"):
         if argv[0] == "--inputs":
             n = int(argv[1])
+        elif argv[0] == "--chunks":
+            chunks = tuple(int(x) for x in argv[1].split(","))
         else:
             streams = tuple(int(x) for x in argv[1].split(","))
         argv = argv[2:]
@@ -37,14 +40,14 @@ def main():
         X, st = eng.enc_value(vals, rnd)
         del rnd
         name = os.path.basename(path)
-        for s in streams:
-            eng.ct_mul_chain(X, 8, streams=s, chunk=1024)   # warm: arenas, buffers
+        for s, c in [(s, c) for s in streams for c in chunks]:
+            eng.ct_mul_chain(X, 8, streams=s, chunk=c)   # warm: arenas, buffers
             torch.cuda.synchronize()
             t = time.perf_counter()
-            r = eng.ct_mul_chain(X, 8, streams=s, chunk=1024, digest_n=64)
+            r = eng.ct_mul_chain(X, 8, streams=s, chunk=c, digest_n=64)
             torch.cuda.synchronize()
             el = time.perf_counter() - t
-            k = f"{name}:s{s}"
+            k = f"{name}:s{s}" + (f":c{c}" if len(chunks) > 1 else "")
             res[k] = round(n * 8 / el)
             same = ref is None or bool(np.array_equal(ref, r["digests"]))
             if ref is None:
