@@ -388,10 +388,9 @@ class Engine:
     # ---- ciphertext ops
     def ct_mul_plan(self, A: DeviceBatch, B: DeviceBatch):
         torch = self.torch
-        C_ = DeviceBatch(A.n, torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device),
-                         torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device), None,
-                         torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device),
-                         torch.zeros(max(A.n, 1), dtype=torch.int64, device=self.device), None, None, None)
+        m = max(A.n, 1)
+        cnt = torch.zeros(4 * m, dtype=torch.int64, device=self.device)   # l_off, l_cnt, e_off, e_cnt: one fill
+        C_ = DeviceBatch(A.n, cnt[:m], cnt[m:2 * m], None, cnt[2 * m:3 * m], cnt[3 * m:], None, None, None)
         plan = Plan()
         sa, sb, sc = A.struct(), B.struct(), C_.struct()
         self._check(self.lib.pvac_hip_ct_mul_plan(self.ctx, C.byref(sa), C.byref(sb), C.byref(sc), C.byref(plan)))

@@ -99,7 +99,7 @@ __device__ __forceinline__ uint64_t fmod64(uint64_t x, const fastmod64& f) {
 
 // plan statistics written by the plan kernels (device, zeroed before launch)
 struct plan_stats {
-    unsigned long long total_layers, total_edges;
+    unsigned long long total_layers, total_edges;   // the plan scans' totals (pvac_hip_ctx::totals)
     unsigned long long n_small, n_large, n_invalid;
     unsigned int max_keys, max_prod, max_na, max_nb, max_buckets, max_layers;
 };

@@ -127,7 +127,7 @@ struct pvac_hip_ctx {
     size_t scan_cap = 0;
     plan_stats* stats = nullptr;
     unsigned int* check_buf = nullptr;   // gsum check: 4 layer maxima, then a u64 failure count
-    unsigned long long* totals = nullptr;   // [2]
+    unsigned long long* totals = nullptr;   // [2]: &stats->total_layers (layer and edge slot totals)
     sigma_tables H;
     // timing
     bool timing = false;
@@ -442,7 +442,8 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
     if (e == hipSuccess) e = hipMalloc(&c->nb_magic, mg.size() * 8);
     if (e == hipSuccess) e = hipMemcpy(c->nb_magic, mg.data(), mg.size() * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(plan_stats));
-    if (e == hipSuccess) e = hipMalloc(&c->totals, 2 * sizeof(unsigned long long));
+    // the scans' two totals are plan_stats' first words: a plan reads stats and totals back in one copy
+    if (e == hipSuccess) c->totals = &c->stats->total_layers;
     if (e != hipSuccess) { pvac_hip_ctx_destroy(c); return PVAC_ENOMEM; }
     *out = c;
     return PVAC_OK;
@@ -500,7 +501,6 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->scan_scratch);
     hipFree(c->stats);
     hipFree(c->check_buf);
-    hipFree(c->totals);
     sigma_tables_free(c->H);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -712,10 +712,9 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->l_off, A->n, c->scan_scratch, &c->totals[0], c->stream);
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->e_off, A->n, c->scan_scratch, &c->totals[1], c->stream);
     plan_stats st{};
-    unsigned long long tot[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpyAsync(&st, c->stats, sizeof st, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(tot, c->totals, sizeof tot, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    const unsigned long long tot[2] = {st.total_layers, st.total_edges};
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_plan");
     plan->total_layer_slots = tot[0];
     plan->total_edge_slots = tot[1];
@@ -1113,10 +1112,9 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->l_off, A->n, c->scan_scratch, &c->totals[0], c->stream);
     if (e == hipSuccess) e = launch_exclusive_scan_u64(C->e_off, A->n, c->scan_scratch, &c->totals[1], c->stream);
     plan_stats st{};
-    unsigned long long tot[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpyAsync(&st, c->stats, sizeof st, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(tot, c->totals, sizeof tot, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    const unsigned long long tot[2] = {st.total_layers, st.total_edges};
     if (e != hipSuccess) return hip_fail(c, e, "ct_add_plan");
     plan->total_layer_slots = tot[0];
     plan->total_edge_slots = tot[1];
