@@ -335,11 +335,11 @@ def _enc_inputs(eng, n, seed):
     return X, man
 
 
-def _oracle_chain(oracle, X, n, depth, canon_tag, edge_budget=1200000):
+def _oracle_chain(oracle, X, n, depth, canon_tag, edge_budget=1200000, B=337):
     px = pack_device_batch(X, n)
     P_ = lambda a: a.ctypes.data_as(C.c_void_p)
     ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
-    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(canon_tag, edge_budget=edge_budget)), n,
+    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(canon_tag, edge_budget=edge_budget, B=B)), n,
                                       *(P_(a) for a in px), depth, 8, P_(ocnt), P_(odig), P_(se))
     return ocnt, odig
 
@@ -392,3 +392,34 @@ def test_chain_image_inputs_redone_on_records(oracle):
     assert np.array_equal(img["digests"], rec["digests"]) and np.array_equal(img["counts"], rec["counts"])
     ocnt, odig = _oracle_chain(oracle, X, n, depth, man["canon_tag"], edge_budget=30000)
     assert np.array_equal(ocnt, img["counts"]) and np.array_equal(odig, img["digests"])
+
+
+def test_chain_images_with_four_b_layers(oracle):
+    """Inputs with four edge layers (ct_add of two fresh batches, 15 edges per layer: 60 <= 63 B edges,
+    the direct mode's per-A-edge masks) and B = 131 (262 cells per product layer, so the product
+    layers fill after two steps): every chain step multiplies by four B layers, so the image writer
+    takes its scattered-store path (more than two B layers), and the intermediate steps whose product
+    layers are all filled hand C on as dense images. Final digests and counts equal the record-only
+    run (after_step hook), the step-by-step engine run and the CPU port's chain."""
+    from pvac_hfhe_cppbyv_amd import STEP_CB, Engine
+    tag, Bm = 0xF0A4, 131
+    eng = Engine(device=0, canon_tag=tag, B=Bm)
+    n, depth, chunk, seed = 3, 4, 2, 0xF0A5
+    X = eng.ct_add(eng.gen_fresh(n, 0xF0A6, 15), eng.gen_fresh(n, 0xF0A7, 15))
+    assert X.l_cnt[:n].cpu().tolist() == [4] * n and X.e_cnt[:n].cpu().tolist() == [60] * n
+    img = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=2, chunk=chunk, digest_n=n)
+
+    def after(user, step, first, A, Xb, Cb, words, nw, stream):
+        return 0
+
+    rec = eng.ct_mul_chain(X, depth, nonce_seed=seed, streams=2, chunk=chunk, digest_n=n, after_step=STEP_CB(after))
+    assert img["redo"] == 0 and rec["redo"] == 0
+    # step 3's C (256 product layers x 262 cells) is full: one image per chain; step 2's is not
+    assert img["image_steps"] == n and rec["image_steps"] == 0
+    assert img["edges"][2] == n * 256 * 2 * Bm
+    assert np.array_equal(img["digests"], rec["digests"]) and np.array_equal(img["counts"], rec["counts"])
+    assert img["edges"] == rec["edges"]
+    dig, cnt, edges = _stepwise(eng, X, depth, seed, chunk)
+    assert np.array_equal(img["digests"], dig) and np.array_equal(img["counts"], cnt) and img["edges"] == edges
+    ocnt, odig = _oracle_chain(oracle, X, n, depth, tag, B=Bm)
+    assert np.array_equal(ocnt, cnt) and np.array_equal(odig, dig)
