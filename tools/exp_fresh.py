@@ -34,6 +34,8 @@ def main():
         eng.timing(False)
         ms, k = eng.timing_get("ct_mul_fresh")
         res[os.path.basename(path)] = round(ms / max(k, 1), 3)
+        lms, lk = eng.timing_get("mul_layers_fresh")
+        res[os.path.basename(path) + ":layers_ms"] = round(lms / max(lk, 1), 4)
         # outputs vs the first library's (the product): a variant must be bit-exact
         out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
         dig = eng.digest(out).cpu()
@@ -42,7 +44,8 @@ def main():
         same = bool(torch.equal(dig, ref))
         res[os.path.basename(path) + ":same_as_first"] = same
         res[os.path.basename(path) + ":redo"] = eng.ct_mul_redo_count()
-        print(os.path.basename(path), res[os.path.basename(path)], "same" if same else "DIFFERENT", flush=True)
+        print(os.path.basename(path), res[os.path.basename(path)], "layers", res[os.path.basename(path) + ":layers_ms"],
+              "same" if same else "DIFFERENT", flush=True)
         del out, dig
         del A, B, Cb, plan, nonces, eng
         torch.cuda.empty_cache()
