@@ -2,6 +2,8 @@
 //
 // ct_mul itself lives in k_mul_fresh.hip (LDS-resident fresh-shape pairs) and
 // k_mul_large.hip (general pairs: chains, squares, dense layers).
+#include <cstddef>
+
 #include "common.hpp"
 
 namespace pvhip {
@@ -53,10 +55,14 @@ __device__ __forceinline__ void max_if_greater(unsigned int* p, uint32_t v) {
     if (v > __atomic_load_n(p, __ATOMIC_RELAXED)) atomicMax(p, v);
 }
 
+// one pair per thread up to 2^20 pairs (a second grid-stride round only beyond): the loop's loads
+// are not overlapped across rounds
 inline unsigned plan_grid(uint64_t n) {
     const uint64_t b = (n + kPlanBlock - 1) / kPlanBlock;
-    return (unsigned)(b < 2048 ? b : 2048);
+    return (unsigned)(b < 4096 ? b : 4096);
 }
+static_assert(offsetof(plan_stats, max_layers) == offsetof(plan_stats, max_keys) + 5 * sizeof(unsigned int),
+              "k_plan_mul updates the six maxima as consecutive words");
 
 // Classifies every pair (fresh-shape kernel or general path), writes per-pair output
 // capacities (scanned in place afterwards) and the launch maxima of the fresh kernel.
@@ -90,14 +96,14 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
     uint32_t v[6] = {mk, mp, ma, mb, mbk, ml};
     const bool is_sum[6] = {false, false, false, false, false, false};
     block_reduce_stats<6>(v, is_sum, red);
-    if (threadIdx.x == 0) {
-        max_if_greater(&stats->max_keys, v[0]);
-        max_if_greater(&stats->max_prod, v[1]);
-        max_if_greater(&stats->max_na, v[2]);
-        max_if_greater(&stats->max_nb, v[3]);
-        max_if_greater(&stats->max_buckets, v[4]);
-        max_if_greater(&stats->max_layers, v[5]);
-    }
+    // the six maxima (consecutive plan_stats fields) by six lanes at once: one read and at most one
+    // atomic round trip at the block's end instead of six of each in sequence
+    __syncthreads();   // red[] was read by thread 0 inside block_reduce_stats
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int f = 0; f < 6; ++f) red[f] = v[f];
+    __syncthreads();
+    if (threadIdx.x < 6) max_if_greater(&stats->max_keys + threadIdx.x, red[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(kPlanBlock) void k_plan_add(pvac_ct_batch A, pvac_ct_batch B, pvac_ct_batch C,
