@@ -116,8 +116,11 @@ hipError_t launch_plan_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_
                            uint8_t* pair_class, uint64_t* merge_ids, uint64_t edge_budget, hipStream_t st);
 hipError_t launch_gather_merge(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C,
                                const uint64_t* ids, uint64_t n, uint64_t* out, hipStream_t st);
-// in-place exclusive scan of n u64 values; scratch >= scan_scratch_words(n) u64
+// in-place exclusive scan of n u64 values (or of two arrays of n values at once: one launch per
+// scan kernel); scratch >= scan_scratch_words(n) u64
 size_t scan_scratch_words(size_t n);
+hipError_t launch_exclusive_scan2_u64(uint64_t* d0, uint64_t* d1, size_t n, uint64_t* scratch,
+                                      unsigned long long* total0, unsigned long long* total1, hipStream_t st);
 hipError_t launch_exclusive_scan_u64(uint64_t* data, size_t n, uint64_t* scratch, unsigned long long* total_out,
                                      hipStream_t st);
 

@@ -185,8 +185,18 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* part, u
     return base + x - v;
 }
 
-__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint64_t* data, size_t n, uint64_t* tile_sums) {
+// The scan kernels take up to two arrays of n values (blockIdx.y picks one, its tile sums at
+// tile_sums + y * stride): a plan's two capacity arrays are scanned by one launch of each kernel.
+struct scan_arrays {
+    uint64_t* data[2];
+    unsigned long long* total[2];
+    size_t stride;   // tile-sum words per array
+};
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(scan_arrays a, size_t n, uint64_t* tile_sums) {
     __shared__ uint64_t part[kScanBlock / 64];
+    const uint64_t* data = a.data[blockIdx.y];
+    tile_sums += blockIdx.y * a.stride;
     const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanPer;
     uint64_t s = 0;
 #pragma unroll
@@ -198,9 +208,10 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint64_t* data
 }
 
 // single workgroup: exclusive scan of tile sums (any count), writes grand total
-__global__ __launch_bounds__(kScanBlock) void k_scan_tiles(uint64_t* tile_sums, size_t ntiles,
-                                                          unsigned long long* total_out) {
+__global__ __launch_bounds__(kScanBlock) void k_scan_tiles(scan_arrays a, uint64_t* tile_sums, size_t ntiles) {
     __shared__ uint64_t part[kScanBlock / 64];
+    tile_sums += blockIdx.x * a.stride;
+    unsigned long long* total_out = a.total[blockIdx.x];
     uint64_t carry = 0;
     for (size_t b = 0; b < ntiles; b += kScanBlock) {
         const size_t i = b + threadIdx.x;
@@ -213,8 +224,10 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_tiles(uint64_t* tile_sums, 
     if (threadIdx.x == 0 && total_out) *total_out = carry;
 }
 
-__global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* data, size_t n, const uint64_t* tile_offs) {
+__global__ __launch_bounds__(kScanBlock) void k_scan_apply(scan_arrays a, size_t n, const uint64_t* tile_offs) {
     __shared__ uint64_t part[kScanBlock / 64];
+    uint64_t* data = a.data[blockIdx.y];
+    tile_offs += blockIdx.y * a.stride;
     const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanPer;
     uint64_t v[kScanPer];
     uint64_t s = 0;
@@ -519,16 +532,29 @@ hipError_t launch_gather_merge(const pvac_ct_batch& A, const pvac_ct_batch& B, c
     return hipGetLastError();
 }
 
-size_t scan_scratch_words(size_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+size_t scan_scratch_words(size_t n) { return 2 * ((n + kScanTile - 1) / kScanTile + 1); }
+
+namespace {
+hipError_t launch_scans(const scan_arrays& a, unsigned arrays, size_t n, uint64_t* scratch, hipStream_t st) {
+    if (!n) return hipSuccess;
+    const size_t tiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)tiles, arrays), dim3(kScanBlock), 0, st, a, n, scratch);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(arrays), dim3(kScanBlock), 0, st, a, scratch, tiles);
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)tiles, arrays), dim3(kScanBlock), 0, st, a, n, scratch);
+    return hipGetLastError();
+}
+}  // namespace
 
 hipError_t launch_exclusive_scan_u64(uint64_t* data, size_t n, uint64_t* scratch, unsigned long long* total_out,
                                      hipStream_t st) {
-    if (!n) return hipSuccess;
-    const size_t tiles = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)tiles), dim3(kScanBlock), 0, st, data, n, scratch);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanBlock), 0, st, scratch, tiles, total_out);
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)tiles), dim3(kScanBlock), 0, st, data, n, scratch);
-    return hipGetLastError();
+    const scan_arrays a{{data, data}, {total_out, total_out}, (n + kScanTile - 1) / kScanTile + 1};
+    return launch_scans(a, 1, n, scratch, st);
+}
+
+hipError_t launch_exclusive_scan2_u64(uint64_t* d0, uint64_t* d1, size_t n, uint64_t* scratch,
+                                      unsigned long long* total0, unsigned long long* total1, hipStream_t st) {
+    const scan_arrays a{{d0, d1}, {total0, total1}, (n + kScanTile - 1) / kScanTile + 1};
+    return launch_scans(a, 2, n, scratch, st);
 }
 
 hipError_t launch_ct_add(const pvac_ct_batch& A, const pvac_ct_batch& B, pvac_ct_batch& C, int negate_b,

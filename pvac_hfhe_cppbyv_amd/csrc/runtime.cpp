@@ -709,8 +709,8 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (e == hipSuccess)
         e = launch_plan_mul(*A, *B, *C, c->pair_class, c->large_ids, c->stats, c->nb_table, kNbTableLen, c->prm.B,
                             c->stream);
-    if (e == hipSuccess) e = launch_exclusive_scan_u64(C->l_off, A->n, c->scan_scratch, &c->totals[0], c->stream);
-    if (e == hipSuccess) e = launch_exclusive_scan_u64(C->e_off, A->n, c->scan_scratch, &c->totals[1], c->stream);
+    if (e == hipSuccess)
+        e = launch_exclusive_scan2_u64(C->l_off, C->e_off, A->n, c->scan_scratch, &c->totals[0], &c->totals[1], c->stream);
     plan_stats st{};
     if (e == hipSuccess) e = hipMemcpyAsync(&st, c->stats, sizeof st, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1109,8 +1109,8 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     hipError_t e = hipMemsetAsync(c->stats, 0, sizeof(plan_stats), c->stream);
     if (e == hipSuccess)
         e = launch_plan_add(*A, *B, *C, c->stats, c->pair_class, c->large_ids, c->prm.edge_budget, c->stream);
-    if (e == hipSuccess) e = launch_exclusive_scan_u64(C->l_off, A->n, c->scan_scratch, &c->totals[0], c->stream);
-    if (e == hipSuccess) e = launch_exclusive_scan_u64(C->e_off, A->n, c->scan_scratch, &c->totals[1], c->stream);
+    if (e == hipSuccess)
+        e = launch_exclusive_scan2_u64(C->l_off, C->e_off, A->n, c->scan_scratch, &c->totals[0], &c->totals[1], c->stream);
     plan_stats st{};
     if (e == hipSuccess) e = hipMemcpyAsync(&st, c->stats, sizeof st, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
