@@ -169,8 +169,8 @@ int pvac_hip_fp_binop(pvac_hip_ctx* ctx, int op, const uint64_t* a_lo, const uin
  * ct_mul (ops/arithmetic.hpp:47-106) over n independent pairs C[i] = A[i] * B[i].
  * Two-phase sizing:
  *   1. pvac_hip_ct_mul_plan: writes C->l_off / C->e_off (device) with per-pair capacities
- *      (layers |A.L|+|B.L|+|A.L||B.L|, edges 2*min(|A.E||B.E|, |A.L||B.L|B)) and fills *plan
- *      (synchronises the stream once to read totals back).
+ *      (layers |A.L|+|B.L|+|A.L||B.L|, edges 2*min(|A.E||B.E|, |A.L||B.L|B)), zeroes C->l_cnt /
+ *      C->e_cnt when given, and fills *plan (synchronises the stream once to read totals back).
  *   2. caller allocates C->layers (total_layer_slots), C->meta/w_lo/w_hi (total_edge_slots),
  *      optional C->sigma, then pvac_hip_ct_mul_exec writes C->l_cnt/e_cnt and the records.
  * Randomness (replaces the getrandom draws of arithmetic.hpp:59-70,90-94):

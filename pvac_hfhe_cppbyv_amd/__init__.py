@@ -389,7 +389,8 @@ class Engine:
     def ct_mul_plan(self, A: DeviceBatch, B: DeviceBatch):
         torch = self.torch
         m = max(A.n, 1)
-        cnt = torch.zeros(4 * m, dtype=torch.int64, device=self.device)   # l_off, l_cnt, e_off, e_cnt: one fill
+        # l_off, l_cnt, e_off, e_cnt: the plan kernel writes all four (capacities, zero counts)
+        cnt = torch.empty(4 * m, dtype=torch.int64, device=self.device)
         C_ = DeviceBatch(A.n, cnt[:m], cnt[m:2 * m], None, cnt[2 * m:3 * m], cnt[3 * m:], None, None, None)
         plan = Plan()
         sa, sb, sc = A.struct(), B.struct(), C_.struct()

@@ -80,6 +80,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_mul(pvac_ct_batch A, pvac_c
         const uint64_t capE = 2 * (prod < keys ? prod : keys);
         C.l_off[i] = capL;   // scanned in place afterwards
         C.e_off[i] = capE;
+        if (C.l_cnt) C.l_cnt[i] = 0;   // exec's counts start from zero (no separate fill by the caller)
+        if (C.e_cnt) C.e_cnt[i] = 0;
         const bool sm = keys <= kFreshKeysMax && prod <= kFreshProdMax && prod < nb_len && nA <= kFreshEdgesMax &&
                         nB <= kFreshEdgesMax && capL <= kFreshLayersMax &&
                         nb_table[prod < nb_len ? prod : 0] + prod + 3 <= 3 * keys;   // chains + key sums fit in LDS
