@@ -128,6 +128,7 @@ struct pvac_hip_ctx {
     plan_stats* stats = nullptr;
     unsigned int* check_buf = nullptr;   // gsum check: 4 layer maxima, then a u64 failure count
     unsigned long long* totals = nullptr;   // [2]: &stats->total_layers (layer and edge slot totals)
+    void* pin = nullptr;                    // pinned host words for the plan's and exec's read-backs
     sigma_tables H;
     // timing
     bool timing = false;
@@ -213,6 +214,35 @@ void flush_timers(pvac_hip_ctx* c) {
         }
         kv.second.pending.clear();
     }
+}
+
+#ifndef PVAC_FAST_READBACK   // A/B builds only: pinned read-back words and a spinning wait for them
+#define PVAC_FAST_READBACK 1
+#endif
+// The short host waits of a plan (its totals) and of exec (the redo count): a blocking
+// hipStreamSynchronize wakes tens of microseconds after the copy lands, so spin on hipStreamQuery
+// (up to 50 ms, then block) and read into pinned words (a pageable destination stages the copy).
+hipError_t read_back(pvac_hip_ctx* c, void* dst, const void* src, size_t bytes) {
+#if PVAC_FAST_READBACK
+    if (c->pin && bytes <= 256) {
+        hipError_t e = hipMemcpyAsync(c->pin, src, bytes, hipMemcpyDeviceToHost, c->stream);
+        if (e != hipSuccess) return e;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            e = hipStreamQuery(c->stream);
+            if (e != hipErrorNotReady) break;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+                e = hipStreamSynchronize(c->stream);
+                break;
+            }
+        }
+        if (e == hipSuccess) std::memcpy(dst, c->pin, bytes);
+        return e;
+    }
+#endif
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e;
 }
 
 int ensure_pairs(pvac_hip_ctx* c, size_t n) {
@@ -444,6 +474,9 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
     if (e == hipSuccess) e = hipMalloc(&c->stats, sizeof(plan_stats));
     // the scans' two totals are plan_stats' first words: a plan reads stats and totals back in one copy
     if (e == hipSuccess) c->totals = &c->stats->total_layers;
+#if PVAC_FAST_READBACK
+    if (e == hipSuccess) e = hipHostMalloc(&c->pin, 256, hipHostMallocDefault);
+#endif
     if (e != hipSuccess) { pvac_hip_ctx_destroy(c); return PVAC_ENOMEM; }
     *out = c;
     return PVAC_OK;
@@ -500,6 +533,7 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->dec_roff);
     hipFree(c->scan_scratch);
     hipFree(c->stats);
+    if (c->pin) hipHostFree(c->pin);
     hipFree(c->check_buf);
     sigma_tables_free(c->H);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -712,8 +746,7 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (e == hipSuccess)
         e = launch_exclusive_scan2_u64(C->l_off, C->e_off, A->n, c->scan_scratch, &c->totals[0], &c->totals[1], c->stream);
     plan_stats st{};
-    if (e == hipSuccess) e = hipMemcpyAsync(&st, c->stats, sizeof st, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = read_back(c, &st, c->stats, sizeof st);
     const unsigned long long tot[2] = {st.total_layers, st.total_edges};
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_plan");
     plan->total_layer_slots = tot[0];
@@ -933,8 +966,7 @@ int run_large(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, c
 int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, const uint64_t* nonces,
                      pvac_ct_batch* C, uint32_t flags, uint32_t* salt_pos) {
     unsigned int cnt = 0;
-    hipError_t e = hipMemcpyAsync(&cnt, c->redo_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipError_t e = read_back(c, &cnt, c->redo_cnt, sizeof cnt);
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_exec (redo count)");
     if (!cnt) return PVAC_OK;
     std::vector<uint64_t> info(5 * (size_t)cnt);
@@ -1112,8 +1144,7 @@ int pvac_hip_ct_add_plan(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_
     if (e == hipSuccess)
         e = launch_exclusive_scan2_u64(C->l_off, C->e_off, A->n, c->scan_scratch, &c->totals[0], &c->totals[1], c->stream);
     plan_stats st{};
-    if (e == hipSuccess) e = hipMemcpyAsync(&st, c->stats, sizeof st, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = read_back(c, &st, c->stats, sizeof st);
     const unsigned long long tot[2] = {st.total_layers, st.total_edges};
     if (e != hipSuccess) return hip_fail(c, e, "ct_add_plan");
     plan->total_layer_slots = tot[0];
