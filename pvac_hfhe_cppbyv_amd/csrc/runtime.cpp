@@ -123,6 +123,8 @@ struct pvac_hip_ctx {
     size_t salt_cap = 0;
     mul_fresh_args* fresh_args = nullptr;   // device copy of the fresh kernel's arguments
     mul_fresh_args fresh_args_host{};
+    bool fresh_args_uploaded = false;       // the device copy holds fresh_args_host
+    bool redo_cnt_dirty = true;             // redo_cnt may be nonzero (zeroed before the next exec)
     uint64_t* scan_scratch = nullptr;
     size_t scan_cap = 0;
     plan_stats* stats = nullptr;
@@ -968,7 +970,10 @@ int redo_fresh_pairs(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batc
     unsigned int cnt = 0;
     hipError_t e = read_back(c, &cnt, c->redo_cnt, sizeof cnt);
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_exec (redo count)");
-    if (!cnt) return PVAC_OK;
+    if (!cnt) {
+        c->redo_cnt_dirty = false;
+        return PVAC_OK;
+    }
     std::vector<uint64_t> info(5 * (size_t)cnt);
     e = launch_gather_large(*A, *B, c->redo_ids, cnt, c->large_info, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(info.data(), c->large_info, info.size() * 8, hipMemcpyDeviceToHost, c->stream);
@@ -1040,13 +1045,15 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         if (rc) return rc;
         salt_pos = c->salt_pos;
     }
-    {
+    if (c->redo_cnt_dirty) {   // a read-back of zero leaves it clean: no memset per exec
         const hipError_t e = hipMemsetAsync(c->redo_cnt, 0, sizeof(unsigned int), c->stream);
         if (e != hipSuccess) return hip_fail(c, e, "reset redo count");
     }
+    c->redo_cnt_dirty = true;   // until this exec reads back a zero count
     c->path_total[0] += plan->n_small;
     if (plan->n_small) {
-        mul_fresh_args a{};
+        mul_fresh_args a;
+        std::memset(&a, 0, sizeof a);   // padding too: the upload below is skipped on equal bytes
         a.A = *A; a.B = *B; a.C = *C;
         a.recs = c->fresh_recs;
         a.nonces = nonces;
@@ -1076,9 +1083,15 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
             hipError_t ea = hipMalloc(&c->fresh_args, sizeof(mul_fresh_args));
             if (ea != hipSuccess) return hip_fail(c, ea, "alloc fresh args");
         }
-        // stream-ordered copy from the ctx's host mirror (kept alive until the next exec)
-        c->fresh_args_host = a;
-        hipError_t e = hipMemcpyAsync(c->fresh_args, &c->fresh_args_host, sizeof a, hipMemcpyHostToDevice, c->stream);
+        // stream-ordered copy from the ctx's host mirror (kept alive until the next exec); a batch
+        // exec'd again into the same buffers (the kernels never write their arguments) reuses it
+        hipError_t e = hipSuccess;
+        if (!c->fresh_args_uploaded || std::memcmp(&c->fresh_args_host, &a, sizeof a) != 0) {
+            c->fresh_args_uploaded = false;
+            std::memcpy(&c->fresh_args_host, &a, sizeof a);
+            e = hipMemcpyAsync(c->fresh_args, &c->fresh_args_host, sizeof a, hipMemcpyHostToDevice, c->stream);
+            c->fresh_args_uploaded = e == hipSuccess;
+        }
         if (e != hipSuccess) return hip_fail(c, e, "upload fresh args");
         scoped_timer t(c, "ct_mul_fresh");
         e = launch_ct_mul_fresh(a, c->fresh_args, c->num_cus, c->stream);
