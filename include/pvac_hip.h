@@ -220,8 +220,8 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * single caller thread gets the concurrency. Synchronous: returns when every chunk is done.
  * Memory: each worker holds two output batches sized for its chunk's largest step (24 B per edge
  * slot; a depth-8 chain of enc_value inputs ends near 345 K edges, ~8.3 MB) plus a scratch arena
- * of at most half the free HBM over streams; streams x chunk beyond the device's HBM fails with
- * PVAC_ENOMEM ("alloc edges"). A call whose (streams, n_devices, chunk) differ from the previous
+ * of at most half the free HBM over streams (an output array that does not fit takes the worker's
+ * arena back first); streams x chunk beyond the device's HBM fails with PVAC_ENOMEM ("alloc edges"). A call whose (streams, n_devices, chunk) differ from the previous
  * call's first releases the workers' buffers and arenas.
  * Each step is exactly pvac_hip_ct_mul_plan + pvac_hip_ct_mul_exec (weights only, reference hash
  * order unless flags has PVAC_MUL_ORDER_CANONICAL). With PVAC_MUL_WITH_SIGMA the FINAL step also

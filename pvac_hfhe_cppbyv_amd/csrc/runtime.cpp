@@ -1882,14 +1882,27 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
             C.e_cnt = S.e_cnt;
             pvac_hip_plan plan{};
             if (!rcchk(pvac_hip_ct_mul_plan(k, &A, &Xv, &C, &plan), "plan")) return;
-            if (plan.total_layer_slots > S.l_cap &&
-                !hipchk(grow_async(S.layers, S.l_cap, plan.total_layer_slots, k->stream), "alloc layers"))
+            // an output array that does not fit first takes this worker's scratch arena back (the
+            // general path reallocates it within what is left, splitting its sub-batch if needed)
+            auto grow_out = [&](auto*& p, size_t& cap, size_t need, const char* what) -> bool {
+                hipError_t e = grow_async(p, cap, need, k->stream);
+                if (e == hipErrorOutOfMemory && k->arena) {
+                    (void)hipGetLastError();
+                    e = hipStreamSynchronize(k->stream);
+                    hipFree(k->arena);
+                    k->arena = nullptr;
+                    k->arena_words = 0;
+                    if (e == hipSuccess) e = grow_async(p, cap, need, k->stream);
+                }
+                return hipchk(e, what);
+            };
+            if (plan.total_layer_slots > S.l_cap && !grow_out(S.layers, S.l_cap, plan.total_layer_slots, "alloc layers"))
                 return;
             if (plan.total_edge_slots > S.e_cap) {
                 size_t c1 = S.e_cap, c2 = S.e_cap, c3 = S.e_cap;
-                if (!hipchk(grow_async(S.meta, c1, plan.total_edge_slots, k->stream), "alloc edges") ||
-                    !hipchk(grow_async(S.w_lo, c2, plan.total_edge_slots, k->stream), "alloc edges") ||
-                    !hipchk(grow_async(S.w_hi, c3, plan.total_edge_slots, k->stream), "alloc edges"))
+                if (!grow_out(S.meta, c1, plan.total_edge_slots, "alloc edges") ||
+                    !grow_out(S.w_lo, c2, plan.total_edge_slots, "alloc edges") ||
+                    !grow_out(S.w_hi, c3, plan.total_edge_slots, "alloc edges"))
                     return;
                 S.e_cap = std::min(c1, std::min(c2, c3));
             }
