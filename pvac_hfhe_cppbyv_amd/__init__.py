@@ -203,10 +203,10 @@ class DeviceBatch:
         self.meta, self.w_lo, self.w_hi, self.sigma = meta, w_lo, w_hi, sigma
 
     def struct(self) -> CtBatch:
-        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
-        return CtBatch(n=self.n, l_off=p(self.l_off), l_cnt=p(self.l_cnt), layers=p(self.layers),
-                       e_off=p(self.e_off), e_cnt=p(self.e_cnt), meta=p(self.meta), w_lo=p(self.w_lo),
-                       w_hi=p(self.w_hi), sigma=p(self.sigma), sigma_words=128, pad=0)
+        # positional integer addresses (0 = NULL): built on every call, so kept cheap
+        p = lambda t: 0 if t is None else t.data_ptr()
+        return CtBatch(self.n, p(self.l_off), p(self.l_cnt), p(self.layers), p(self.e_off), p(self.e_cnt),
+                       p(self.meta), p(self.w_lo), p(self.w_hi), p(self.sigma), 128, 0)
 
     @staticmethod
     def empty(n, layer_slots, edge_slots, device, sigma=False):
