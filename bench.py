@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--pairs", type=int, default=None,
                     help="pairs per GPU (default 2^20 = cfg 3 at N=1; 2^21 at N>1, so N=8 is cfg 5's 2^24 pairs)")
     ap.add_argument("--epl", type=int, default=20, help="edges per BASE layer")
+    ap.add_argument("--shard-rank", type=int, default=None,
+                    help="one GPU runs rank R's shard of a cfg-5 job: pairs [R n, (R + 1) n) of the global batch "
+                         "(n = --pairs, default 2^21): the per-GPU shape of the 8-GPU run, checked end to end")
     ap.add_argument("--cpu-pairs", type=int, default=1 << 17)
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--cpu-share-threads", type=int, default=16, help="second CPU baseline: the box's CPU share")
@@ -211,10 +214,12 @@ def main():
         print(json.dumps(add_bench(eng, args)), flush=True)
         return
     from pvac_hfhe_cppbyv_amd.shard import global_edge_offsets, max_over_ranks
-    n = args.pairs if args.pairs else (1 << 20 if world == 1 else 1 << 21)
+    shard_rank = args.shard_rank if world == 1 else None
+    n = args.pairs if args.pairs else (1 << 20 if world == 1 and shard_rank is None else 1 << 21)
     # weak scaling: rank r owns global pairs [r*n, (r+1)*n); inputs and nonces are keyed by the
-    # global pair index, so the N-GPU result is the 1-GPU result of the same global batch, sharded
-    first = rank * n
+    # global pair index, so the N-GPU result is the 1-GPU result of the same global batch, sharded.
+    # --shard-rank R at world 1 runs rank R's shard alone (global pair indices up to (R + 1) n)
+    first = (shard_rank if shard_rank is not None else rank) * n
     seed = 0x5EED0003
     A = eng.gen_fresh(n, seed, args.epl, first_index=first)
     B = eng.gen_fresh(n, seed + 1, args.epl, first_index=first)
@@ -293,9 +298,11 @@ def main():
         "dtype": "u64",
         "data": "synthetic (device splitmix64 generator, cfg-3 fresh-shaped ciphers)",
         "config": {
-            "workload": ("cfg3" if world == 1 else "cfg5") + f": {n} fresh-shaped Cipher pairs per GPU, "
-                        "batched ct_mul (weights + layers + reference emit order; sigma in side field), "
-                        "default Params B=337",
+            "workload": ("cfg3" if world == 1 and shard_rank is None else "cfg5") +
+                        (f" (rank {shard_rank}'s shard alone: global pairs [{first}, {first + n}))"
+                         if shard_rank is not None else "") +
+                        f": {n} fresh-shaped Cipher pairs per GPU, batched ct_mul, weights-only (weights + "
+                        "layers + the reference's emit order; no sigma in the timed region), default Params B=337",
             "pairs_per_gpu": n,
             "edges_per_layer": args.epl,
             "global_pairs": world * n,
@@ -306,7 +313,10 @@ def main():
                       "global_edge_slots": placement.get("total_edge_slots")},
         },
         "roofline": {
-            "bound": "hbm",
+            # the kernel is VALU-issue-bound (roofline.valu.frac, PMC), not HBM-bound; achieved / peak /
+            # frac are its HBM figures (algorithmic bytes over the HIP-event time), the contract's metric
+            "bound": "valu",
+            "frac_basis": "hbm (algorithmic bytes / kernel time / 8 TB/s); the binding roof is roofline.valu",
             "kernel": FRESH_KERNEL,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PVAC_HIP_ABI_VERSION 2
+#define PVAC_HIP_ABI_VERSION 3
 
 /* status codes */
 #define PVAC_OK 0
@@ -244,6 +244,7 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * PVAC_EINVAL.
  * Step hooks (all optional, called on the worker thread with the worker's stream; A = c_{step},
  * X = the chunk's inputs, C = c_{step+1}, all device batches valid during the call):
+ *   (with per-step operands, below, X is the step's operand)
  *   nonces_at  before step `step`'s exec: fill dev_words[0, n_words) (2 words per layer slot of C,
  *              product layer (la, lb) of pair i at C.l_off[i] + |A_i.L| + |X_i.L| + la |X_i.L| + lb,
  *              lo then hi). Replaces fill_nonces.
@@ -270,6 +271,7 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pva
  * arrays on X's device. ctx keeps the worker contexts of every device between calls. */
 #define PVAC_CHAIN_CHECK_GSUM 0x100u
 #define PVAC_CHAIN_STAGE_INPUTS 0x200u   /* ranges j > 0 stage their chunks even on X's device (tests) */
+#define PVAC_CHAIN_IMG_BATCH2 0x400u     /* image -> records conversions in launches of 2 pairs (tests) */
 #define PVAC_CHAIN_MAX_DEVICES 64
 typedef int (*pvac_chain_step_fn)(void* user, uint32_t step, uint64_t first_input, const pvac_ct_batch* A,
                                   const pvac_ct_batch* X, const pvac_ct_batch* C, uint64_t* dev_words,
@@ -299,6 +301,15 @@ typedef struct pvac_chain_opts {
     uint32_t pad2;
     uint64_t* sumdigest_out;         /* DEVICE [sumdigest_n], nullable: pvac_hip_batch_sumdigest of c_depth */
     uint64_t sumdigest_n;            /* leading inputs whose sum digests are written (reads their whole c_depth) */
+    /* Per-step operands (nullable): HOST [n_operands] batch descriptors of DEVICE arrays on X's device,
+     * each of X->n ciphers. Step d (from 0) computes c_{d+1} = ct_mul(c_d, operands[d]) for d <
+     * n_operands and ct_mul(c_d, x) after that, so the reference's own loop
+     *   chain = enc_value(pk, sk, 2); for i in 1..N-1: chain = ct_mul(pk, chain, enc_value(pk, sk, 2))
+     * (tests/test_main.cpp:289-293) is X = the first encryptions and operands = the later ones. The
+     * step hooks' X argument is the step's operand. n_operands <= depth. */
+    const pvac_ct_batch* operands;
+    uint32_t n_operands;
+    uint32_t pad3;
 } pvac_chain_opts;
 typedef struct pvac_chain_stats {
     uint64_t pair_steps;                        /* inputs x depth */

@@ -425,17 +425,32 @@ public:
     // replayed from a reference stream is byte-identical to the reference's c_depth. devices: GPU
     // ordinals to spread the chains over (whole chunks per device; empty = this engine's device);
     // chunk: inputs per worker chunk (with sigma the last step holds 1 KiB per edge: keep it small).
+    // ops (optional): per-step operands, ops[d][i] the cipher chain i multiplies by at step d + 1
+    // (the reference's own loop, tests/test_main.cpp:291-292, multiplies by a fresh enc_value(2) per
+    // step); steps past ops.size() multiply by x. rnds then carry only the ct_mul draws: a caller
+    // replaying one interleaved stream encrypts the operands from their own stretches of it.
     template <class PubKeyT, class CipherT>
     std::vector<CipherT> ct_mul_chain(const PubKeyT& pk, const std::vector<const CipherT*>& xs, uint32_t depth,
                                       bool with_sigma, std::vector<RandomSource>& rnds,
-                                      const std::vector<int>& devices = {}, uint32_t streams = 2, uint64_t chunk = 16) {
+                                      const std::vector<int>& devices = {}, uint32_t streams = 2, uint64_t chunk = 16,
+                                      const std::vector<std::vector<const CipherT*>>& ops = {}) {
         const size_t n = xs.size();
         if (rnds.size() != n) throw Error(PVAC_EINVAL, "ct_mul_chain: one RandomSource per input");
+        if (ops.size() > depth) throw Error(PVAC_EINVAL, "ct_mul_chain: more operand steps than depth");
+        for (const auto& y : ops)
+            if (y.size() != n) throw Error(PVAC_EINVAL, "ct_mul_chain: one operand per input and step");
         if (!n) return {};
         if (with_sigma) ensure_H(pk);
         detail::batch x;
         detail::to_host(xs, sigma_words(), false, x);
         detail::upload(x, stream_, false);
+        std::vector<detail::batch> yb(ops.size());
+        std::vector<pvac_ct_batch> yv(ops.size());
+        for (size_t d = 0; d < ops.size(); ++d) {
+            detail::to_host(ops[d], sigma_words(), false, yb[d]);
+            detail::upload(yb[d], stream_, false);
+            yv[d] = yb[d].view(false);
+        }
         detail::hip_ok(hipStreamSynchronize(stream_), "sync");
         struct state {
             std::vector<RandomSource>* rnds;
@@ -451,6 +466,8 @@ public:
         o.user = &stt;
         o.devices = devices.empty() ? nullptr : devices.data();
         o.n_devices = (uint32_t)devices.size();
+        o.operands = yv.empty() ? nullptr : yv.data();
+        o.n_operands = (uint32_t)yv.size();
         // hooks run on the library's worker threads; chunks (and so their inputs' sources) are disjoint
         o.nonces_at = [](void* u, uint32_t, uint64_t c0, const pvac_ct_batch* A, const pvac_ct_batch* X,
                          const pvac_ct_batch* C, uint64_t* words, uint64_t nw, void* st) -> int {
@@ -861,6 +878,20 @@ std::vector<CipherT> ct_mul_chain(const PubKeyT& pk, const std::vector<CipherT>&
     std::vector<const CipherT*> x;
     for (auto& c : xs) x.push_back(&c);
     return engine_for(pk).ct_mul_chain(pk, x, depth, with_sigma, rnds, devices);
+}
+
+// The reference's loop c_k = ct_mul(c_{k-1}, y_k) with a fresh operand per step (tests/test_main.cpp:
+// 289-293): ys[k - 1][i] is chain i's operand at step k (depth = ys.size()).
+template <class PubKeyT, class CipherT>
+std::vector<CipherT> ct_mul_chain(const PubKeyT& pk, const std::vector<CipherT>& xs,
+                                  const std::vector<std::vector<CipherT>>& ys, bool with_sigma,
+                                  std::vector<RandomSource>& rnds, const std::vector<int>& devices = {}) {
+    std::vector<const CipherT*> x;
+    for (auto& c : xs) x.push_back(&c);
+    std::vector<std::vector<const CipherT*>> ops(ys.size());
+    for (size_t d = 0; d < ys.size(); ++d)
+        for (auto& c : ys[d]) ops[d].push_back(&c);
+    return engine_for(pk).ct_mul_chain(pk, x, (uint32_t)ys.size(), with_sigma, rnds, devices, 2, 16, ops);
 }
 
 template <class PubKeyT, class CipherT>

@@ -16,3 +16,5 @@ mkdir -p "$OUT"
 "$H" encdeep "$OUT"            # depth hints 16-100, non-default noise Params
 "$H" fullrange "$OUT"          # ct_mul with weights anywhere in [0, 2^128)
 "$H" chainx "$OUT" 4           # chain entry point: x = enc_value(2), c_k = ct_mul(c_{k-1}, x), k <= 4, full stream
+"$H" chainf "$OUT" 4           # the reference's own loop: a fresh enc_value(2) operand per step, k <= 4, full stream
+"$H" chainf8 "$OUT" 8          # the same loop to depth 8: per-step commit digests, stream stretches (manifest only)

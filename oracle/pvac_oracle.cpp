@@ -1008,34 +1008,43 @@ double orc_ct_add_batch_timed(const orc_params* prm, uint64_t npairs, const uint
 }
 
 /* cfg 4 on the CPU port (SURVEY 8(d) restatement of tests/test_main.cpp:289-295): per input i,
- * c_0 = x_i, c_k = ct_mul(c_{k-1}, x_i) for k = 1..depth, weights only. Nonces do not reach the
- * edges (only layer records), so they are synthetic here; the FNV-1a edge digest of c_depth is
+ * c_0 = x_i, c_k = ct_mul(c_{k-1}, y_{k,i}) for k = 1..depth, weights only, with y_{k,i} = x_i (the
+ * cfg-4 shape) or, for k <= nops, operand d = k - 1 of input i: cipher d * ninputs + i of the packed
+ * operand batch (the reference's own loop, a fresh enc_value per step, :291-292). Nonces do not reach
+ * the edges (only layer records), so they are synthetic here; the FNV-1a edge digest of c_depth is
  * comparable with the engine's. step_edges[d] accumulates |c_{d+1}.E| over the inputs. */
-double orc_ct_mul_chain_timed(const orc_params* prm, uint64_t ninputs, const uint64_t* loff, const orc_layer* layers,
-                              const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
-                              int depth, int threads, uint64_t* out_counts, uint64_t* out_digests,
-                              uint64_t* step_edges) {
+double orc_ct_mul_chain_ops_timed(const orc_params* prm, uint64_t ninputs, const uint64_t* loff, const orc_layer* layers,
+                                  const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
+                                  int depth, int nops, const uint64_t* oloff, const orc_layer* olayers,
+                                  const uint64_t* oeoff, const uint64_t* ometa, const uint64_t* owlo,
+                                  const uint64_t* owhi, int threads, uint64_t* out_counts, uint64_t* out_digests,
+                                  uint64_t* step_edges) {
     if (threads < 1) threads = 1;
     std::vector<std::vector<u64>> per((size_t)threads, std::vector<u64>((size_t)(depth > 0 ? depth : 1), 0));
+    auto view = [](uint64_t j, const uint64_t* lo, const orc_layer* ly, const uint64_t* eo, const uint64_t* m,
+                   const uint64_t* wl, const uint64_t* wh) {
+        orc_cipher X{};
+        X.nL = lo[j + 1] - lo[j]; X.nE = eo[j + 1] - eo[j];
+        X.layers = const_cast<orc_layer*>(ly + lo[j]);
+        X.meta = const_cast<uint64_t*>(m + eo[j]);
+        X.w_lo = const_cast<uint64_t*>(wl + eo[j]);
+        X.w_hi = const_cast<uint64_t*>(wh + eo[j]);
+        return load(&X);
+    };
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
         th.emplace_back([&, t] {
             std::vector<u64> nonces;
             for (uint64_t i = (uint64_t)t; i < ninputs; i += (uint64_t)threads) {
-                orc_cipher X{};
-                X.nL = loff[i + 1] - loff[i]; X.nE = eoff[i + 1] - eoff[i];
-                X.layers = const_cast<orc_layer*>(layers + loff[i]);
-                X.meta = const_cast<uint64_t*>(meta + eoff[i]);
-                X.w_lo = const_cast<uint64_t*>(wlo + eoff[i]);
-                X.w_hi = const_cast<uint64_t*>(whi + eoff[i]);
-                const Ct x = load(&X);
+                const Ct x = view(i, loff, layers, eoff, meta, wlo, whi);
                 Ct c = x;
                 for (int d = 0; d < depth; ++d) {
                     Ct nxt;
-                    nonces.assign(2 * c.L.size() * x.L.size(), 0);
+                    const Ct y = d < nops ? view((uint64_t)d * ninputs + i, oloff, olayers, oeoff, ometa, owlo, owhi) : x;
+                    nonces.assign(2 * c.L.size() * y.L.size(), 0);
                     for (size_t k = 0; k < nonces.size(); ++k) nonces[k] = i * 0x100000001b3ULL + 977u * (u64)d + k;
-                    ct_mul_impl(prm, nullptr, c, x, nonces.data(), nullptr, nxt);
+                    ct_mul_impl(prm, nullptr, c, y, nonces.data(), nullptr, nxt);
                     c = std::move(nxt);
                     per[(size_t)t][(size_t)d] += c.E.size();
                 }
@@ -1057,6 +1066,14 @@ double orc_ct_mul_chain_timed(const orc_params* prm, uint64_t ninputs, const uin
             for (int t = 0; t < threads; ++t) step_edges[d] += per[(size_t)t][(size_t)d];
         }
     return secs;
+}
+
+double orc_ct_mul_chain_timed(const orc_params* prm, uint64_t ninputs, const uint64_t* loff, const orc_layer* layers,
+                              const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
+                              int depth, int threads, uint64_t* out_counts, uint64_t* out_digests,
+                              uint64_t* step_edges) {
+    return orc_ct_mul_chain_ops_timed(prm, ninputs, loff, layers, eoff, meta, wlo, whi, depth, 0, nullptr, nullptr,
+                                      nullptr, nullptr, nullptr, nullptr, threads, out_counts, out_digests, step_edges);
 }
 
 }  // extern "C"

@@ -137,6 +137,14 @@ double orc_ct_mul_chain_timed(const orc_params* prm, uint64_t ninputs, const uin
                               const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
                               int depth, int threads, uint64_t* out_counts, uint64_t* out_digests,
                               uint64_t* step_edges);
+/* The same with per-step operands for steps 1..nops: c_k = ct_mul(c_{k-1}, ops[(k-1) * ninputs + i])
+ * (a packed batch of nops * ninputs ciphers, step-major), x_i after that. */
+double orc_ct_mul_chain_ops_timed(const orc_params* prm, uint64_t ninputs, const uint64_t* loff, const orc_layer* layers,
+                                  const uint64_t* eoff, const uint64_t* meta, const uint64_t* wlo, const uint64_t* whi,
+                                  int depth, int nops, const uint64_t* oloff, const orc_layer* olayers,
+                                  const uint64_t* oeoff, const uint64_t* ometa, const uint64_t* owlo,
+                                  const uint64_t* owhi, int threads, uint64_t* out_counts, uint64_t* out_digests,
+                                  uint64_t* step_edges);
 
 #ifdef __cplusplus
 }

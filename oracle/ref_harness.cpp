@@ -737,6 +737,71 @@ static void cmd_chainx(const std::string& dir, int depth) {
     std::ofstream(dir + "/chainx_manifest.json") << js.str();
 }
 
+// ---- the reference's OWN chain loop (tests/test_main.cpp:289-293): chain = enc_value(pk, sk, 2), then
+//      chain = ct_mul(pk, chain, enc_value(pk, sk, 2)) for steps 1..depth, a FRESH operand per step (the
+//      operand is encrypted before the ct_mul consumes it, so the stream interleaves enc, mul, enc, ...).
+//      The stream is the interposed splitmix64 sequence from reseed(S): word j (0-based) is
+//      splitmix64(S + (j + 1) * golden), so a consumer regenerates any stretch of it from S and j. The
+//      manifest gives each step's enc and mul stretches, the product-layer nonce words at the head of
+//      the mul stretch (2 |c_{k-1}.L| |y_k.L|), |E| / |L| of c_k and two commit_ct digests (ops/commit.hpp)
+//      of c_k: with its sigmas and of a sigma-less copy (weights, layers, order).
+//      full = true (chainf): also the whole stream, every operand (weights-only .ct), c_depth's .ct,
+//      layer table and per-edge sigma digests. full = false (chainf8): the manifest only.
+static Cipher strip_sigma(const Cipher& c) {
+    Cipher w = c;
+    for (auto& e : w.E) e.s = BitVec();
+    return w;
+}
+
+static void cmd_chainf(const std::string& dir, int depth, bool full) {
+    reseed(0x5EED0C00ULL);   // the same key as cmd_fixtures
+    Params prm;
+    PubKey pk;
+    SecKey sk;
+    g_logging = false;
+    keygen(prm, pk, sk);
+    (void)enc_value(pk, sk, 1);   // the Toeplitz autotuner's own draws stay out of the logged stream
+    const std::string tag = full ? "chainf" : "chainf8";
+    const uint64_t S = full ? 0x5EED0CF0ULL : 0x5EED0CF8ULL;
+    reseed(S);
+    g_logging = true;
+    const size_t base = g_log.size();
+    Cipher c = enc_value(pk, sk, 2);
+    const size_t x_len = g_log.size() - base;
+    if (full) write_ct(dir + "/" + tag + "_x.ct", {c}, false);
+    std::ostringstream js;
+    js << "{\n  \"canon_tag\": " << pk.canon_tag << ", \"depth\": " << depth << ", \"seed\": " << S
+       << ", \"x_stream\": [0, " << x_len << "],\n  \"steps\": [\n";
+    for (int k = 1; k <= depth; ++k) {
+        const size_t e0 = g_log.size() - base;
+        Cipher y = enc_value(pk, sk, 2);
+        const size_t m0 = g_log.size() - base;
+        const size_t nonce_words = 2 * c.L.size() * y.L.size();
+        c = ct_mul(pk, c, y);
+        const size_t m1 = g_log.size() - base;
+        g_logging = false;
+        const auto cm = commit_ct(pk, c), cw = commit_ct(pk, strip_sigma(c));
+        g_logging = true;
+        if (full) write_ct(dir + "/" + tag + "_y" + std::to_string(k) + ".ct", {y}, false);
+        js << "    {\"enc_stream\": [" << e0 << ", " << (m0 - e0) << "], \"mul_stream\": [" << m0 << ", " << (m1 - m0)
+           << "], \"nonce_words\": " << nonce_words << ", \"edges\": " << c.E.size() << ", \"layers\": "
+           << c.L.size() << ", \"commit\": \"" << hex(cm.data(), 32) << "\", \"commit_weights\": \""
+           << hex(cw.data(), 32) << "\"}" << (k < depth ? "," : "") << "\n";
+        std::printf("%s step %d edges %zu layers %zu\n", tag.c_str(), k, c.E.size(), c.L.size());
+        std::fflush(stdout);
+    }
+    g_logging = false;
+    const Fp d = dec_value(pk, sk, c);
+    js << "  ],\n  \"stream\": " << (g_log.size() - base) << ", \"dec\": " << fpjson(d) << "\n}\n";
+    if (full) {
+        write_u64(dir + "/" + tag + "_stream.u64", std::vector<uint64_t>(g_log.begin() + (long)base, g_log.end()));
+        write_ct(dir + "/" + tag + "_final.ct", {c}, false);
+        write_layers(dir + "/" + tag + "_final_layers.u64", c);
+        write_u64(dir + "/" + tag + "_final_sigdig.u64", sigma_digests(c));
+    }
+    std::ofstream(dir + "/" + tag + "_manifest.json") << js.str();
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: ref_harness fp|fixtures|time_mul ...\n"); return 2; }
     std::string cmd = argv[1];
@@ -750,6 +815,10 @@ int main(int argc, char** argv) {
     }
     if (cmd == "chainx" && argc >= 3) {
         cmd_chainx(argv[2], argc > 3 ? std::atoi(argv[3]) : 4);
+        return 0;
+    }
+    if ((cmd == "chainf" || cmd == "chainf8") && argc >= 3) {
+        cmd_chainf(argv[2], argc > 3 ? std::atoi(argv[3]) : (cmd == "chainf" ? 4 : 8), cmd == "chainf");
         return 0;
     }
     if (cmd == "encdepth" && argc >= 3) {

@@ -28,6 +28,7 @@ FP_ADD, FP_SUB, FP_MUL, FP_NEG, FP_SCALE, FP_INV = 0, 1, 2, 3, 4, 5
 MUL_WITH_SIGMA, MUL_ORDER_CANONICAL = 0x1, 0x2
 CHAIN_CHECK_GSUM = 0x100
 CHAIN_STAGE_INPUTS = 0x200
+CHAIN_IMG_BATCH2 = 0x400
 CHAIN_MAX_DEPTH = 32
 ENC_WITH_SIGMA = 0x1
 
@@ -91,7 +92,8 @@ class ChainOpts(C.Structure):
                 ("on_chunk", ON_CHUNK_CB),
                 ("user", C.c_void_p), ("nonces_at", STEP_CB), ("after_step", STEP_CB), ("salts_at", STEP_CB),
                 ("devices", C.c_void_p), ("n_devices", C.c_uint32), ("pad2", C.c_uint32),
-                ("sumdigest_out", C.c_void_p), ("sumdigest_n", C.c_uint64)]
+                ("sumdigest_out", C.c_void_p), ("sumdigest_n", C.c_uint64),
+                ("operands", C.c_void_p), ("n_operands", C.c_uint32), ("pad3", C.c_uint32)]
 
 
 class ChainStats(C.Structure):
@@ -424,7 +426,7 @@ class Engine:
     def ct_mul_chain(self, X: DeviceBatch, depth, nonce_seed=0x5EED0040, streams=4, chunk=1024, check_gsum=False,
                      digest_n=0, canonical=False, fill_nonces=None, on_chunk=None, count_n=None, sigma=False,
                      devices=None, stage_inputs=False, nonces_at=None, after_step=None, salts_at=None,
-                     sumdigest=False):
+                     sumdigest=False, operands=None, img_batch2=False):
         """c_0 = x, c_k = ct_mul(c_{k-1}, x) to `depth` for every input x of X (tests/test_main.cpp:289-295)
         on `streams` internal worker streams in chunks of `chunk` inputs (pvac_hip_ct_mul_chain).
         Returns a dict of the call's statistics; with digest_n > 0 also the final digests / edge
@@ -435,7 +437,10 @@ class Engine:
         ordinals, one contiguous range of whole chunks each (stage_inputs: ranges after the first copy
         their chunks to worker buffers even on this device). nonces_at / after_step / salts_at: STEP_CB
         hooks (include/pvac_hip.h). sumdigest: True (every input) or the number of leading inputs
-        whose pvac_hip_batch_sumdigest is returned."""
+        whose pvac_hip_batch_sumdigest is returned. operands: DeviceBatches of |X| ciphers, step d
+        multiplying by operands[d] (the reference's loop with a fresh enc_value per step,
+        tests/test_main.cpp:291-292), later steps by X. img_batch2: image conversions in launches of
+        two pairs (tests)."""
         torch = self.torch
         dn = min(int(digest_n), X.n)
         cn = dn if count_n is None else min(int(count_n), X.n)
@@ -444,16 +449,23 @@ class Engine:
         sn = min(X.n if sumdigest is True else int(sumdigest or 0), X.n)   # True: every input
         sdg = torch.zeros(max(sn, 1), dtype=torch.int64, device=self.device) if sn else None
         devs = (C.c_int * len(devices))(*devices) if devices else None
+        ops = list(operands or [])
+        for Y in ops:
+            if Y.n != X.n:
+                raise PvacError("ct_mul_chain: every operand batch needs |X| ciphers")
+        op_structs = (CtBatch * len(ops))(*[Y.struct() for Y in ops]) if ops else None
         o = ChainOpts(depth=depth, streams=streams, chunk=chunk, nonce_seed=nonce_seed,
                       flags=(CHAIN_CHECK_GSUM if check_gsum else 0) | (MUL_ORDER_CANONICAL if canonical else 0) |
-                      (MUL_WITH_SIGMA if sigma else 0) | (CHAIN_STAGE_INPUTS if stage_inputs else 0),
+                      (MUL_WITH_SIGMA if sigma else 0) | (CHAIN_STAGE_INPUTS if stage_inputs else 0) |
+                      (CHAIN_IMG_BATCH2 if img_batch2 else 0),
                       pad=0, digest_n=dn, digest_out=C.c_void_p(dig.data_ptr()) if dn else None,
                       count_n=cn, count_out=C.c_void_p(cnt.data_ptr()) if cn else None,
                       fill_nonces=fill_nonces or FILL_NONCES_CB(), on_chunk=on_chunk or ON_CHUNK_CB(), user=None,
                       nonces_at=nonces_at or STEP_CB(), after_step=after_step or STEP_CB(),
                       salts_at=salts_at or STEP_CB(), devices=C.cast(devs, C.c_void_p) if devs else None,
                       n_devices=len(devices) if devices else 0, pad2=0,
-                      sumdigest_out=C.c_void_p(sdg.data_ptr()) if sdg is not None else None, sumdigest_n=sn)
+                      sumdigest_out=C.c_void_p(sdg.data_ptr()) if sdg is not None else None, sumdigest_n=sn,
+                      operands=C.cast(op_structs, C.c_void_p) if ops else None, n_operands=len(ops), pad3=0)
         st = ChainStats()
         sx = X.struct()
         self._check(self.lib.pvac_hip_ct_mul_chain(self.ctx, C.byref(sx), C.byref(o), C.byref(st)))

@@ -357,9 +357,10 @@ constexpr uint32_t kLaPerWG = 8;
 constexpr uint32_t kLaMaxLB = 4;
 hipError_t launch_ct_mul_large(const mul_large_args& a, hipStream_t st);
 // dense chain images back to hash-order records for the listed pairs whose flag is set (the flag is
-// cleared): tmp holds 3 words per edge of every listed pair (sum of their |A.E|)
+// cleared): pairs = [n_pairs ids, then n_pairs offsets into tmp], tmp holds 3 words per edge of every
+// listed pair (sum of their |A.E|); launches of at most y_cap pairs each (65535: the grid-y limit)
 hipError_t launch_image_to_records(const pvac_ct_batch& A, uint32_t* img, const uint64_t* pairs, uint32_t n_pairs,
-                                   uint64_t* tmp, uint32_t Bm, hipStream_t st);
+                                   uint64_t* tmp, uint32_t Bm, uint32_t y_cap, hipStream_t st);
 // LDS of k_large_products_direct for B and nbl staged B layers (the direct mode needs it <= 160 KB)
 uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl);
 // measured integer-ALU ceilings (k_ubench.hip)
@@ -370,7 +371,9 @@ hipError_t launch_check_sizes(const pvac_ct_batch& A, const pvac_ct_batch& B, co
                               hipStream_t st);
 hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C, const uint64_t* nonces,
                              const uint64_t* powg, uint32_t Bm, const unsigned int* mx_host, uint32_t* status,
-                             unsigned long long* n_bad, int num_cus, hipStream_t st);
+                             unsigned long long* n_bad, int num_cus, uint8_t* gscratch, hipStream_t st);
+// global scratch bytes launch_check_gsum needs when a pair's layer tables exceed LDS (0 if they fit)
+uint64_t check_gsum_scratch_bytes(uint32_t Bm, const unsigned int* mx_host, uint64_t n, int num_cus);
 // pvac_hip_ct_mul_chain statistics: out[0] += sum |C.E|, out[1] += sum |A.E| |X.E| (k_check.hip)
 hipError_t launch_stage_rows(const pvac_ct_batch& src, const pvac_ct_batch& dst, hipStream_t st);
 hipError_t launch_chain_stats(const pvac_ct_batch& A, const pvac_ct_batch& X, const pvac_ct_batch& C,

@@ -11,7 +11,9 @@
 // (no edge emitted) must have gsum(A, la) * gsum(B, lb) == 0; a C layer with edges that is not a
 // product layer fails the check.
 //
-// One 256-thread workgroup per pair (persistent over the batch). Per-layer sums are exact: each
+// One 256-thread workgroup per pair (persistent over the batch). The layer tables live in LDS while
+// they fit (to depth 8 of the cfg-4 chains); deeper steps (depth 9: |C.L| ~ 3,100 layers of 48-byte
+// sums) run the same code over a per-workgroup slab of global scratch. Per-layer sums are exact: each
 // canonical term is split into 43/42/42-bit limbs (fp_split3) and summed per (layer, channel) with
 // LDS u64 atomics (< 2^21 edges per cipher), then folded and P - M taken once. Equal to the
 // reference's fp_add / fp_sub chains, which compute exact residues for canonical terms.
@@ -38,6 +40,8 @@ struct check_args {
     uint32_t Bm;
     uint32_t* status;
     unsigned long long* n_bad;
+    uint8_t* gscratch;      // global mode: per-workgroup slabs of gstride bytes (else null: LDS)
+    uint64_t gstride;
 };
 
 struct check_lds {   // byte offsets into dynamic LDS
@@ -94,8 +98,10 @@ __device__ void gsum_fold(unsigned long long* acc, uint32_t L) {
     }
 }
 
+template <bool kGlobal>
 __global__ __launch_bounds__(kCB) void k_check_gsum(check_args g, check_lds Ls) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+    uint8_t* lds = kGlobal ? g.gscratch + (uint64_t)blockIdx.x * g.gstride : lds_dyn;
     ulonglong2* pg = (ulonglong2*)(lds + Ls.powg);
     unsigned long long* accA = (unsigned long long*)(lds + Ls.accA);
     unsigned long long* accB = (unsigned long long*)(lds + Ls.accB);
@@ -122,6 +128,7 @@ __global__ __launch_bounds__(kCB) void k_check_gsum(check_args g, check_lds Ls) 
             cand[q] = make_ulonglong2(g.nonces[2 * (cslot + q)], g.nonces[2 * (cslot + q) + 1]);
             found[q] = 0;
         }
+        if (kGlobal) __threadfence();   // global slab: each phase's writes / atomics visible to the next
         __syncthreads();
         if (bad != 3u) {
             uint32_t b = 0;
@@ -130,10 +137,12 @@ __global__ __launch_bounds__(kCB) void k_check_gsum(check_args g, check_lds Ls) 
             gsum_edges(g.C, g.C.e_off[p], nC, LC, pg, g.Bm, accC, cntC, b);
             if (b) bad = b;
         }
+        if (kGlobal) __threadfence();
         __syncthreads();
         gsum_fold(accA, LA);
         gsum_fold(accB, LB);
         gsum_fold(accC, LC);
+        if (kGlobal) __threadfence();
         __syncthreads();
         if (bad == 0u) {
             // every C layer with edges is the product layer of the (la, lb) whose nonce it carries
@@ -206,17 +215,36 @@ hipError_t launch_check_sizes(const pvac_ct_batch& A, const pvac_ct_batch& B, co
     return hipGetLastError();
 }
 
-// returns hipErrorInvalidValue when one pair's layer tables exceed the LDS of a workgroup
+namespace {
+constexpr uint32_t kCheckLds = 160u * 1024u;
+uint64_t check_blocks(uint64_t n, int num_cus, bool global) {
+    const uint64_t b = (uint64_t)num_cus * (global ? 2 : 8);
+    return b > n ? n : b;
+}
+}  // namespace
+
+// global scratch the check needs for the batch's largest tables (0: they fit LDS)
+uint64_t check_gsum_scratch_bytes(uint32_t Bm, const unsigned int* mx_host, uint64_t n, int num_cus) {
+    const check_lds L = check_layout(Bm, mx_host[0], mx_host[1], mx_host[2], mx_host[3]);
+    if (L.total <= kCheckLds) return 0;
+    return check_blocks(n, num_cus, true) * (uint64_t)al16(L.total);
+}
+
+// tables beyond LDS run over gscratch (check_gsum_scratch_bytes of it; hipErrorInvalidValue if null)
 hipError_t launch_check_gsum(const pvac_ct_batch& A, const pvac_ct_batch& B, const pvac_ct_batch& C, const uint64_t* nonces,
                              const uint64_t* powg, uint32_t Bm, const unsigned int* mx_host, uint32_t* status,
-                             unsigned long long* n_bad, int num_cus, hipStream_t st) {
+                             unsigned long long* n_bad, int num_cus, uint8_t* gscratch, hipStream_t st) {
     if (!A.n) return hipSuccess;
     const check_lds L = check_layout(Bm, mx_host[0], mx_host[1], mx_host[2], mx_host[3]);
-    if (L.total > 160u * 1024u) return hipErrorInvalidValue;
-    check_args g{A, B, C, nonces, (const ulonglong2*)powg, Bm, status, n_bad};
-    uint64_t blocks = (uint64_t)num_cus * 8;
-    if (blocks > A.n) blocks = A.n;
-    hipLaunchKernelGGL(k_check_gsum, dim3((unsigned)blocks), dim3(kCB), L.total, st, g, L);
+    const bool global = L.total > kCheckLds;
+    if (global && !gscratch) return hipErrorInvalidValue;
+    check_args g{A, B, C, nonces, (const ulonglong2*)powg, Bm, status, n_bad, global ? gscratch : nullptr,
+                 al16(L.total)};
+    const uint64_t blocks = check_blocks(A.n, num_cus, global);
+    if (global)
+        hipLaunchKernelGGL(k_check_gsum<true>, dim3((unsigned)blocks), dim3(kCB), 0, st, g, L);
+    else
+        hipLaunchKernelGGL(k_check_gsum<false>, dim3((unsigned)blocks), dim3(kCB), L.total, st, g, L);
     return hipGetLastError();
 }
 

@@ -2455,13 +2455,15 @@ uint32_t large_direct_lds_bytes(uint32_t Bm, uint32_t nbl) { return dir_lds_byte
 // ---------------------------------------------------------------- dense chain images -> records
 // (k_large_products_direct's image writer; see mul_large_args::A_img) Listed pair y (pairs[y], its
 // edges at tmp + 3 pairs[n + y]): the image is copied out, then every slot's edge is written back at
-// its hash-order position as (meta, w_lo, w_hi); the flags are cleared last.
+// its hash-order position as (meta, w_lo, w_hi); the flags are cleared last. A launch covers the
+// listed pairs y = y0 + blockIdx.y (grid y is capped, so a long list takes several launches).
 __global__ __launch_bounds__(256) void k_img_copy(pvac_ct_batch A, const uint32_t* img, const uint64_t* pairs, uint32_t n,
-                                                  uint64_t* tmp) {
-    const uint64_t pr = pairs[blockIdx.y];
+                                                  uint32_t y0, uint64_t* tmp) {
+    const uint32_t y = y0 + blockIdx.y;
+    const uint64_t pr = pairs[y];
     if (!img[pr]) return;
     const uint64_t eo = A.e_off[pr], ne = A.e_cnt[pr];
-    uint64_t* t = tmp + 3u * pairs[n + blockIdx.y];
+    uint64_t* t = tmp + 3u * pairs[n + y];
     const uint32_t* ids = (const uint32_t*)(A.meta + eo);
     for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < ne; k += (uint64_t)gridDim.x * 256u) {
         t[3u * k] = ids[k];
@@ -2470,12 +2472,13 @@ __global__ __launch_bounds__(256) void k_img_copy(pvac_ct_batch A, const uint32_
     }
 }
 __global__ __launch_bounds__(256) void k_img_scatter(pvac_ct_batch A, const uint32_t* img, const uint64_t* pairs, uint32_t n,
-                                                     const uint64_t* tmp, uint32_t Bm) {
-    const uint64_t pr = pairs[blockIdx.y];
+                                                     uint32_t y0, const uint64_t* tmp, uint32_t Bm) {
+    const uint32_t y = y0 + blockIdx.y;
+    const uint64_t pr = pairs[y];
     if (!img[pr]) return;
     const uint64_t eo = A.e_off[pr], ne = A.e_cnt[pr];
     const uint64_t slab = 2u * Bm, first = A.l_cnt[pr] - ne / slab;   // the slabs are the last layers
-    const uint64_t* t = tmp + 3u * pairs[n + blockIdx.y];
+    const uint64_t* t = tmp + 3u * pairs[n + y];
     for (uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x; k < ne; k += (uint64_t)gridDim.x * 256u) {
         const uint32_t id = (uint32_t)t[3u * k];
         const uint32_t pos = id & 0x1FFFFFu, cell = id >> 21;
@@ -2491,12 +2494,13 @@ __global__ __launch_bounds__(64) void k_img_clear(uint32_t* img, const uint64_t*
     if (y < n) img[pairs[y]] = 0u;
 }
 hipError_t launch_image_to_records(const pvac_ct_batch& A, uint32_t* img, const uint64_t* pairs, uint32_t n_pairs,
-                                   uint64_t* tmp, uint32_t Bm, hipStream_t st) {
+                                   uint64_t* tmp, uint32_t Bm, uint32_t y_cap, hipStream_t st) {
     if (!n_pairs) return hipSuccess;
-    for (uint32_t y0 = 0; y0 < n_pairs; y0 += 65535u) {   // grid y limit
-        const uint32_t ny = std::min<uint32_t>(n_pairs - y0, 65535u);
-        hipLaunchKernelGGL(k_img_copy, dim3(64, ny), dim3(256), 0, st, A, img, pairs + y0, n_pairs - y0, tmp);
-        hipLaunchKernelGGL(k_img_scatter, dim3(64, ny), dim3(256), 0, st, A, img, pairs + y0, n_pairs - y0, tmp, Bm);
+    y_cap = std::min<uint32_t>(std::max<uint32_t>(y_cap, 1u), 65535u);   // grid y limit (tests pass small caps)
+    for (uint32_t y0 = 0; y0 < n_pairs; y0 += y_cap) {
+        const uint32_t ny = std::min<uint32_t>(n_pairs - y0, y_cap);
+        hipLaunchKernelGGL(k_img_copy, dim3(64, ny), dim3(256), 0, st, A, img, pairs, n_pairs, y0, tmp);
+        hipLaunchKernelGGL(k_img_scatter, dim3(64, ny), dim3(256), 0, st, A, img, pairs, n_pairs, y0, tmp, Bm);
     }
     hipLaunchKernelGGL(k_img_clear, dim3((n_pairs + 63u) / 64u), dim3(64), 0, st, img, pairs, n_pairs);
     return hipGetLastError();

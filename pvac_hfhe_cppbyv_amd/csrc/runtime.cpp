@@ -129,6 +129,8 @@ struct pvac_hip_ctx {
     size_t scan_cap = 0;
     plan_stats* stats = nullptr;
     unsigned int* check_buf = nullptr;   // gsum check: 4 layer maxima, then a u64 failure count
+    uint8_t* check_scratch = nullptr;    // gsum check: layer tables beyond LDS (global slabs)
+    size_t check_scratch_cap = 0;
     unsigned long long* totals = nullptr;   // [2]: &stats->total_layers (layer and edge slot totals)
     void* pin = nullptr;                    // pinned host words for the plan's and exec's read-backs
     sigma_tables H;
@@ -147,10 +149,13 @@ struct pvac_hip_ctx {
     size_t img_tmp_cap = 0;
     uint64_t* img_pairs = nullptr;     // [2 n]: pair ids, then their offsets in img_tmp
     size_t img_pairs_cap = 0;
+    uint32_t img_grid_y = 65535;       // pairs per image -> records launch (PVAC_CHAIN_IMG_BATCH2: 2)
+    uint32_t spin_us = 50000;          // read_back's spin before a blocking wait (chain workers: 200)
     // pvac_hip_ct_mul_chain: worker contexts (own stream / arena), and a worker's own buffers
     std::vector<pvac_hip_ctx*> chain_kids;   // [range j * streams + w] of the last call's layout
     chain_set chain_bufs[2];
     chain_set chain_stage;                   // a worker's staged chunk inputs (another device, or STAGE)
+    chain_set chain_stage_op;                // ... and its staged per-step operand (pvac_chain_opts::operands)
     uint64_t* chain_nonces = nullptr;
     size_t chain_nonce_cap = 0;
     uint64_t* chain_salts = nullptr;         // final-step salts (WITH_SIGMA)
@@ -158,7 +163,7 @@ struct pvac_hip_ctx {
     uint64_t* chain_out = nullptr;           // digests / counts of a chunk before the copy to X's device
     size_t chain_out_cap = 0;
     unsigned long long* chain_stats = nullptr;   // [2 * PVAC_CHAIN_MAX_DEPTH + 1]: edges / products, image pair-steps
-    uint64_t chain_layout[3] = {0, 0, 0};       // the last call's (streams, devices, chunk)
+    std::vector<int64_t> chain_layout;          // the last call's (streams, chunk, n_devices, ordinals...)
     uint64_t H_gen = 0;                      // bumped whenever H is set (a worker's copy follows it)
     uint64_t H_from = 0;                     // worker: the parent's H_gen its H copy was taken from
 };
@@ -223,7 +228,10 @@ void flush_timers(pvac_hip_ctx* c) {
 #endif
 // The short host waits of a plan (its totals) and of exec (the redo count): a blocking
 // hipStreamSynchronize wakes tens of microseconds after the copy lands, so spin on hipStreamQuery
-// (up to 50 ms, then block) and read into pinned words (a pageable destination stages the copy).
+// (up to spin_us, then block) and read into pinned words (a pageable destination stages the copy).
+// A caller's context spins up to 50 ms (one thread, the headline step); the chain's worker contexts
+// (several threads per device) spin 200 us and then block, so they do not hold cores and the HIP
+// runtime's locks while their kernels run.
 hipError_t read_back(pvac_hip_ctx* c, void* dst, const void* src, size_t bytes) {
 #if PVAC_FAST_READBACK
     if (c->pin && bytes <= 256) {
@@ -233,7 +241,7 @@ hipError_t read_back(pvac_hip_ctx* c, void* dst, const void* src, size_t bytes) 
         for (;;) {
             e = hipStreamQuery(c->stream);
             if (e != hipErrorNotReady) break;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) {
                 e = hipStreamSynchronize(c->stream);
                 break;
             }
@@ -486,7 +494,7 @@ int pvac_hip_ctx_create(int device, const pvac_hip_params* prm, pvac_hip_ctx** o
 
 // a chain worker's output batches (stream-ordered frees on its stream; the caller synchronises)
 static void free_chain_sets(pvac_hip_ctx* c) {
-    for (chain_set* b : {&c->chain_bufs[0], &c->chain_bufs[1], &c->chain_stage}) {
+    for (chain_set* b : {&c->chain_bufs[0], &c->chain_bufs[1], &c->chain_stage, &c->chain_stage_op}) {
         for (void* q : {(void*)b->l_off, (void*)b->l_cnt, (void*)b->e_off, (void*)b->e_cnt, (void*)b->layers,
                         (void*)b->meta, (void*)b->w_lo, (void*)b->w_hi, (void*)b->sigma, (void*)b->img})
             if (q) hipFreeAsync(q, c->stream);
@@ -494,11 +502,33 @@ static void free_chain_sets(pvac_hip_ctx* c) {
     }
 }
 
+// everything a chain worker grew during a call (output batches, nonce / salt / result words, image
+// scratch, the general-path arena); the caller selected the worker's device
+static hipError_t release_chain_worker(pvac_hip_ctx* k) {
+    free_chain_sets(k);
+    for (void** q : {(void**)&k->chain_nonces, (void**)&k->chain_salts, (void**)&k->chain_out}) {
+        if (*q) hipFreeAsync(*q, k->stream);
+        *q = nullptr;
+    }
+    k->chain_nonce_cap = k->chain_salt_cap = k->chain_out_cap = 0;
+    const hipError_t e = hipStreamSynchronize(k->stream);
+    for (void** q : {(void**)&k->img_tmp, (void**)&k->img_pairs, (void**)&k->arena, (void**)&k->check_scratch}) {
+        hipFree(*q);
+        *q = nullptr;
+    }
+    k->img_tmp_cap = k->img_pairs_cap = k->check_scratch_cap = 0;
+    k->arena_words = 0;
+    return e;
+}
+
 int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     if (!c) return PVAC_OK;
+    int caller_dev = -1;   // the calling thread's device, restored on return
+    if (hipGetDevice(&caller_dev) != hipSuccess) caller_dev = -1;
     hipSetDevice(c->device);
     for (pvac_hip_ctx* k : c->chain_kids) pvac_hip_ctx_destroy(k);
     c->chain_kids.clear();
+    hipSetDevice(c->device);   // each worker's destroy selected the worker's device
     if (c->stream) hipStreamSynchronize(c->stream);
     flush_timers(c);
     free_chain_sets(c);
@@ -537,9 +567,11 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipFree(c->stats);
     if (c->pin) hipHostFree(c->pin);
     hipFree(c->check_buf);
+    hipFree(c->check_scratch);
     sigma_tables_free(c->H);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
+    if (caller_dev >= 0) hipSetDevice(caller_dev);
     return PVAC_OK;
 }
 
@@ -812,7 +844,8 @@ int images_to_records(pvac_hip_ctx* c, const pvac_ct_batch* A, const std::vector
     if (rc) return rc;
     hipError_t e = hipMemcpyAsync(c->img_pairs, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess)
-        e = launch_image_to_records(*A, c->img_in, c->img_pairs, (uint32_t)pn.size(), c->img_tmp, c->prm.B, c->stream);
+        e = launch_image_to_records(*A, c->img_in, c->img_pairs, (uint32_t)pn.size(), c->img_tmp, c->prm.B,
+                                    c->img_grid_y, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // h is read from the host stack
     return e == hipSuccess ? PVAC_OK : hip_fail(c, e, "chain images to records");
 }
@@ -1552,8 +1585,15 @@ int pvac_hip_check_mul_gsum(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "check_mul_gsum (sizes)");
     unsigned long long* cnt = (unsigned long long*)(c->check_buf + 4);
-    e = launch_check_gsum(*A, *B, *C, nonces, c->powg, c->prm.B, mx, status, cnt, c->num_cus, c->stream);
-    if (e == hipErrorInvalidValue) return fail(c, PVAC_ERANGE, "check_mul_gsum: a pair's layer tables exceed LDS");
+    // layer tables beyond one workgroup's LDS (chain depth 9 on): per-workgroup slabs in global memory
+    const uint64_t gs = check_gsum_scratch_bytes(c->prm.B, mx, A->n, c->num_cus);
+    if (gs) {
+        const int rc = ensure_dev(c, c->check_scratch, c->check_scratch_cap, (size_t)gs, "alloc gsum check scratch");
+        if (rc) return rc;
+    }
+    e = launch_check_gsum(*A, *B, *C, nonces, c->powg, c->prm.B, mx, status, cnt, c->num_cus, gs ? c->check_scratch : nullptr,
+                          c->stream);
+    if (e == hipErrorInvalidValue) return fail(c, PVAC_ERANGE, "check_mul_gsum: no scratch for the layer tables");
     unsigned long long bad = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, cnt, sizeof bad, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1713,8 +1753,7 @@ pvac_ct_batch chain_view(const pvac_ct_batch& X, uint64_t c0, uint64_t k) {
 
 // the inputs of one chunk copied into the worker's own buffers (compact CSR): counts by peer
 // copy, offsets by an exclusive scan, rows by k_stage_rows (peer reads when X lives elsewhere)
-bool stage_chunk(pvac_hip_ctx* k, chain_shared* sh, const pvac_ct_batch& src, pvac_ct_batch& out) {
-    chain_set& S = k->chain_stage;
+bool stage_chunk(pvac_hip_ctx* k, chain_shared* sh, const pvac_ct_batch& src, pvac_ct_batch& out, chain_set& S) {
     const uint64_t kk = src.n;
     auto hipchk = [&](hipError_t e, const char* where) {
         if (e == hipSuccess) return true;
@@ -1854,7 +1893,8 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
         if (c0 >= rg->end) return;
         const uint64_t kk = std::min<uint64_t>(sh->chunk, rg->end - c0);
         pvac_ct_batch Xv = chain_view(X, c0, kk);
-        if ((stage || remote) && !stage_chunk(k, sh, chain_view(X, c0, kk), Xv)) return;
+        if ((stage || remote) && !stage_chunk(k, sh, chain_view(X, c0, kk), Xv, k->chain_stage)) return;
+        const pvac_ct_batch X0 = Xv;   // the chunk's inputs: c_0, and the operand of steps without one
         pvac_ct_batch A = Xv;
         int cur = 0;
         uint32_t* a_img = nullptr;   // the previous step's image flags (A's)
@@ -1864,6 +1904,14 @@ void chain_worker(pvac_hip_ctx* k, chain_shared* sh, chain_range* rg, bool stage
         } img_guard{k};
         for (uint32_t d = 0; d < o.depth; ++d) {
             if (sh->stop.load()) return;
+            // this step's operand: operands[d] (the reference's loop multiplies by a fresh enc_value per
+            // step, tests/test_main.cpp:291-292) or the chunk's inputs
+            Xv = X0;
+            if (d < o.n_operands) {
+                Xv = chain_view(o.operands[d], c0, kk);
+                if ((stage || remote) && !stage_chunk(k, sh, chain_view(o.operands[d], c0, kk), Xv, k->chain_stage_op))
+                    return;
+            }
             chain_set& S = k->chain_bufs[cur];
             if (kk > S.n_cap) {
                 size_t c1 = S.n_cap, c2 = S.n_cap, c3 = S.n_cap, c4 = S.n_cap;
@@ -2006,8 +2054,16 @@ int pvac_hip_chain_partition(uint64_t n, uint64_t chunk, uint32_t parts, uint64_
 int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_chain_opts* o, pvac_chain_stats* st) {
     if (!c || !o || !st || !batch_ok(X)) return fail(c, PVAC_EINVAL, "ct_mul_chain: bad arguments");
     if (o->depth < 1 || o->depth > PVAC_CHAIN_MAX_DEPTH) return fail(c, PVAC_EINVAL, "ct_mul_chain: depth");
-    if (o->flags & ~(PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM | PVAC_MUL_WITH_SIGMA | PVAC_CHAIN_STAGE_INPUTS))
+    if (o->flags & ~(PVAC_MUL_ORDER_CANONICAL | PVAC_CHAIN_CHECK_GSUM | PVAC_MUL_WITH_SIGMA | PVAC_CHAIN_STAGE_INPUTS |
+                     PVAC_CHAIN_IMG_BATCH2))
         return fail(c, PVAC_EINVAL, "ct_mul_chain: flags");
+    if (o->n_operands > o->depth || (o->n_operands && !o->operands))
+        return fail(c, PVAC_EINVAL, "ct_mul_chain: operands");
+    for (uint32_t d = 0; d < o->n_operands; ++d) {
+        const pvac_ct_batch& Y = o->operands[d];
+        if (!batch_ok(&Y) || Y.n != X->n || (Y.n && (!Y.layers || !Y.meta || !Y.w_lo || !Y.w_hi)))
+            return fail(c, PVAC_EINVAL, "ct_mul_chain: operand " + std::to_string(d) + " is not a batch of |X| ciphers");
+    }
     if ((o->flags & PVAC_CHAIN_CHECK_GSUM) && !c->powg)
         return fail(c, PVAC_EINVAL, "ct_mul_chain: CHECK_GSUM needs pvac_hip_ctx_set_powg");
     if ((o->flags & PVAC_MUL_WITH_SIGMA) && !c->H.ready)
@@ -2026,26 +2082,23 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
     // inputs already enqueued on the caller's stream must be complete before other streams read them
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "ct_mul_chain (caller stream)");
-    // a layout change (streams, devices, chunk) first returns the workers' grown buffers and scratch
-    // arenas, so the HBM shares below are taken over the device's memory, not over what the previous
-    // layout's workers left free
-    const uint64_t layout[3] = {S, D, chunk};
-    if (!c->chain_kids.empty() && !std::equal(layout, layout + 3, c->chain_layout)) {
+    // a layout change (streams, chunk, the device list) first returns everything the workers grew
+    // (output batches, nonce / salt / result words, image scratch, scratch arenas), so the HBM shares
+    // below are taken over the device's memory, not over what the previous layout's workers left free
+    std::vector<int64_t> layout{(int64_t)S, (int64_t)chunk, (int64_t)D};
+    layout.insert(layout.end(), devs.begin(), devs.end());
+    if (!c->chain_kids.empty() && layout != c->chain_layout) {
         for (pvac_hip_ctx* k : c->chain_kids) {
             hipSetDevice(k->device);
-            free_chain_sets(k);
-            e = hipStreamSynchronize(k->stream);
+            e = release_chain_worker(k);
             if (e != hipSuccess) {
                 hipSetDevice(c->device);
                 return hip_fail(c, e, "ct_mul_chain: worker release");
             }
-            hipFree(k->arena);
-            k->arena = nullptr;
-            k->arena_words = 0;
         }
         hipSetDevice(c->device);
     }
-    std::copy(layout, layout + 3, c->chain_layout);
+    c->chain_layout = layout;
     // worker contexts: [range j * S + w] on devs[j]; a layout change rebuilds the ones that differ
     if (c->chain_kids.size() > (size_t)D * S) {
         for (size_t w = (size_t)D * S; w < c->chain_kids.size(); ++w) pvac_hip_ctx_destroy(c->chain_kids[w]);
@@ -2092,6 +2145,8 @@ int pvac_hip_ct_mul_chain(pvac_hip_ctx* c, const pvac_ct_batch* X, const pvac_ch
             }
             k->arena_cap_words = cap_words;
             k->prm = c->prm;
+            k->spin_us = 200;
+            k->img_grid_y = (o->flags & PVAC_CHAIN_IMG_BATCH2) ? 2u : 65535u;
             if (c->powg && (k->powg_n != c->powg_n || !k->powg)) {
                 hipFree(k->powg);
                 k->powg = nullptr;

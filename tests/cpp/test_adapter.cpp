@@ -153,6 +153,19 @@ static std::vector<uint64_t> read_u64(const std::string& p) {
     return v;
 }
 
+// every "[a, b]" pair that follows an occurrence of `key` in a manifest's text (the harness writes them)
+static std::vector<std::pair<size_t, size_t>> json_pairs(const std::string& js, const std::string& key) {
+    std::vector<std::pair<size_t, size_t>> out;
+    for (size_t at = js.find(key); at != std::string::npos; at = js.find(key, at + 1)) {
+        const size_t lb = js.find('[', at);
+        char* e = nullptr;
+        const size_t a = std::strtoull(js.c_str() + lb + 1, &e, 10);
+        const size_t b = std::strtoull(e + 1, nullptr, 10);
+        out.emplace_back(a, b);
+    }
+    return out;
+}
+
 // A .ct keeps BASE seeds and PROD parents only: project a full cipher the same way.
 static Cipher ct_view(Cipher c) {
     for (auto& L : c.L) {
@@ -581,6 +594,58 @@ int main(int argc, char** argv) {
                 MUST(pvac_hip::dec_value(pk, sk, c).lo == v, "dec_value(enc depth case %zu)", i);
             }
             MUST(i > 0, "no enc depth cases");
+        }
+        // the reference's own chain loop (tests/test_main.cpp:289-293, harness cmd_chainf): chain =
+        // enc_value(2), then chain = ct_mul(chain, enc_value(2)) with a FRESH operand per step, depth 4,
+        // replayed from its one interleaved stream (enc, mul, enc, mul, ...): (a) by value, the loop as
+        // the reference writes it (enc_value, then ct_mul with sigmas, step by step); (b) through the
+        // chain entry point with per-step operands (rnds carry the mul stretches only). Both give c_4
+        // byte-identical to the reference's (weights-only .ct, layer table, every sigma's digest).
+        {
+            const auto mb = slurp(ref + "/chainf_manifest.json");
+            const std::string man(mb.begin(), mb.end());
+            const auto stream = read_u64(ref + "/chainf_stream.u64");
+            const auto xst = json_pairs(man, "\"x_stream\"");
+            const auto encs = json_pairs(man, "\"enc_stream\""), muls = json_pairs(man, "\"mul_stream\"");
+            MUST(xst.size() == 1 && encs.size() == 4 && muls.size() == 4, "chainf manifest");
+            auto weights = [](Cipher c) {   // the fixture files are weights-only .ct
+                for (auto& E : c.E) E.s = mirror::BitVec{};
+                return ct_view(c);
+            };
+            auto stretch = [&](std::pair<size_t, size_t> p) {
+                MUST(p.first + p.second <= stream.size(), "chainf stretch");
+                return std::vector<uint64_t>(stream.begin() + (long)p.first, stream.begin() + (long)(p.first + p.second));
+            };
+            replay_pad rx{stretch(xst[0])};
+            const Cipher x = pvac_hip::enc_value<Cipher>(pk, sk, 2, std::ref(rx));
+            MUST(write_ct({weights(x)}) == slurp(ref + "/chainf_x.ct"), "chainf x .ct bytes");
+            Cipher c = x;
+            std::vector<std::vector<Cipher>> ys;
+            std::vector<uint64_t> mul_words;
+            for (size_t k = 0; k < 4; ++k) {
+                replay_pad ry{stretch(encs[k])};
+                const Cipher y = pvac_hip::enc_value<Cipher>(pk, sk, 2, std::ref(ry));
+                MUST(write_ct({weights(y)}) == slurp(ref + "/chainf_y" + std::to_string(k + 1) + ".ct"), "chainf y%zu", k + 1);
+                ys.push_back({y});
+                replay rm{stretch(muls[k])};
+                c = pvac_hip::ct_mul(pk, c, y, std::ref(rm));
+                MUST(rm.k == rm.s.size(), "chainf step %zu consumed %zu of %zu words", k + 1, rm.k, rm.s.size());
+                mul_words.insert(mul_words.end(), rm.s.begin(), rm.s.end());
+            }
+            MUST(write_ct({weights(c)}) == slurp(ref + "/chainf_final.ct"), "chainf c_4 weights .ct bytes (by value)");
+            const auto lay = read_u64(ref + "/chainf_final_layers.u64");
+            MUST(c.L.size() * 6 == lay.size(), "chainf layers %zu", c.L.size());
+            for (size_t l = 0; l < c.L.size(); ++l)
+                MUST(c.L[l].seed.ztag == lay[6 * l + 3] && c.L[l].seed.nonce.lo == lay[6 * l + 4], "chainf layer %zu", l);
+            const auto dig = read_u64(ref + "/chainf_final_sigdig.u64");
+            MUST(dig.size() == c.E.size(), "chainf sigma digests");
+            for (size_t e = 0; e < c.E.size(); ++e) MUST(sigma_digest(c.E[e].s.w) == dig[e], "chainf sigma %zu", e);
+            MUST(pvac_hip::dec_value(pk, sk, c).lo == 32, "chainf dec_value");
+            auto rp = std::make_shared<replay>(replay{mul_words});
+            std::vector<pvac_hip::RandomSource> rnds{[rp] { return (*rp)(); }};
+            const Cipher c2 = pvac_hip::ct_mul_chain(pk, std::vector<Cipher>{x}, ys, true, rnds)[0];
+            MUST(rp->k == mul_words.size(), "chainf chain entry consumed %zu of %zu words", rp->k, mul_words.size());
+            MUST(same_layers(c2, c) && same_edges(c2, c, true), "chainf c_4 (chain entry point) == by value");
         }
         // fresh randomness, batched both ways
         const auto cs = pvac_hip::enc_value_batch<Cipher>(pk, sk, vs);

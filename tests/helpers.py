@@ -239,6 +239,9 @@ class Oracle:
         lib.orc_ct_mul_chain_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 6 + \
             [C.c_int, C.c_int, u64p, u64p, u64p]
         lib.orc_ct_mul_chain_timed.restype = C.c_double
+        lib.orc_ct_mul_chain_ops_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 6 + \
+            [C.c_int, C.c_int] + [u64p] * 6 + [C.c_int, u64p, u64p, u64p]
+        lib.orc_ct_mul_chain_ops_timed.restype = C.c_double
         lib.orc_ct_add_batch_timed.argtypes = [C.POINTER(OrcParams), C.c_uint64] + [u64p] * 12 + \
             [C.c_int, C.c_int, u64p, u64p]
         lib.orc_ct_add_batch_timed.restype = C.c_double
@@ -487,3 +490,22 @@ def sumdigest(c):
         e = np.arange(c.nE, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
         v = m(m(m(e ^ c.meta) ^ c.w_lo) ^ c.w_hi)
         return int((v.sum(dtype=np.uint64) + np.uint64(c.nE)) & np.uint64(2**64 - 1))
+
+
+GOLDEN = 0x9E3779B97F4A7C15
+
+
+def splitmix_stream(seed, j0, n):
+    """Words j0 .. j0 + n - 1 of the harness' interposed getrandom stream after reseed(seed)
+    (oracle/ref_harness.cpp: word j = splitmix64(seed + (j + 1) * golden)); equal to
+    pvac_hip_fill_random(seed + j0 * golden, n) on the device."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (np.arange(j0 + 1, j0 + n + 1, dtype=np.uint64) * np.uint64(GOLDEN))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
+
+
+def stream_seed(seed, j0):
+    """pvac_hip_fill_random seed whose output starts at word j0 of splitmix_stream(seed, ...)."""
+    return (int(seed) + int(j0) * GOLDEN) & (2**64 - 1)

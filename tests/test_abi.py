@@ -42,7 +42,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version(lib):
     lib.pvac_hip_abi_version.restype = C.c_int
-    assert lib.pvac_hip_abi_version() == 2
+    assert lib.pvac_hip_abi_version() == 3
 
 
 def test_python_binding_covers_abi():

@@ -162,12 +162,14 @@ def test_chain_api_callbacks_and_errors():
 
 
 def test_reference_chain_2_pow_10_on_gpu(oracle):
-    """The reference's own end-to-end chain check (tests/test_main.cpp:289-293: enc_value(2), nine
-    ct_mul steps, dec_value == 2^10), all on the GPU through the chain entry point: x = enc_value(2)
-    per chain (GPU PRF), c_0 = x, c_k = ct_mul(c_{k-1}, x) for 9 steps through pvac_hip_ct_mul_chain
-    (step 9's A operands hold ~340 K edges, its outputs ~690 K), the final ciphers taken from the
-    on_chunk callback, then base_R (prf_R of the BASE layers) and dec_value: every chain decrypts to
-    2^10. The depth-9 digests and edge counts equal the CPU port's on the same inputs."""
+    """The reference's own end-to-end chain check, as its loop is written (tests/test_main.cpp:289-293:
+    chain = enc_value(2), then nine times chain = ct_mul(chain, enc_value(2)), dec_value == 2^10), all
+    on the GPU through the chain entry point: x and a FRESH enc_value(2) operand per step (GPU PRF, ten
+    independent encryptions per chain) passed as per-step operands (pvac_chain_opts.operands), nine
+    steps through pvac_hip_ct_mul_chain with its dense-image intermediate steps (step 9's A operands hold
+    ~345 K edges, its outputs ~690 K), the final ciphers taken from the on_chunk callback, then base_R
+    (prf_R of the BASE layers) and dec_value: every chain decrypts to 2^10. The depth-9 digests and edge
+    counts equal the CPU port's chains over the same operands (orc_ct_mul_chain_ops_timed)."""
     import threading
     from pvac_hfhe_cppbyv_amd import ON_CHUNK_CB, DeviceBatch, Engine, HostCipher
     from helpers import hip_batch_to_host
@@ -181,6 +183,11 @@ def test_reference_chain_2_pow_10_on_gpu(oracle):
     n, depth = 4, 9
     X, st = eng.enc_value(np.full(n, 2, np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
     assert not st.any()
+    ops = []
+    for _ in range(depth):
+        Y, st = eng.enc_value(np.full(n, 2, np.uint64), rng.integers(0, 2**64, (n, 256), dtype=np.uint64))
+        assert not st.any()
+        ops.append(Y)
     lock = threading.Lock()
     finals = {}
 
@@ -191,10 +198,15 @@ def test_reference_chain_2_pow_10_on_gpu(oracle):
                 finals[first + i] = c
         return 0
 
-    r = eng.ct_mul_chain(X, depth, nonce_seed=0x2A11, streams=2, chunk=2, digest_n=n,
+    r = eng.ct_mul_chain(X, depth, nonce_seed=0x2A11, streams=2, chunk=2, digest_n=n, operands=ops,
                          on_chunk=ON_CHUNK_CB(keep))
-    # (no gsum check here: check_mul_gsum's LDS layer tables stop at depth 8's layer counts; the
-    # decryption and the digests below are the stronger checks)
+    assert r["image_steps"] > 0 and r["redo"] == 0   # the image fast path holds with fresh operands
+    # the reference's gsum invariant on every pair-step, depth 9 included (step 9's layer tables exceed
+    # a workgroup's LDS: k_check_gsum runs over global slabs), records throughout: the same chains
+    chk = eng.ct_mul_chain(X, depth, nonce_seed=0x2A11, streams=2, chunk=2, digest_n=n, operands=ops,
+                           check_gsum=True)
+    assert chk["gsum_pairs"] == n * depth and chk["gsum_failed"] == 0 and chk["image_steps"] == 0
+    assert np.array_equal(chk["digests"], r["digests"]) and np.array_equal(chk["counts"], r["counts"])
     assert sorted(finals) == list(range(n))
     assert min(c.nE for c in finals.values()) > 600000   # step 9 on the GPU: ~690 K-edge ciphers
     cs = [finals[i] for i in range(n)]
@@ -203,12 +215,18 @@ def test_reference_chain_2_pow_10_on_gpu(oracle):
     assert not dst.any()
     assert vals == [1 << 10] * n
     px = pack_device_batch(X, n)
+    po = [pack_device_batch(Y, n) for Y in ops]
+    cat = lambda k: np.ascontiguousarray(np.concatenate([p[k] for p in po]))
+    eoff = lambda k: np.ascontiguousarray(np.concatenate([[0]] + [p[k][1:] + sum(int(q[k][-1]) for q in po[:j])
+                                                                  for j, p in enumerate(po)]).astype(np.uint64))
+    oops = (eoff(0), cat(1), eoff(2), cat(3), cat(4), cat(5))
     P_ = lambda a: a.ctypes.data_as(C.c_void_p)
     ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
-    oracle.lib.orc_ct_mul_chain_timed(C.byref(default_params(man["canon_tag"])), n, *(P_(a) for a in px), depth, 8,
-                                      P_(ocnt), P_(odig), P_(se))
+    oracle.lib.orc_ct_mul_chain_ops_timed(C.byref(default_params(man["canon_tag"])), n, *(P_(a) for a in px), depth,
+                                          depth, *(P_(a) for a in oops), 8, P_(ocnt), P_(odig), P_(se))
     assert np.array_equal(ocnt, r["counts"]) and np.array_equal(odig, r["digests"])
     assert np.array_equal(ocnt, np.array([c.nE for c in cs], np.uint64))
+    assert [int(v) for v in se] == r["edges"]
 
 
 def test_chain_two_device_ranges_equal_one_device():
@@ -423,3 +441,229 @@ def test_chain_images_with_four_b_layers(oracle):
     assert np.array_equal(img["digests"], dig) and np.array_equal(img["counts"], cnt) and img["edges"] == edges
     ocnt, odig = _oracle_chain(oracle, X, n, depth, tag, B=Bm)
     assert np.array_equal(ocnt, cnt) and np.array_equal(odig, dig)
+
+
+def _chainf_on_gpu(eng, man, depth, n, powg, images=True):
+    """ref_harness chainf / chainf8 on the GPU through the chain entry point: x and every operand
+    encrypted by the GPU enc_value from their stretches of the regenerated stream (device splitmix,
+    pvac_hip_fill_random at the stretch's offset), the operands passed per step, each step's nonces from
+    the head of its mul stretch (nonces_at) and the final step's salts from the rest (salts_at), sigmas
+    on the final step. n copies of the chain run in one call (2 streams, chunks of 1). Returns the
+    final ciphers (with sigmas) and the call's statistics."""
+    import threading
+    import torch
+    from pvac_hfhe_cppbyv_amd import ON_CHUNK_CB, STEP_CB
+    from helpers import hip_batch_to_host, hip_d2h_u64, hip_h2d, splitmix_stream, stream_seed
+    S = man["seed"]
+    stride = eng.enc_caps()[2]
+
+    def enc_stretch(j0, ln):
+        assert ln <= stride
+        rnd = torch.empty(stride, dtype=torch.int64, device=eng.device)
+        eng.fill_random(rnd, stream_seed(S, j0))   # the device generator at the stretch's offset
+        assert np.array_equal(rnd.cpu().numpy().view(np.uint64), splitmix_stream(S, j0, stride))
+        Y, st = eng.enc_value(np.full(n, 2, np.uint64), rnd.repeat(n).reshape(n, stride))
+        assert not st.any()
+        return Y
+
+    X = enc_stretch(*man["x_stream"])
+    ops = [enc_stretch(*rec["enc_stream"]) for rec in man["steps"][:depth]]
+    lock = threading.Lock()
+    finals = {}
+
+    def nonces_at(user, step, first, A, Xb, Cb, words, nw, stream):
+        rec = man["steps"][step]
+        m0, nn = rec["mul_stream"][0], rec["nonce_words"]
+        k = Cb.contents.n
+        la, lx = hip_d2h_u64(A.contents.l_cnt, k, stream), hip_d2h_u64(Xb.contents.l_cnt, k, stream)
+        lo = hip_d2h_u64(Cb.contents.l_off, k, stream)
+        w = np.zeros(int(nw), np.uint64)
+        for i in range(k):
+            assert 2 * int(la[i]) * int(lx[i]) == nn
+            s0 = 2 * int(lo[i] + la[i] + lx[i])
+            w[s0:s0 + nn] = splitmix_stream(S, m0, nn)
+        hip_h2d(words, w, stream)
+        return 0
+
+    def salts_at(user, step, first, A, Xb, Cb, words, nw, stream):
+        rec = man["steps"][step]
+        m0, nn = rec["mul_stream"][0], rec["nonce_words"]
+        k = Cb.contents.n
+        ec, eo = hip_d2h_u64(Cb.contents.e_cnt, k, stream), hip_d2h_u64(Cb.contents.e_off, k, stream)
+        w = np.zeros(int(nw), np.uint64)
+        for i in range(k):
+            assert int(ec[i]) == rec["edges"]
+            w[int(eo[i]):int(eo[i]) + int(ec[i])] = splitmix_stream(S, m0 + nn, int(ec[i]))
+        hip_h2d(words, w, stream)
+        return 0
+
+    def keep(user, first, cb, stream):
+        cs = hip_batch_to_host(cb.contents, stream, sigma_words=128)
+        with lock:
+            for i, c in enumerate(cs):
+                finals[first + i] = c
+        return 0
+
+    hooks = dict(nonces_at=STEP_CB(nonces_at), salts_at=STEP_CB(salts_at), on_chunk=ON_CHUNK_CB(keep))
+    if not images:
+        hooks["after_step"] = STEP_CB(lambda *a: 0)
+    r = eng.ct_mul_chain(X, depth, streams=2, chunk=1, sigma=True, operands=ops, digest_n=n, **hooks)
+    return [finals[i] for i in range(n)], r
+
+
+def _chainf_check(oracle, eng, man, depth, cs, powg):
+    """c_depth against the fixture: edges, layers, commit_ct with sigmas and of the weights only."""
+    from helpers import Cipher as HC
+    import json
+    import os
+    from helpers import REF
+    with open(os.path.join(REF, "manifest.json")) as f:
+        Hd = bytes.fromhex(json.load(f)["H_digest"])
+    rec = man["steps"][depth - 1]
+    for c in cs:
+        assert c.nE == rec["edges"] and c.nL == rec["layers"]
+        assert oracle.commit(c, man["canon_tag"], Hd).hex() == rec["commit"], depth
+        assert oracle.commit(HC(c.layers, c.meta, c.w_lo, c.w_hi), man["canon_tag"], Hd).hex() == rec["commit_weights"]
+
+
+def _chainf_engine(name):
+    import json
+    import os
+    from pvac_hfhe_cppbyv_amd import Engine
+    from helpers import REF
+    with open(os.path.join(REF, f"{name}_manifest.json")) as f:
+        man = json.load(f)
+    sk, m0, em = fixture_secret()
+    eng = Engine(device=0, canon_tag=man["canon_tag"])
+    assert eng.gen_H().hex() == m0["H_digest"]
+    eng.set_secret(read_u64("sk_prf_k.u64"), read_u64("sk_lpn_s.u64"), em["lpn_n"], em["lpn_t"], em["lpn_tau_num"],
+                   em["lpn_tau_den"])
+    powg = read_u64("powg_B.u64")
+    eng.set_powg(powg)
+    return eng, man, powg
+
+
+def test_chainf_reference_loop_replay_on_gpu(oracle):
+    """The reference's own chain loop with a fresh enc_value(2) per step (tests/test_main.cpp:289-293,
+    ref_harness chainf, depth 4, full stream) through the chain entry point's per-step operands: for
+    every depth k = 1..4 a chain call of depth k gives c_k whose commit_ct (with sigmas, and of the
+    weights alone) equals the reference's; c_4's weights-only .ct bytes, layer table and per-edge sigma
+    digests equal the fixture files, and it decrypts to 2^5 on the GPU. Two copies per call."""
+    import hashlib
+    import os
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, HostCipher
+    from helpers import REF, Cipher as HC, read_layers_u64
+    from helpers import write_ct
+    eng, man, powg = _chainf_engine("chainf")
+    for k in range(1, man["depth"] + 1):
+        cs, r = _chainf_on_gpu(eng, man, k, 2, powg)
+        assert r["redo"] == 0
+        _chainf_check(oracle, eng, man, k, cs, powg)
+    c = cs[0]
+    with open(os.path.join(REF, "chainf_final.ct"), "rb") as f:
+        assert write_ct([HC(c.layers, c.meta, c.w_lo, c.w_hi)]) == f.read()
+    lay = read_layers_u64("chainf_final_layers.u64")
+    for fld in ("rule", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(c.layers[fld], lay[fld])
+    dig = np.array([int.from_bytes(hashlib.sha256(s.astype("<u8").tobytes()).digest()[:8], "little")
+                    for s in c.sigma], np.uint64)
+    assert np.array_equal(dig, read_u64("chainf_final_sigdig.u64"))
+    F = DeviceBatch.from_host([HostCipher(c.layers, c.meta, c.w_lo, c.w_hi, None)], eng.device)
+    vals, st = eng.dec_value(F, eng.base_R(F))
+    assert not st.any() and vals == [32]
+
+
+def test_chainf8_reference_loop_depth8_on_gpu(oracle):
+    """The same loop to depth 8 (ref_harness chainf8: steps 5-8 are the dense / direct-mode / image
+    regime, c_8 holds 345,088 edges), pinned to the reference's own per-step commit_ct digests: a chain
+    call of depth k for every k = 1..8 through the per-step operands, with the dense images between
+    steps 3 .. k-1, gives c_k whose commit (with sigmas, and of the weights alone) equals the
+    reference's; the depth-8 call with records throughout (an after_step hook) gives the same c_8; c_8
+    decrypts to 2^9 on the GPU."""
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, HostCipher
+    eng, man, powg = _chainf_engine("chainf8")
+    assert man["depth"] == 8
+    for k in range(1, 9):
+        cs, r = _chainf_on_gpu(eng, man, k, 1, powg)
+        assert r["redo"] == 0
+        if k >= 4:
+            assert r["image_steps"] == k - 3   # steps 3 .. k - 1 handed on as images
+        _chainf_check(oracle, eng, man, k, cs, powg)
+    rec_cs, r = _chainf_on_gpu(eng, man, 8, 1, powg, images=False)
+    assert r["image_steps"] == 0
+    _chainf_check(oracle, eng, man, 8, rec_cs, powg)
+    c = cs[0]
+    F = DeviceBatch.from_host([HostCipher(c.layers, c.meta, c.w_lo, c.w_hi, None)], eng.device)
+    vals, st = eng.dec_value(F, eng.base_R(F))
+    assert not st.any() and vals == [512]
+
+
+def _three_layer_ciphers(rng, k, epl=20, B=337):
+    """k host ciphers of 3 BASE layers x epl distinct (idx, ch) cells (3 epl <= 63 edges: the direct
+    mode's per-A-edge masks), weights canonical and nonzero."""
+    from pvac_hfhe_cppbyv_amd import HostCipher
+    from helpers import LAYER_DT
+    out = []
+    for _ in range(k):
+        L = np.zeros(3, LAYER_DT)
+        L["ztag"], L["nonce_lo"], L["nonce_hi"] = (rng.integers(0, 2**63, 3, dtype=np.uint64) for _ in range(3))
+        meta = []
+        for l in range(3):
+            for c in rng.choice(2 * B, epl, replace=False):
+                meta.append(l | (int(c % B) << 32) | (int(c // B) << 48))
+        ne = len(meta)
+        out.append(HostCipher(L, np.array(meta, np.uint64), rng.integers(1, 2**64, ne, dtype=np.uint64),
+                              rng.integers(0, 2**62, ne, dtype=np.uint64)))
+    return out
+
+
+def test_chain_image_redo_of_mixed_sizes(oracle):
+    """ADVICE r5 (k_img_copy / k_img_scatter batching): image inputs of DIFFERENT sizes turned back into
+    records in one exec, in launches of two pairs (PVAC_CHAIN_IMG_BATCH2). Four chains in one chunk:
+    pairs 0, 1 multiply by 2-layer operands at step 1, pairs 2, 3 by 3-layer ones, later steps by x, so
+    from step 3 on the second pair group's dense images hold more product layers. edge_budget sits
+    between every step-4 and every step-5 output: steps 3 and 4 hand C on as images, and at step 5 all
+    four pairs leave the direct mode, so their images (small, small, large, large) are converted in two
+    launches. Digests and counts equal the record-only run (after_step hook), the call without the
+    small launches, and the CPU port's chains with the same operands and budget."""
+    import ctypes
+    from pvac_hfhe_cppbyv_amd import STEP_CB, DeviceBatch, Engine
+    rng = np.random.default_rng(0x1A6B)
+    tag = 0x1A6B
+    n, depth = 4, 6
+    probe = Engine(device=0, canon_tag=tag)
+    X = probe.gen_fresh(n, 0x1A6C, 20)
+    xs = X.to_host()
+    y3 = _three_layer_ciphers(rng, 2)
+    ops_h = [xs[0], xs[1], y3[0], y3[1]]
+    # step sizes of both groups from the CPU port: the budget goes between steps 4 and 5
+    sizes = []
+    for i in (0, 2):
+        c = Cipher(xs[i].layers, xs[i].meta, xs[i].w_lo, xs[i].w_hi)
+        row = []
+        for d in range(depth):
+            y = ops_h[i] if d == 0 else xs[i]
+            y = Cipher(y.layers, y.meta, y.w_lo, y.w_hi)
+            c = oracle.ct_mul(c, y, np.zeros(2 * c.nL * y.nL, np.uint64), canon_tag=tag)
+            row.append(c.nE)
+        sizes.append(row)
+    budget = max(sizes[0][3], sizes[1][3])
+    assert min(sizes[0][4], sizes[1][4]) > budget and sizes[1][2] != sizes[0][2]
+    eng = Engine(device=0, canon_tag=tag, edge_budget=budget)
+    X = DeviceBatch.from_host(xs, eng.device)
+    Y = DeviceBatch.from_host(ops_h, eng.device)
+    kw = dict(nonce_seed=0x1A6D, streams=1, chunk=n, digest_n=n, operands=[Y])
+    img2 = eng.ct_mul_chain(X, depth, img_batch2=True, **kw)
+    assert img2["image_steps"] == 2 * n and img2["redo"] >= 2 * n   # images: steps 3, 4; redone: 5, 6
+    img = eng.ct_mul_chain(X, depth, **kw)
+    rec = eng.ct_mul_chain(X, depth, after_step=STEP_CB(lambda *a: 0), **kw)
+    assert rec["image_steps"] == 0
+    for r in (img, rec):
+        assert np.array_equal(img2["digests"], r["digests"]) and np.array_equal(img2["counts"], r["counts"])
+    assert [int(v) for v in img2["counts"]] == [sizes[0][-1]] * 2 + [sizes[1][-1]] * 2
+    px, po = pack_device_batch(X, n), pack_device_batch(Y, n)
+    P_ = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ocnt, odig, se = np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(depth, np.uint64)
+    oracle.lib.orc_ct_mul_chain_ops_timed(ctypes.byref(default_params(tag, edge_budget=budget)), n, *(P_(a) for a in px),
+                                          depth, 1, *(P_(a) for a in po), 4, P_(ocnt), P_(odig), P_(se))
+    assert np.array_equal(ocnt, img2["counts"]) and np.array_equal(odig, img2["digests"])

@@ -475,20 +475,18 @@ def _pair_host(X, p):
     return Cipher(layers, u(X.meta[eo:eo + ec]).copy(), u(X.w_lo[eo:eo + ec]).copy(), u(X.w_hi[eo:eo + ec]).copy())
 
 
-def test_cfg3_full_batch_sampled_vs_oracle(oracle):
-    """BASELINE cfg 3 at its full size (2^20 fresh-shaped pairs, the bench's batch and generator):
-    every reported output slot written by this launch (sentinel-filled outputs), every pair's
-    edges equal to the pinned CPU port's (per-pair digests, all 2^20), the reference's
-    gsum invariant on every pair, 512 pairs spread over the whole batch bit-exact
-    vs the oracle (weights, emit order, layers incl. ztags), every pair within its planned capacity
-    with status 0, and a second run of the same batch identical (per-pair device digests)."""
+def _full_batch_vs_oracle(oracle, n, first, n_picks, rerun):
+    """One full batch of the bench's generator at global pair indices [first, first + n): every
+    reported output slot written by this launch (sentinel-filled outputs), every pair's edges equal to
+    the pinned CPU port's (per-pair digests), the reference's gsum invariant on every pair, n_picks
+    pairs spread over the batch bit-exact vs the oracle (weights, emit order, layers incl. ztags),
+    every pair within its planned capacity with status 0, and (rerun) a second run identical."""
     from pvac_hfhe_cppbyv_amd import Engine
     eng = Engine(device=0, canon_tag=0x5EED0003)
-    n = 1 << 20
-    A = eng.gen_fresh(n, 0x5EED0003, 20)
-    B = eng.gen_fresh(n, 0x5EED0004, 20)
+    A = eng.gen_fresh(n, 0x5EED0003, 20, first_index=first)
+    B = eng.gen_fresh(n, 0x5EED0004, 20, first_index=first)
     Cb, plan = eng.ct_mul_plan(A, B)
-    nonces = eng.fill_nonces(A, B, Cb, plan, 0x5EED0005)
+    nonces = eng.fill_nonces(A, B, Cb, plan, 0x5EED0005, first_index=first)
     # outputs pre-filled with a sentinel no record can hold (meta ch byte, w_hi top bit): every
     # reported edge and layer slot must have been written by this launch, not left from an earlier one
     torch = eng.torch
@@ -496,6 +494,8 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     Cb.layers = torch.full((ls, 5), -1, dtype=torch.int64, device=eng.device)
     Cb.meta, Cb.w_lo, Cb.w_hi = (torch.full((es,), -1, dtype=torch.int64, device=eng.device) for _ in range(3))
     out = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan)
+    assert eng.ct_mul_redo_count() == 0
+    assert not eng.ct_mul_status(n).any()   # every pair in the reference's hash order
     tot_e, tot_l = int(out.e_cnt[:n].sum().item()), int(out.l_cnt[:n].sum().item())
     for t in (out.meta, out.w_lo, out.w_hi):
         assert int((t != -1).sum().item()) == tot_e
@@ -518,11 +518,11 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
     bad = np.nonzero(dig != dig1)[0]
     assert bad.size == 0, f"{bad.size} pairs differ from the oracle, first {bad[:8]}"
     del pa, pb
-    # the reference's gsum invariant (utils/metrics.hpp:88-113) on every one of the 2^20 pairs
+    # the reference's gsum invariant (utils/metrics.hpp:88-113) on every pair
     eng.set_powg(read_u64("powg_B.u64"))
     assert eng.check_mul_gsum(A, B, out, nonces) == 0
     rng = np.random.default_rng(3)
-    picks = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 510)]))
+    picks = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, n_picks - 2)]))
     nz = nonces.cpu().numpy().view(np.uint64)
     loff = u(Cb.l_off[:n])
     for p in picks:
@@ -530,11 +530,40 @@ def test_cfg3_full_batch_sampled_vs_oracle(oracle):
         base = int(loff[p]) + x.nL + y.nL
         ref = oracle.ct_mul(x, y, nz[2 * base:2 * base + 2 * x.nL * y.nL], canon_tag=0x5EED0003)
         _assert_same(_pair_host(out, int(p)), ref, layers_view=False)
+    if not rerun:
+        return dig1
     del out, Cb   # two 2^20-pair outputs together are ~140 GB
     eng.torch.cuda.empty_cache()
     Cb2, plan2 = eng.ct_mul_plan(A, B)
     out2 = eng.ct_mul(A, B, nonces=nonces, C_=Cb2, plan=plan2)
     assert np.array_equal(u(eng.digest(out2)[:n]), dig1)
+    return dig1
+
+
+def test_cfg3_full_batch_sampled_vs_oracle(oracle):
+    """BASELINE cfg 3 at its full size (2^20 fresh-shaped pairs, the bench's batch and generator):
+    the full-batch checks of _full_batch_vs_oracle, 512 pairs bit-exact, a rerun identical."""
+    _full_batch_vs_oracle(oracle, 1 << 20, 0, 512, rerun=True)
+
+
+def test_cfg5_rank7_shard_vs_oracle(oracle):
+    """BASELINE cfg 5's per-GPU work: the last rank's shard of the 8-GPU job, alone on this GPU —
+    2^21 pairs at global indices [7 * 2^21, 2^24) from the bench's generator and nonces (bench.py at
+    --gpus 8 hands rank 7 exactly this), ~136 GB of output capacity: every slot written, every pair's
+    digest equal to the pinned port's, the gsum invariant on every pair, 256 pairs bit-exact vs the
+    oracle, status and capacities. Its digests also equal the same global pairs cut from a batch that
+    starts at another offset (the shard is keyed by global index only)."""
+    n, first = 1 << 21, 7 << 21
+    dig = _full_batch_vs_oracle(oracle, n, first, 256, rerun=False)
+    from pvac_hfhe_cppbyv_amd import Engine
+    eng = Engine(device=0, canon_tag=0x5EED0003)
+    k, off = 4096, (7 << 21) + (1 << 20)   # 4,096 pairs from the middle of the shard, generated alone
+    A = eng.gen_fresh(k, 0x5EED0003, 20, first_index=off)
+    B = eng.gen_fresh(k, 0x5EED0004, 20, first_index=off)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    nz = eng.fill_nonces(A, B, Cb, plan, 0x5EED0005, first_index=off)
+    o = eng.ct_mul(A, B, nonces=nz, C_=Cb, plan=plan)
+    assert np.array_equal(eng.digest(o)[:k].cpu().numpy().view(np.uint64), dig[off - first:off - first + k])
 
 
 @pytest.mark.parametrize("s", [2, P - 1, (0x0123456789ABCDEF << 64) | 0xFEDCBA9876543210])

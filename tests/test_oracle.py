@@ -329,3 +329,106 @@ def test_chainx_fixture_replay(oracle, manifest, H_dense):
     assert np.array_equal(got, dig)
     R = R_for(c, [(x, read_u64("chainx_x_R.u64"))])
     assert list(oracle.dec(c, read_u64("powg_B.u64"), R)) == man["dec"] == [32, 0]
+
+
+def _chainf(name):
+    import json
+    with open(os.path.join(REF, f"{name}_manifest.json")) as f:
+        return json.load(f)
+
+
+def _weights(c):
+    return Cipher(c.layers, c.meta, c.w_lo, c.w_hi)
+
+
+def _chainf_replay(oracle, man, H, sk, powg, sigma_steps):
+    """The port replaying ref_harness chainf / chainf8 (the reference's own loop, tests/test_main.cpp:
+    289-293: x = enc_value(2), c_k = ct_mul(c_{k-1}, enc_value(2))): every operand encrypted from its
+    stretch of the regenerated getrandom stream, every step's nonces from the head of its mul stretch.
+    Checks |E|, |L| and the sigma-less commit_ct of every step, and the commit with sigmas (salts from
+    the rest of the stretch) for the steps in sigma_steps. Returns (x, operands, c_depth weights-only,
+    c_depth with sigmas or None)."""
+    from helpers import splitmix_stream
+    S, tag = man["seed"], man["canon_tag"]
+    Hd = bytes.fromhex(_man_H_digest())
+    j0, n = man["x_stream"]
+    x, used = oracle.enc_value(sk, 2, splitmix_stream(S, j0, n), powg, canon_tag=tag)
+    assert used == n
+    c, ys, full = _weights(x), [], None
+    for k, rec in enumerate(man["steps"], start=1):
+        e0, en = rec["enc_stream"]
+        y, used = oracle.enc_value(sk, 2, splitmix_stream(S, e0, en), powg, canon_tag=tag)
+        assert used == en
+        y = _weights(y)
+        ys.append(y)
+        m0, mn = rec["mul_stream"]
+        nn = rec["nonce_words"]
+        assert nn == 2 * c.nL * y.nL
+        words = splitmix_stream(S, m0, mn)
+        if k in sigma_steps:
+            full = oracle.ct_mul(c, y, words[:nn], salts=words[nn:], H=H, canon_tag=tag)
+            assert oracle.commit(full, tag, Hd).hex() == rec["commit"], k
+        c = oracle.ct_mul(c, y, words[:nn], canon_tag=tag)
+        assert c.nE == rec["edges"] and c.nL == rec["layers"] and nn + c.nE == mn, k
+        assert oracle.commit(c, tag, Hd).hex() == rec["commit_weights"], k
+    return x, ys, c, full
+
+
+def _man_H_digest():
+    import json
+    with open(os.path.join(REF, "manifest.json")) as f:
+        return json.load(f)["H_digest"]
+
+
+def test_chainf_fixture_replay(oracle, H_dense):
+    """ref_harness chainf: the reference's own chain loop with a FRESH enc_value(2) operand per step
+    (tests/test_main.cpp:291-292), depth 4, one interleaved getrandom stream (enc, mul, enc, ...).
+    The stream regenerated from its seed equals the committed stream; the port's enc_value reproduces
+    x and every operand from their stretches; every step's commit_ct with and without sigmas; c_4's
+    weights-only .ct bytes, layer table, sigma digests and decryption (2^5 = 32)."""
+    import hashlib
+    from helpers import R_for, fixture_secret, splitmix_stream
+    man = _chainf("chainf")
+    sk, _, _ = fixture_secret()
+    powg = read_u64("powg_B.u64")
+    stream = read_u64("chainf_stream.u64")
+    assert len(stream) == man["stream"] and np.array_equal(splitmix_stream(man["seed"], 0, len(stream)), stream)
+    x, ys, c, full = _chainf_replay(oracle, man, H_dense, sk, powg, sigma_steps=range(1, 5))
+    for name, got in [("x", x)] + [(f"y{k}", y) for k, y in enumerate(ys, start=1)]:
+        with open(os.path.join(REF, f"chainf_{name}.ct"), "rb") as f:
+            assert write_ct([got]) == f.read(), name
+    with open(os.path.join(REF, "chainf_final.ct"), "rb") as f:
+        assert write_ct([c]) == f.read()
+    lay = read_layers_u64("chainf_final_layers.u64")
+    for fld in ("rule", "ztag", "nonce_lo", "nonce_hi"):
+        assert np.array_equal(full.layers[fld], lay[fld])
+    dig = np.array([int.from_bytes(hashlib.sha256(s.astype("<u8").tobytes()).digest()[:8], "little")
+                    for s in full.sigma], np.uint64)
+    assert np.array_equal(dig, read_u64("chainf_final_sigdig.u64"))
+    R = _base_R(oracle, sk, man["canon_tag"], c)
+    assert list(oracle.dec(c, powg, R)) == man["dec"] == [32, 0]
+
+
+def _base_R(oracle, sk, tag, c):
+    """prf_R of every BASE layer of c (2 words per layer slot, 0 for PROD layers)."""
+    R = np.zeros(2 * c.nL, np.uint64)
+    for i, L in enumerate(c.layers):
+        if L["rule"] == 0:
+            R[2 * i:2 * i + 2] = oracle.prf_R(sk, tag, (L["ztag"], L["nonce_lo"], L["nonce_hi"]))
+    return R
+
+
+def test_chainf8_fixture_digests(oracle, H_dense):
+    """ref_harness chainf8: the same loop to depth 8 (steps 5-8: dense layers, the direct-mode regime,
+    c_8 with 345,088 edges), pinned by the reference's per-step commit_ct digests. The port reproduces
+    every step's sigma-less commit (weights, layers incl. nonces / ztags, emit order) and the commit
+    with sigmas of steps 1-5, and c_8 decrypts to 2^9."""
+    from helpers import fixture_secret
+    man = _chainf("chainf8")
+    sk, _, _ = fixture_secret()
+    powg = read_u64("powg_B.u64")
+    assert man["depth"] == 8
+    _, _, c, _ = _chainf_replay(oracle, man, H_dense, sk, powg, sigma_steps=range(1, 6))
+    assert c.nE == 345088
+    R = _base_R(oracle, sk, man["canon_tag"], c)
+    assert list(oracle.dec(c, powg, R)) == man["dec"] == [512, 0]
