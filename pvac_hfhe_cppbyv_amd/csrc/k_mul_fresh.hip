@@ -268,8 +268,8 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
                 m = (pa < Lc ? 1ull << pa : 0ull) | (pb < Lc ? 1ull << pb : 0ull);
             }
         } else {
-            const uint32_t lp = t - base;   // < 64: float quotient is exact after floor
-            const uint32_t la = (uint32_t)__float2uint_rd(((float)lp + 0.5f) / (float)h.LB);
+            const uint32_t lp = t - base;   // < 64: lp / LB by multiply-shift (exact for lp < 2^16 / LB)
+            const uint32_t la = (lp * ((65536u + h.LB - 1u) / h.LB)) >> 16;
             m = (1ull << la) | (1ull << (h.LA + lp - la * h.LB));
         }
         pm[t] = m;
@@ -813,16 +813,22 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
         {
             // 32-bit LDS byte offsets (no 64-bit address arithmetic): a cell word's low half, limb 2
             // of a position
-            const uint32_t tkb = Ls.tkey, lmb = Ls.lim + 16u;
-            auto emit = [&](uint32_t m, uint32_t e, uint32_t p) {   // slot m's cells at p (P), p + (P present) (M)
+            // (LDS pointers: 32-bit address arithmetic, no 64-bit mad per store)
+            typedef __attribute__((address_space(3))) uint8_t lds8;
+            lds8* const L3 = (lds8*)lds;
+            const uint32_t tkb = Ls.tkey, lmb = Ls.lim + 20u;   // limb 2's HIGH dword of position 0
+            // slot m's cells at p (P), p + (P present) (M). Limb 2 of a position holds the cell id at
+            // bit 52: only its high dword is written (cell << 20), the limbs being zero between pairs
+            auto emit = [&](uint32_t m, uint32_t e, uint32_t p) {
+                const uint32_t ca = tkb + 8u * m, la = lmb + 24u * p;
                 if (e & 1u) {
-                    *(uint16_t*)(lds + (tkb + 8u * m)) = (uint16_t)p;
-                    *(unsigned long long*)(lds + (lmb + 24u * p)) = (unsigned long long)(2u * m) << 52;
-                    ++p;
+                    *(__attribute__((address_space(3))) uint16_t*)(L3 + ca) = (uint16_t)p;
+                    *(__attribute__((address_space(3))) uint32_t*)(L3 + la) = m << 21;
                 }
                 if (e & 2u) {
-                    *(uint16_t*)(lds + (tkb + 8u * m + 4u)) = (uint16_t)p;
-                    *(unsigned long long*)(lds + (lmb + 24u * p)) = (unsigned long long)(2u * m + 1u) << 52;
+                    const uint32_t pp = e & 1u;
+                    *(__attribute__((address_space(3))) uint16_t*)(L3 + ca + 4u) = (uint16_t)(p + pp);
+                    *(__attribute__((address_space(3))) uint32_t*)(L3 + la + 24u * pp) = (m << 21) | (1u << 20);
                 }
             };
             // emit offset of bucket time tb: in-segment suffix offset + segment offset (from lane
@@ -967,7 +973,11 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
             uint64_t* cl = gq->C.w_lo + ceo;
             uint64_t* chh = gq->C.w_hi + ceo;
             uint32_t* sp = gq->salt_pos ? gq->salt_pos + ceo : nullptr;
-            uint32_t zero = canonical || misc[F3_BIGOVF] ? 1u : 0u;
+            const bool zero0 = canonical || misc[F3_BIGOVF];
+            uint64_t zmask = 0;   // lanes that folded a 0 sum (a ballot per position round: SGPRs, no VALU)
+            // one zero register pair for the three limb clears (else rematerialised per position)
+            uint64_t z64 = 0;
+            asm volatile("" : "+v"(z64));
             // buffer stores: one 32-bit offset for the three arrays (SGPR bases) instead of three
             // 64-bit address computations per position (round 4: -1.7%, A/B)
             typedef unsigned int u2v __attribute__((ext_vector_type(2)));
@@ -981,12 +991,12 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
 #endif
                 unsigned long long* q = lim + 3u * p;
                 const uint64_t l0 = q[0], l1 = q[1], l2c = q[2];
-                q[0] = 0;
-                q[1] = 0;
-                q[2] = 0;
+                q[0] = z64;
+                q[1] = z64;
+                q[2] = z64;
                 const uint32_t cell = (uint32_t)(l2c >> 52);
                 const fp w = fp_fold3_44(l0, l1, l2c & ((1ull << 52) - 1ull));
-                zero |= fp_nonzero(w) ? 0u : 1u;
+                zmask |= __builtin_amdgcn_ballot_w64(!fp_nonzero(w));
                 const uint32_t s = cell >> 1;
                 const uint32_t lp = __umulhi(s, bdiv);
                 const uint32_t r = s - lp * Bm;
@@ -999,7 +1009,7 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
                 __builtin_amdgcn_raw_buffer_store_b64(u2v{(uint32_t)w.hi, (uint32_t)(w.hi >> 32)}, rh, bo, 0, 2);
                 if (sp) sp[p] = p;   // hash order == emit order here
             }
-            if (zero) misc[F3_ZERO] = 1u;
+            if (zero0 || zmask) misc[F3_ZERO] = 1u;
             STAMP3_SYNC(11);
             const uint32_t used = (max(2u * KS, n) + 3u) >> 2;   // b128 words of this pair's cells and G
             uint4* tv = (uint4*)tkey;
