@@ -37,13 +37,14 @@ def main():
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / steps
         dig = eng.digest(out).cpu()
-        same = ref is None or bool(torch.equal(dig, ref))
+        lay = out.layers[:plan.total_layer_slots].cpu()   # the layer records (ztags) too
+        same = ref is None or (bool(torch.equal(dig, ref[0])) and bool(torch.equal(lay, ref[1])))
         if ref is None:
-            ref = dig
+            ref = (dig, lay)
         name = os.path.basename(path)
         res[name] = round(ms, 4)
         print(name, round(ms, 4), "ms/step", "same" if same else "DIFFERENT", flush=True)
-        del out, dig, A, B, Cb, plan, nonces, eng
+        del out, dig, lay, A, B, Cb, plan, nonces, eng
         torch.cuda.empty_cache()
     print(json.dumps(res))
 
