@@ -95,7 +95,11 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
         y.pad = 0;
         y.nonce_lo = g.nonces[2 * slot];
         y.nonce_hi = g.nonces[2 * slot + 1];
+#ifdef PVAC_EXP_NOZTAG   // timing experiment only: no SHA-256 (ztags wrong)
+        y.ztag = y.nonce_lo ^ g.canon_tag;
+#else
         y.ztag = layer_ztag(g.canon_tag, y.nonce_lo, y.nonce_hi);
+#endif
         g.C.layers[slot] = y;
     }
 }
