@@ -377,6 +377,13 @@ int pvac_hip_batch_digest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* o
  * m(m(m(e * 0x9E3779B97F4A7C15 ^ meta) ^ w_lo) ^ w_hi) mod 2^64, m = the splitmix64 finaliser.
  * Order-sensitive, computed in parallel (one workgroup per cipher). */
 int pvac_hip_batch_sumdigest(pvac_hip_ctx* ctx, const pvac_ct_batch* X, uint64_t* out);
+/* The used rows of a capacity-padded batch (a plan's output, every pair at its capacity) packed
+ * back to back into dst, e.g. before copying a result to the host. dst (DEVICE arrays): counts =
+ * src's, offsets = their exclusive scans, rows and, when dst->sigma is set (src must carry sigma of
+ * the same sigma_words), sigma rows; dst->n is set. dst's row arrays must hold the packed rows (src's
+ * row capacity always does). totals (HOST [2]) = packed layer and edge counts. No reference
+ * counterpart: the reference's Ciphers are std::vectors of exact size (core/types.hpp:95-98). */
+int pvac_hip_batch_pack(pvac_hip_ctx* ctx, const pvac_ct_batch* src, pvac_ct_batch* dst, uint64_t* totals);
 
 /* ---------------------------------------------------------------- LPN PRF
  * SecKey (core/types.hpp:134-137): prf_k and the LPN secret (ceil(lpn_n/64) words, host) with

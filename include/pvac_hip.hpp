@@ -35,6 +35,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <exception>
 #include <cstdint>
@@ -80,22 +81,30 @@ inline void hip_ok(hipError_t e, const char* what) {
     if (e != hipSuccess) throw Error(PVAC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// RAII device array of T
+// RAII device array of T; alloc() keeps the allocation when it already holds count elements, so
+// an engine-owned array reused call after call stops paying hipMalloc / hipFree.
 template <class T>
 struct dev_array {
     T* p = nullptr;
-    size_t n = 0;
+    size_t n = 0, cap = 0;
     dev_array() = default;
     explicit dev_array(size_t count) { alloc(count); }
     dev_array(const dev_array&) = delete;
     dev_array& operator=(const dev_array&) = delete;
-    dev_array(dev_array&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
-    ~dev_array() { if (p) (void)hipFree(p); }
-    void alloc(size_t count) {
+    dev_array(dev_array&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+    ~dev_array() { release(); }
+    void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
+        n = cap = 0;
+    }
+    void alloc(size_t count) {
         n = count;
-        hip_ok(hipMalloc(&p, (count ? count : 1) * sizeof(T)), "hipMalloc");
+        if (p && count <= cap) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = count ? count : 1;
+        hip_ok(hipMalloc(&p, cap * sizeof(T)), "hipMalloc");
     }
     void upload(const T* h, size_t count, hipStream_t s) {
         if (count) hip_ok(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s), "H2D");
@@ -105,13 +114,67 @@ struct dev_array {
     }
 };
 
+// Host arrays that are filled right after they are sized (by a copy or a conversion loop): default-
+// initialised, so sizing a few GB of output does not first zero it on one thread.
+template <class T>
+struct default_init : std::allocator<T> {
+    template <class U>
+    struct rebind { using other = default_init<U>; };
+    using std::allocator<T>::allocator;
+    default_init() noexcept = default;
+    template <class U>
+    default_init(const default_init<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) { ::new ((void*)p) U; }
+    template <class U, class... Args>
+    void construct(U* p, Args&&... args) { ::new ((void*)p) U(std::forward<Args>(args)...); }
+};
+template <class T>
+using hvec = std::vector<T, default_init<T>>;
+
+// The same, in page-locked host memory (hipHostMalloc): copies to and from the device run at the
+// link's rate instead of through the runtime's pageable staging. Pinning is slow to set up, so only
+// engine-owned arrays that are reused call after call use it.
+template <class T>
+struct pinned_alloc : default_init<T> {
+    using value_type = T;
+    template <class U>
+    struct rebind { using other = pinned_alloc<U>; };
+    pinned_alloc() noexcept = default;
+    template <class U>
+    pinned_alloc(const pinned_alloc<U>&) noexcept {}
+    T* allocate(size_t count) {
+        void* q = nullptr;
+        if (hipHostMalloc(&q, (count ? count : 1) * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+        return static_cast<T*>(q);
+    }
+    void deallocate(T* q, size_t) noexcept { (void)hipHostFree(q); }
+    template <class U>
+    bool operator==(const pinned_alloc<U>&) const noexcept { return true; }
+    template <class U>
+    bool operator!=(const pinned_alloc<U>&) const noexcept { return false; }
+};
+
 // Host SoA image of a batch of reference Ciphers + its device copy.
-struct batch {
-    std::vector<uint64_t> l_off, l_cnt, e_off, e_cnt, meta, w_lo, w_hi, sigma;
-    std::vector<pvac_layer> layers;
+template <bool Pinned>
+struct basic_batch {
+    template <class T>
+    using vec = std::vector<T, typename std::conditional<Pinned, pinned_alloc<T>, default_init<T>>::type>;
+    vec<uint64_t> l_off, l_cnt, e_off, e_cnt, meta, w_lo, w_hi, sigma;
+    vec<pvac_layer> layers;
     dev_array<uint64_t> d_l_off, d_l_cnt, d_e_off, d_e_cnt, d_meta, d_w_lo, d_w_hi, d_sigma;
     dev_array<pvac_layer> d_layers;
     uint32_t sigma_words = 0;
+
+    // frees every host and device array (an engine-owned batch between calls)
+    void release() {
+        basic_batch e;
+        std::swap(l_off, e.l_off); std::swap(l_cnt, e.l_cnt); std::swap(e_off, e.e_off); std::swap(e_cnt, e.e_cnt);
+        std::swap(meta, e.meta); std::swap(w_lo, e.w_lo); std::swap(w_hi, e.w_hi); std::swap(sigma, e.sigma);
+        std::swap(layers, e.layers);
+        for (auto* d : {&d_l_off, &d_l_cnt, &d_e_off, &d_e_cnt, &d_meta, &d_w_lo, &d_w_hi, &d_sigma}) d->release();
+        d_layers.release();
+    }
 
     pvac_ct_batch view(bool with_sigma) {
         pvac_ct_batch b{};
@@ -124,6 +187,8 @@ struct batch {
         return b;
     }
 };
+using batch = basic_batch<false>;
+using pinned_batch = basic_batch<true>;
 
 // Runs f(begin, end) over [0, n) on up to hardware_concurrency() threads (AoS <-> SoA conversion
 // of large batches; each cipher is independent).
@@ -141,8 +206,8 @@ void parallel_ranges(size_t n, F f) {
     for (auto& x : th) x.join();
 }
 
-template <class CipherT>
-void to_host(const std::vector<const CipherT*>& cs, uint32_t sigma_words, bool with_sigma, batch& b) {
+template <class CipherT, class Batch>
+void to_host(const std::vector<const CipherT*>& cs, uint32_t sigma_words, bool with_sigma, Batch& b) {
     const size_t n = cs.size();
     b.sigma_words = sigma_words;
     b.l_off.resize(n); b.l_cnt.resize(n); b.e_off.resize(n); b.e_cnt.resize(n);
@@ -176,7 +241,8 @@ void to_host(const std::vector<const CipherT*>& cs, uint32_t sigma_words, bool w
     });
 }
 
-inline void upload(batch& b, hipStream_t s, bool with_sigma) {
+template <class Batch>
+void upload(Batch& b, hipStream_t s, bool with_sigma) {
     b.d_l_off.alloc(b.l_off.size()); b.d_l_off.upload(b.l_off.data(), b.l_off.size(), s);
     b.d_l_cnt.alloc(b.l_cnt.size()); b.d_l_cnt.upload(b.l_cnt.data(), b.l_cnt.size(), s);
     b.d_e_off.alloc(b.e_off.size()); b.d_e_off.upload(b.e_off.data(), b.e_off.size(), s);
@@ -190,7 +256,8 @@ inline void upload(batch& b, hipStream_t s, bool with_sigma) {
 
 // Output records of capacity layer/edge slots; the per-cipher offset/count arrays were
 // allocated before the plan (which writes the offsets) and are kept.
-inline void alloc_out(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t sigma_words, bool with_sigma) {
+template <class Batch>
+void alloc_out(Batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t sigma_words, bool with_sigma) {
     c.sigma_words = sigma_words;
     c.d_layers.alloc(lslots);
     c.d_meta.alloc(eslots); c.d_w_lo.alloc(eslots); c.d_w_hi.alloc(eslots);
@@ -199,8 +266,8 @@ inline void alloc_out(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint
 }
 
 // host SoA image (c.l_off ... c.sigma filled) -> reference Ciphers
-template <class CipherT>
-std::vector<CipherT> convert_host(batch& c, size_t n, uint32_t m_bits, bool with_sigma) {
+template <class CipherT, class Batch>
+std::vector<CipherT> convert_host(Batch& c, size_t n, uint32_t m_bits, bool with_sigma) {
     std::vector<CipherT> out(n);
     parallel_ranges(n, [&](size_t i0, size_t i1) {
     for (size_t i = i0; i < i1; ++i) {
@@ -233,27 +300,34 @@ std::vector<CipherT> convert_host(batch& c, size_t n, uint32_t m_bits, bool with
     return out;
 }
 
+// device records of d (lslots / eslots rows) -> host SoA image c, synchronous
+template <class Batch, class Dev>
+void download(Batch& c, const Dev& d, size_t n, uint64_t lslots, uint64_t eslots, bool with_sigma, hipStream_t s) {
+    c.sigma_words = d.sigma_words;
+    c.l_off.resize(n); c.l_cnt.resize(n); c.e_off.resize(n); c.e_cnt.resize(n);
+    c.layers.resize(lslots); c.meta.resize(eslots); c.w_lo.resize(eslots); c.w_hi.resize(eslots);
+    d.d_l_off.download(c.l_off.data(), n, s); d.d_l_cnt.download(c.l_cnt.data(), n, s);
+    d.d_e_off.download(c.e_off.data(), n, s); d.d_e_cnt.download(c.e_cnt.data(), n, s);
+    d.d_layers.download(c.layers.data(), lslots, s);
+    d.d_meta.download(c.meta.data(), eslots, s);
+    d.d_w_lo.download(c.w_lo.data(), eslots, s); d.d_w_hi.download(c.w_hi.data(), eslots, s);
+    if (with_sigma) {
+        c.sigma.resize(eslots * c.sigma_words);
+        d.d_sigma.download(c.sigma.data(), c.sigma.size(), s);
+    }
+    hip_ok(hipStreamSynchronize(s), "sync");
+}
+
 template <class CipherT>
 std::vector<CipherT> from_device(batch& c, size_t n, uint64_t lslots, uint64_t eslots, uint32_t m_bits,
                                  bool with_sigma, hipStream_t s) {
-    c.l_off.resize(n); c.l_cnt.resize(n); c.e_off.resize(n); c.e_cnt.resize(n);
-    c.layers.resize(lslots); c.meta.resize(eslots); c.w_lo.resize(eslots); c.w_hi.resize(eslots);
-    c.d_l_off.download(c.l_off.data(), n, s); c.d_l_cnt.download(c.l_cnt.data(), n, s);
-    c.d_e_off.download(c.e_off.data(), n, s); c.d_e_cnt.download(c.e_cnt.data(), n, s);
-    c.d_layers.download(c.layers.data(), lslots, s);
-    c.d_meta.download(c.meta.data(), eslots, s);
-    c.d_w_lo.download(c.w_lo.data(), eslots, s); c.d_w_hi.download(c.w_hi.data(), eslots, s);
-    if (with_sigma) {
-        c.sigma.resize(eslots * c.sigma_words);
-        c.d_sigma.download(c.sigma.data(), c.sigma.size(), s);
-    }
-    hip_ok(hipStreamSynchronize(s), "sync");
+    download(c, c, n, lslots, eslots, with_sigma, s);
     return convert_host<CipherT>(c, n, m_bits, with_sigma);
 }
 
 // small synchronous device -> host copies of a batch view handed to a chain hook (valid only there)
-inline std::vector<uint64_t> d2h_u64(const uint64_t* p, size_t n, hipStream_t s) {
-    std::vector<uint64_t> v(n);
+inline hvec<uint64_t> d2h_u64(const uint64_t* p, size_t n, hipStream_t s) {
+    hvec<uint64_t> v(n);
     if (n) hip_ok(hipMemcpyAsync(v.data(), p, n * 8, hipMemcpyDeviceToHost, s), "D2H");
     hip_ok(hipStreamSynchronize(s), "sync");
     return v;
@@ -297,7 +371,12 @@ public:
     }
     Engine(const Engine&) = delete;
     Engine& operator=(const Engine&) = delete;
-    ~Engine() { pvac_hip_ctx_destroy(ctx_); }
+    ~Engine() {
+        if (stream_) (void)hipStreamSynchronize(stream_);
+        mul_a_.release(); mul_b_.release(); mul_c_.release(); mul_p_.release();
+        mul_nonces_.release(); mul_salts_.release(); mul_status_.release();
+        pvac_hip_ctx_destroy(ctx_);
+    }
 
     template <class PubKeyT>
     static pvac_hip_params params_of(const PubKeyT& pk) {
@@ -311,6 +390,19 @@ public:
 
     pvac_hip_ctx* ctx() const { return ctx_; }
     uint32_t sigma_words() const { return (prm_.m_bits + 63) / 64; }
+
+    // Wall-clock split of the last batched ct_mul, in seconds: host AoS -> SoA, H2D, plan + nonce
+    // draws, exec (+ salts, sigma and the device-side pack of the used rows), D2H, SoA -> AoS.
+    struct Phases { double to_soa = 0, h2d = 0, plan = 0, exec = 0, d2h = 0, to_aos = 0; };
+    const Phases& last_phases() const { return phases_; }
+
+    // Batched ct_mul keeps its host (pinned) and device arrays between calls, sized by the largest
+    // batch so far; trim() hands them back.
+    void trim() {
+        detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+        mul_a_.release(); mul_b_.release(); mul_c_.release(); mul_p_.release();
+        mul_nonces_.release(); mul_salts_.release(); mul_status_.release();
+    }
 
     // H regenerated on the device from canon_tag (gen_H, crypto/matrix.hpp:191-251); returns the
     // H_digest for comparison with pk.H_digest.
@@ -346,11 +438,24 @@ public:
         const size_t n = A.size();
         if (!n) return {};
         if (with_sigma) ensure_H(pk);
-        detail::batch a, b, c;
+        using clk = std::chrono::steady_clock;
+        auto t = clk::now();
+        auto lap = [&t](double& into) {
+            const auto u = clk::now();
+            into = std::chrono::duration<double>(u - t).count();
+            t = u;
+        };
+        // engine-owned (pinned, grow-only) arrays: a steady stream of batches maps, pins and frees nothing
+        detail::pinned_batch& a = mul_a_;
+        detail::pinned_batch& b = mul_b_;
+        detail::pinned_batch& c = mul_c_;
         detail::to_host(A, sigma_words(), false, a);
         detail::to_host(B, sigma_words(), false, b);
+        lap(phases_.to_soa);
         detail::upload(a, stream_, false);
         detail::upload(b, stream_, false);
+        detail::hip_ok(hipStreamSynchronize(stream_), "sync");
+        lap(phases_.h2d);
         pvac_ct_batch va = a.view(false), vb = b.view(false);
         c.d_l_off.alloc(n); c.d_l_cnt.alloc(n); c.d_e_off.alloc(n); c.d_e_cnt.alloc(n);
         pvac_ct_batch vc{};
@@ -370,9 +475,11 @@ public:
                 nonces[2 * (s0 + k) + 1] = rnd();
             }
         }
-        detail::dev_array<uint64_t> d_nonces(nonces.size());
+        detail::dev_array<uint64_t>& d_nonces = mul_nonces_;
+        d_nonces.alloc(nonces.size());
         d_nonces.upload(nonces.data(), nonces.size(), stream_);
         detail::alloc_out(c, n, plan.total_layer_slots, plan.total_edge_slots, sigma_words(), with_sigma);
+        lap(phases_.plan);
         vc = c.view(false);
         vc.n = n;
         check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, nullptr, &vc, 0));
@@ -384,7 +491,8 @@ public:
             // second exec with PVAC_MUL_WITH_SIGMA maps (salt positions)
             std::vector<uint64_t> ecnt(n), eoff(n);
             std::vector<uint32_t> status(n);
-            detail::dev_array<uint32_t> d_status(n);
+            detail::dev_array<uint32_t>& d_status = mul_status_;
+            d_status.alloc(n);
             check(pvac_hip_ct_mul_status(ctx_, d_status.p, n));
             c.d_e_cnt.download(ecnt.data(), n, stream_);
             c.d_e_off.download(eoff.data(), n, stream_);
@@ -396,7 +504,8 @@ public:
                 hash_order &= status[i] != 1u;
                 for (uint64_t k = 0; k < ecnt[i]; ++k) salts[eoff[i] + k] = rnd();
             }
-            detail::dev_array<uint64_t> d_salts(salts.size());
+            detail::dev_array<uint64_t>& d_salts = mul_salts_;
+            d_salts.alloc(salts.size());
             d_salts.upload(salts.data(), salts.size(), stream_);
             vc = c.view(true);
             vc.n = n;
@@ -408,11 +517,23 @@ public:
                 vc.n = n;
                 check(pvac_hip_ct_mul_exec(ctx_, &plan, &va, &vb, d_nonces.p, d_salts.p, &vc, PVAC_MUL_WITH_SIGMA));
             }
-            return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits,
-                                                true, stream_);
         }
-        return detail::from_device<CipherT>(c, n, plan.total_layer_slots, plan.total_edge_slots, prm_.m_bits, false,
-                                            stream_);
+        // only the used rows cross the link: packed on the device first (each pair's output kept its
+        // plan capacity), then copied at their exact totals
+        detail::pinned_batch& p = mul_p_;
+        p.d_l_off.alloc(n); p.d_l_cnt.alloc(n); p.d_e_off.alloc(n); p.d_e_cnt.alloc(n);
+        detail::alloc_out(p, n, plan.total_layer_slots, plan.total_edge_slots, sigma_words(), with_sigma);
+        vc = c.view(with_sigma);
+        vc.n = n;
+        pvac_ct_batch vp = p.view(with_sigma);
+        uint64_t tot[2] = {0, 0};
+        check(pvac_hip_batch_pack(ctx_, &vc, &vp, tot));
+        lap(phases_.exec);
+        detail::download(c, p, n, tot[0], tot[1], with_sigma, stream_);
+        lap(phases_.d2h);
+        std::vector<CipherT> out = detail::convert_host<CipherT>(c, n, prm_.m_bits, with_sigma);
+        lap(phases_.to_aos);
+        return out;
     }
 
     // Depth chains through pvac_hip_ct_mul_chain (the chain entry point): for every input x of xs,
@@ -719,6 +840,10 @@ private:
     hipStream_t stream_ = nullptr;
     bool h_ready_ = false;
     bool keys_ready_ = false;
+    Phases phases_;
+    detail::pinned_batch mul_a_, mul_b_, mul_c_, mul_p_;
+    detail::dev_array<uint64_t> mul_nonces_, mul_salts_;
+    detail::dev_array<uint32_t> mul_status_;
     std::vector<uint64_t> key_fp_;
 };
 

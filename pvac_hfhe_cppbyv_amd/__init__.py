@@ -147,6 +147,7 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
         "pvac_hip_fill_random": ([vp, u64, vp, C.c_size_t], i32),
         "pvac_hip_batch_digest": ([vp, C.POINTER(CtBatch), vp], i32),
         "pvac_hip_batch_sumdigest": ([vp, C.POINTER(CtBatch), vp], i32),
+        "pvac_hip_batch_pack": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(u64)], i32),
         "pvac_hip_bucket_count": ([u64], u64),
         "pvac_hip_chain_partition": ([u64, u64, u32, vp], i32),
         "pvac_hip_memcpy": ([vp, vp, C.c_size_t, vp], i32),
@@ -628,6 +629,22 @@ class Engine:
         sx = X.struct()
         self._check(self.lib.pvac_hip_batch_sumdigest(self.ctx, C.byref(sx), C.c_void_p(out.data_ptr())))
         return out[:X.n]
+
+    def pack(self, X: DeviceBatch) -> DeviceBatch:
+        """X's used rows back to back (pvac_hip_batch_pack): dense offsets, arrays of exactly the
+        packed sizes (sigma kept when X has it)."""
+        t = self.torch
+        rows = lambda a: a.shape[0] if a is not None else 0
+        sig = X.sigma is not None
+        D = DeviceBatch.empty(X.n, rows(X.layers), rows(X.meta), self.device)
+        if sig:
+            D.sigma = t.empty_like(X.sigma)
+        sx, sd = X.struct(), D.struct()
+        tot = (C.c_uint64 * 2)()
+        self._check(self.lib.pvac_hip_batch_pack(self.ctx, C.byref(sx), C.byref(sd), tot))
+        nl, ne = int(tot[0]), int(tot[1])
+        return DeviceBatch(X.n, D.l_off, D.l_cnt, D.layers[:nl], D.e_off, D.e_cnt, D.meta[:ne], D.w_lo[:ne],
+                           D.w_hi[:ne], D.sigma[:ne] if sig else None)
 
     # ---- timing
     def timing(self, on=True):

@@ -292,6 +292,12 @@ __global__ __launch_bounds__(256) void k_stage_rows(pvac_ct_batch src, pvac_ct_b
         dst.w_lo[de + e] = src.w_lo[se + e];
         dst.w_hi[de + e] = src.w_hi[se + e];
     }
+    if (dst.sigma) {   // pvac_hip_batch_pack of a batch with sigma: sigma_words per edge, contiguous
+        const uint64_t sw = dst.sigma_words;
+        const uint64_t* sS = src.sigma + se * sw;
+        uint64_t* dS = dst.sigma + de * sw;
+        for (uint64_t w = threadIdx.x; w < ne * sw; w += 256) dS[w] = sS[w];
+    }
 }
 
 hipError_t launch_stage_rows(const pvac_ct_batch& src, const pvac_ct_batch& dst, hipStream_t st) {

@@ -255,6 +255,8 @@ hipError_t read_back(pvac_hip_ctx* c, void* dst, const void* src, size_t bytes) 
     return e;
 }
 
+int ensure_scan(pvac_hip_ctx* c, size_t n);
+
 int ensure_pairs(pvac_hip_ctx* c, size_t n) {
     if (n > c->pair_cap) {
         hipFree(c->pair_class);
@@ -280,6 +282,11 @@ int ensure_pairs(pvac_hip_ctx* c, size_t n) {
         if (e != hipSuccess) { c->pair_cap = 0; return hip_fail(c, e, "alloc pair scratch"); }
         c->pair_cap = cap;
     }
+    return ensure_scan(c, n);
+}
+
+// the exclusive scans' scratch for n counts
+int ensure_scan(pvac_hip_ctx* c, size_t n) {
     const size_t sw = scan_scratch_words(n);
     if (sw > c->scan_cap) {
         hipFree(c->scan_scratch);
@@ -1679,6 +1686,39 @@ int pvac_hip_batch_digest(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* out
 int pvac_hip_batch_sumdigest(pvac_hip_ctx* c, const pvac_ct_batch* X, uint64_t* out) {
     if (!c || !batch_ok(X) || (X->n && !out)) return PVAC_EINVAL;
     return hip_fail(c, launch_batch_sumdigest(*X, out, c->stream), "batch_sumdigest");
+}
+
+// The used rows of a capacity-padded batch packed back to back (a plan's output keeps every pair's
+// capacity): dst's counts = src's, its offsets their exclusive scans, rows (and sigma when both
+// carry it) copied by k_stage_rows. totals[0], [1] = the packed layer / edge counts, so a caller
+// copies exactly those rows to the host. dst's row arrays must hold the packed rows (src's
+// capacity always does); the pair scratch of a pending plan is left alone.
+int pvac_hip_batch_pack(pvac_hip_ctx* c, const pvac_ct_batch* src, pvac_ct_batch* dst, uint64_t* totals) {
+    if (!c || !batch_ok(src) || !dst || !totals) return fail(c, PVAC_EINVAL, "batch_pack: arguments");
+    const uint64_t n = src->n;
+    if (n && (!dst->l_off || !dst->l_cnt || !dst->e_off || !dst->e_cnt || !dst->layers || !dst->meta || !dst->w_lo ||
+              !dst->w_hi || !src->layers || !src->meta || !src->w_lo || !src->w_hi))
+        return fail(c, PVAC_EINVAL, "batch_pack: null arrays");
+    if (dst->sigma && (!src->sigma || dst->sigma_words != src->sigma_words))
+        return fail(c, PVAC_EINVAL, "batch_pack: dst sigma needs src sigma of the same width");
+    dst->n = n;
+    totals[0] = totals[1] = 0;
+    if (!n) return PVAC_OK;
+    int rc = ensure_scan(c, n);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(dst->l_cnt, src->l_cnt, n * 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst->e_cnt, src->e_cnt, n * 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst->l_off, src->l_cnt, n * 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst->e_off, src->e_cnt, n * 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess)
+        e = launch_exclusive_scan2_u64(dst->l_off, dst->e_off, n, c->scan_scratch, &c->totals[0], &c->totals[1],
+                                       c->stream);
+    unsigned long long tot[2] = {0, 0};
+    if (e == hipSuccess) e = read_back(c, tot, c->totals, sizeof tot);
+    if (e != hipSuccess) return hip_fail(c, e, "batch_pack (offsets)");
+    totals[0] = tot[0];
+    totals[1] = tot[1];
+    return hip_fail(c, launch_stage_rows(*src, *dst, c->stream), "batch_pack (rows)");
 }
 
 // ---------------------------------------------------------------- depth chains

@@ -310,8 +310,11 @@ static int time_host_roundtrip(size_t n) {
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     size_t edges = 0;
     for (const auto& c : C) edges += c.E.size();
-    std::printf("{\"pairs\": %zu, \"seconds\": %.6f, \"ct_mul_per_s\": %.1f, \"output_edges\": %zu}\n", n, sec,
-                n / sec, edges);
+    const auto& ph = pvac_hip::engine_for(pk).last_phases();
+    std::printf("{\"pairs\": %zu, \"seconds\": %.6f, \"ct_mul_per_s\": %.1f, \"output_edges\": %zu, "
+                "\"phases_s\": {\"to_soa\": %.4f, \"h2d\": %.4f, \"plan\": %.4f, \"exec\": %.4f, \"d2h\": %.4f, "
+                "\"to_aos\": %.4f}}\n",
+                n, sec, n / sec, edges, ph.to_soa, ph.h2d, ph.plan, ph.exec, ph.d2h, ph.to_aos);
     return 0;
 }
 

@@ -185,10 +185,21 @@ def test_ct_mul_sigma_golden(engine, manifest, oracle):
         nn = 2 * xs[p].nL * ys[p].nL
         s = streams[p][nn:]
         salts[int(eoff[p]):int(eoff[p]) + len(s)] = s
-    out = eng.ct_mul(A, B, nonces=nonces, salts=_i64(salts).to(eng.device), flags=MUL_WITH_SIGMA, C_=Cb,
-                     plan=plan).to_host()
+    Cr = eng.ct_mul(A, B, nonces=nonces, salts=_i64(salts).to(eng.device), flags=MUL_WITH_SIGMA, C_=Cb,
+                    plan=plan)
+    out = Cr.to_host()
     ref0 = read_ct(os.path.join(REF, "pair0_mul.ct"))[0]
     _assert_same(out[0], ref0, sigma=True)
+    # pvac_hip_batch_pack (what the C++ adapter copies to the host): dense offsets, the same rows
+    P = eng.pack(Cr)
+    lc = P.l_cnt.cpu().numpy().astype(np.uint64)
+    ec = P.e_cnt.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(P.l_off.cpu().numpy().astype(np.uint64), np.cumsum(lc) - lc)
+    assert np.array_equal(P.e_off.cpu().numpy().astype(np.uint64), np.cumsum(ec) - ec)
+    assert P.layers.shape[0] == int(lc.sum()) and P.meta.shape[0] == int(ec.sum()) == P.sigma.shape[0]
+    assert int(ec.sum()) < plan.total_edge_slots
+    for p, c in enumerate(P.to_host()):
+        _assert_same(c, out[p], sigma=True, layers_view=False)
     Hd = bytes.fromhex(manifest["H_digest"])
     for p in range(8):
         c = out[p]
