@@ -186,6 +186,16 @@ int pvac_hip_ct_mul_plan(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_c
                          pvac_hip_plan* plan);
 int pvac_hip_ct_mul_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pvac_ct_batch* A, const pvac_ct_batch* B,
                          const uint64_t* nonces, const uint64_t* salts, pvac_ct_batch* C, uint32_t flags);
+/* plan + exec in one call, into output arrays the caller sized once (for a stream of batches of
+ * one shape, no host round trip between the two): C->l_off / e_off / l_cnt / e_cnt hold A->n,
+ * C->layers layer_cap slots, C->meta / w_lo / w_hi (and C->sigma) edge_cap slots. When this plan
+ * needs more, nothing is launched after it and the call returns PVAC_ENOMEM with *plan (nullable)
+ * holding the sizes to allocate. nonces / salts as for pvac_hip_ct_mul_exec (the nonce slots are
+ * C's planned layer slots, so they are valid only while the plan's offsets are: batches of one
+ * shape plan the same offsets). */
+int pvac_hip_ct_mul(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
+                    uint64_t layer_cap, uint64_t edge_cap, const uint64_t* nonces, const uint64_t* salts,
+                    uint32_t flags, pvac_hip_plan* plan);
 /* Pairs that ct_mul_exec re-ran on the general path (see above) since the context was created. */
 int pvac_hip_ct_mul_redo_count(pvac_hip_ctx* ctx, uint64_t* out);
 /* Pair launches by path since the context was created (diagnostics and tests): out[0] the

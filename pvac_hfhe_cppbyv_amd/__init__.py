@@ -126,6 +126,8 @@ def load_library(path: str = _LIB_PATH) -> C.CDLL:
                                   C.POINTER(Plan)], i32),
         "pvac_hip_ct_mul_exec": ([vp, C.POINTER(Plan), C.POINTER(CtBatch), C.POINTER(CtBatch), vp, vp,
                                   C.POINTER(CtBatch), u32], i32),
+        "pvac_hip_ct_mul": ([vp, C.POINTER(CtBatch), C.POINTER(CtBatch), C.POINTER(CtBatch), u64, u64, vp, vp, u32,
+                             C.POINTER(Plan)], i32),
         "pvac_hip_ct_mul_redo_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ct_mul_path_count": ([vp, C.POINTER(u64)], i32),
         "pvac_hip_ctx_set_noise": ([vp, C.c_double, C.c_double, C.c_double], i32),
@@ -423,6 +425,39 @@ class Engine:
         self._check(self.lib.pvac_hip_ct_mul_exec(self.ctx, C.byref(plan), C.byref(sa), C.byref(sb), p(nonces),
                                                   p(salts), C.byref(sc), flags))
         return C_
+
+    def ct_mul_into(self, A: DeviceBatch, B: DeviceBatch, C_: DeviceBatch, nonces, salts=None, flags=0):
+        """plan + exec in one call (pvac_hip_ct_mul) into C_, whose arrays were sized once (e.g. by
+        ct_mul on a batch of the same shape); returns the plan."""
+        cap_l = C_.layers.shape[0]
+        cap_e = C_.meta.shape[0]
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        plan = Plan()
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        self._check(self.lib.pvac_hip_ct_mul(self.ctx, C.byref(sa), C.byref(sb), C.byref(sc), cap_l, cap_e,
+                                             p(nonces), p(salts), flags, C.byref(plan)))
+        return plan
+
+    def ct_mul_step(self, A: DeviceBatch, B: DeviceBatch, C_: DeviceBatch, nonces, salts=None, flags=0):
+        """ct_mul_into over fixed batches, its ctypes arguments built once: the returned function
+        runs plan + exec (pvac_hip_ct_mul) per call and returns the plan (one object, refreshed by
+        every call)."""
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        plan = Plan()
+        sa, sb, sc = A.struct(), B.struct(), C_.struct()
+        args = (self.ctx, C.byref(sa), C.byref(sb), C.byref(sc), C_.layers.shape[0], C_.meta.shape[0], p(nonces),
+                p(salts), flags, C.byref(plan))
+        fn, check = self.lib.pvac_hip_ct_mul, self._check
+        keep = (sa, sb, sc, A, B, C_, nonces, salts)
+
+        def run():
+            rc = fn(*args)
+            if rc:
+                check(rc)
+            return plan
+
+        run.keep = keep
+        return run
 
     def ct_mul_chain(self, X: DeviceBatch, depth, nonce_seed=0x5EED0040, streams=4, chunk=1024, check_gsum=False,
                      digest_n=0, canonical=False, fill_nonces=None, on_chunk=None, count_n=None, sigma=False,

@@ -137,6 +137,7 @@ struct pvac_hip_ctx {
     // timing
     bool timing = false;
     std::map<std::string, timer_rec> timers;
+    std::vector<hipEvent_t> ev_pool;   // timer events returned by flush_timers, reused (no create per launch)
     // general-path scratch cap in words (0 = half the free HBM): chain workers share the device
     uint64_t arena_cap_words = 0;
     bool large_no_direct = false;   // the redo run: every pair on the full (per-key sums) layout
@@ -197,9 +198,19 @@ struct scoped_timer {
     scoped_timer(pvac_hip_ctx* ctx, const char* name) : c(ctx) {
         if (!c->timing) return;
         rec = &c->timers[name];
-        hipEventCreate(&a);
-        hipEventCreate(&b);
+        a = take();
+        b = take();
         hipEventRecord(a, c->stream);
+    }
+    hipEvent_t take() {
+        hipEvent_t e{};
+        if (!c->ev_pool.empty()) {
+            e = c->ev_pool.back();
+            c->ev_pool.pop_back();
+        } else {
+            hipEventCreate(&e);
+        }
+        return e;
     }
     ~scoped_timer() {
         if (!rec) return;
@@ -216,8 +227,8 @@ void flush_timers(pvac_hip_ctx* c) {
             hipEventElapsedTime(&ms, ev.first, ev.second);
             kv.second.ms += ms;
             kv.second.launches += 1;
-            hipEventDestroy(ev.first);
-            hipEventDestroy(ev.second);
+            c->ev_pool.push_back(ev.first);
+            c->ev_pool.push_back(ev.second);
         }
         kv.second.pending.clear();
     }
@@ -538,6 +549,8 @@ int pvac_hip_ctx_destroy(pvac_hip_ctx* c) {
     hipSetDevice(c->device);   // each worker's destroy selected the worker's device
     if (c->stream) hipStreamSynchronize(c->stream);
     flush_timers(c);
+    for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
+    c->ev_pool.clear();
     free_chain_sets(c);
     for (void* q : {(void*)c->chain_nonces, (void*)c->chain_salts, (void*)c->chain_out})
         if (q) hipFreeAsync(q, c->stream);
@@ -639,6 +652,12 @@ const char* pvac_hip_last_error(pvac_hip_ctx* c) { return c ? c->err.c_str() : "
 int pvac_hip_timing_enable(pvac_hip_ctx* c, int on) {
     if (!c) return PVAC_EINVAL;
     c->timing = on != 0;
+    // events for the launches to come, created now rather than inside the timed launches
+    while (c->timing && c->ev_pool.size() < 256) {
+        hipEvent_t e{};
+        if (hipEventCreate(&e) != hipSuccess) break;
+        c->ev_pool.push_back(e);
+    }
     return PVAC_OK;
 }
 
@@ -1173,6 +1192,20 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* c, const pvac_hip_plan* plan, const pvac_
         if (e != hipSuccess) return hip_fail(c, e, "sigma");
     }
     return PVAC_OK;
+}
+
+int pvac_hip_ct_mul(pvac_hip_ctx* c, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
+                    uint64_t layer_cap, uint64_t edge_cap, const uint64_t* nonces, const uint64_t* salts,
+                    uint32_t flags, pvac_hip_plan* plan_out) {
+    pvac_hip_plan p{};
+    int rc = pvac_hip_ct_mul_plan(c, A, B, C, &p);
+    if (plan_out) *plan_out = p;
+    if (rc) return rc;
+    if (p.total_layer_slots > layer_cap || p.total_edge_slots > edge_cap) {
+        ++c->plan_stamp;   // the plan's offsets do not fit C: it is not exec'd
+        return fail(c, PVAC_ENOMEM, "ct_mul: output capacity below the plan's totals");
+    }
+    return pvac_hip_ct_mul_exec(c, &p, A, B, nonces, salts, C, flags);
 }
 
 // ---------------------------------------------------------------- ct_add / ct_sub

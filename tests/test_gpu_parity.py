@@ -235,6 +235,43 @@ def test_ct_mul_synthetic_vs_oracle(engine, oracle):
             _assert_same(out[p], ref, layers_view=False)
 
 
+def test_ct_mul_one_call_equals_plan_exec(engine):
+    """pvac_hip_ct_mul (plan + exec in one call into caller-sized outputs, the bench's step) gives
+    the bytes of plan then exec, call after call into the same arrays, and refuses outputs smaller
+    than the plan's totals with PVAC_ENOMEM before launching anything."""
+    from pvac_hfhe_cppbyv_amd import DeviceBatch, Engine, PvacError
+    eng = Engine(device=0, canon_tag=0x1234)
+    n = 4096
+    A = eng.gen_fresh(n, 0xA001, 20)
+    B = eng.gen_fresh(n, 0xB001, 20)
+    Cb, plan = eng.ct_mul_plan(A, B)
+    nonces = eng.torch.empty(2 * plan.total_layer_slots, dtype=eng.torch.int64, device=eng.device)
+    eng.fill_random(nonces, 91)
+    ref = eng.ct_mul(A, B, nonces=nonces, C_=Cb, plan=plan).to_host()
+    D = eng.ct_mul(A, B, nonces=nonces)   # arrays sized by its own plan
+    for fill in (0x5A5A5A5A5A5A5A5A, -1):
+        for t in (D.meta, D.w_lo, D.w_hi, D.layers, D.e_cnt, D.l_cnt):
+            t.fill_(fill)
+        p2 = eng.ct_mul_into(A, B, D, nonces)
+        assert (p2.total_layer_slots, p2.total_edge_slots) == (plan.total_layer_slots, plan.total_edge_slots)
+        got = D.to_host()
+        for p in range(n):
+            _assert_same(got[p], ref[p], layers_view=False)
+    run = eng.ct_mul_step(A, B, D, nonces)   # the bench's prepared form of the same call
+    for t in (D.meta, D.w_lo, D.w_hi, D.layers):
+        t.fill_(7)
+    assert run().total_edge_slots == plan.total_edge_slots
+    got = D.to_host()
+    for p in range(n):
+        _assert_same(got[p], ref[p], layers_view=False)
+    small = DeviceBatch.empty(n, plan.total_layer_slots, plan.total_edge_slots - 1, eng.device)
+    with pytest.raises(PvacError):
+        eng.ct_mul_into(A, B, small, nonces)
+    # the context stays usable and the refused plan is not exec-able
+    again = eng.ct_mul_into(A, B, D, nonces)
+    assert again.total_edge_slots == plan.total_edge_slots
+
+
 def test_ct_mul_full_range_golden(engine):
     """The reference's own ct_mul outputs on weights anywhere in [0, 2^128) (oracle/ref_harness.cpp
     fullrange): full-range words, p, p-1, 2^127, 2^128-1, 0, a cancelling key pair (fresh kernel ->
