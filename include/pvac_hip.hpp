@@ -45,6 +45,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <thread>
 #include <string>
@@ -134,7 +135,16 @@ using hvec = std::vector<T, default_init<T>>;
 
 // The same, in page-locked host memory (hipHostMalloc): copies to and from the device run at the
 // link's rate instead of through the runtime's pageable staging. Pinning is slow to set up, so only
-// engine-owned arrays that are reused call after call use it.
+// engine-owned arrays that are reused call after call use it. When the runtime refuses to pin (a
+// locked-memory limit), the array is ordinary pageable memory instead: slower copies, same results.
+struct pinned_registry {   // which live allocations are pinned (deallocate frees them the same way)
+    std::mutex mu;
+    std::set<void*> pinned;
+    static pinned_registry& get() {
+        static pinned_registry r;
+        return r;
+    }
+};
 template <class T>
 struct pinned_alloc : default_init<T> {
     using value_type = T;
@@ -144,11 +154,31 @@ struct pinned_alloc : default_init<T> {
     template <class U>
     pinned_alloc(const pinned_alloc<U>&) noexcept {}
     T* allocate(size_t count) {
+        const size_t bytes = (count ? count : 1) * sizeof(T);
         void* q = nullptr;
-        if (hipHostMalloc(&q, (count ? count : 1) * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+        if (hipHostMalloc(&q, bytes, hipHostMallocDefault) == hipSuccess && q) {
+            pinned_registry& r = pinned_registry::get();
+            std::lock_guard<std::mutex> g(r.mu);
+            r.pinned.insert(q);
+            return static_cast<T*>(q);
+        }
+        (void)hipGetLastError();   // the refused pin must not surface as a later launch's error
+        q = std::malloc(bytes);
+        if (!q) throw std::bad_alloc();
         return static_cast<T*>(q);
     }
-    void deallocate(T* q, size_t) noexcept { (void)hipHostFree(q); }
+    void deallocate(T* q, size_t) noexcept {
+        bool was_pinned = false;
+        {
+            pinned_registry& r = pinned_registry::get();
+            std::lock_guard<std::mutex> g(r.mu);
+            was_pinned = r.pinned.erase((void*)q) != 0;
+        }
+        if (was_pinned)
+            (void)hipHostFree(q);
+        else
+            std::free(q);
+    }
     template <class U>
     bool operator==(const pinned_alloc<U>&) const noexcept { return true; }
     template <class U>

@@ -52,8 +52,11 @@ static_assert(kFreshLayersMax <= 64, "layer masks are u64");
 static_assert(kFreshKeysMax <= 2048 && kFreshLayersMax <= 512, "writer entries pack slot, idx (11 bits each) and layer");
 
 // ---------------------------------------------------------------- layer records
+#ifndef PVAC_LAY_LANES   // A/B builds only
+#define PVAC_LAY_LANES 4
+#endif
 constexpr int kLayBlock = 256;
-constexpr int kLayLanes = 4;   // lanes per pair: output layers (and their SHA-256 ztags) split over them
+constexpr int kLayLanes = PVAC_LAY_LANES;   // lanes per pair: output layers (and their SHA-256 ztags) split over them
 
 __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g) {
     const uint64_t pr = ((uint64_t)blockIdx.x * kLayBlock + threadIdx.x) / kLayLanes;
