@@ -109,7 +109,11 @@ __global__ __launch_bounds__(kLayBlock) void k_mul_layers_fresh(mul_fresh_args g
 
 // ---------------------------------------------------------------- aggregation + emit
 // misc u32 word shared with stage_pair: invalid edge / layer references in the staged pair
-enum : int { MF_INVALID = 16 };
+// (and two words: the layers of A and of B that have edges, OR-ed by stage_pair; a product layer
+// (la, lb) is used by compact_layers' closure exactly when both have edges, every product cell
+// being assumed to emit, see P2. Fresh-shape pairs have |A.L| + |B.L| + |A.L||B.L| <= 64, so
+// |A.L|, |B.L| <= 31)
+enum : int { MF_INVALID = 16, MF_AMASK = 56, MF_BMASK = 57 };
 
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
@@ -249,9 +253,11 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
                                            uint32_t* a_inf, ulonglong2* b_w, uint32_t* b_inf, uint64_t* pm,
                                            uint32_t* misc, uint32_t t = threadIdx.x) {
     if (h.pr == kNoPair) return;
+    uint32_t amask = 0, bmask = 0;
     if (t < h.nA) {
         const uint32_t la = meta_layer(f.am), idx = meta_idx(f.am), ch = meta_ch(f.am);
         if (la >= h.LA || idx >= Bm || ch > 1) misc[MF_INVALID] = 1;
+        amask = la < 32u ? 1u << la : 0u;
         const fp w = fp_canon(f.al, f.ah);
         a_w[t] = make_ulonglong2(w.lo, w.hi);
         a_inf[t] = idx | ((la * h.LB * Bm) << 12) | (ch << 24);   // S1 adds A and B records (see there)
@@ -259,9 +265,20 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
     if (t < h.nB) {
         const uint32_t lb = meta_layer(f.bm), idx = meta_idx(f.bm), ch = meta_ch(f.bm);
         if (lb >= h.LB || idx >= Bm || ch > 1) misc[MF_INVALID] = 1;
+        bmask = lb < 32u ? 1u << lb : 0u;
         const fp w = fp_canon(f.bl, f.bh);
         b_w[t] = make_ulonglong2(w.lo, w.hi);
         b_inf[t] = idx | ((lb * Bm) << 12) | (ch << 24);
+    }
+    // layer masks: one OR per wave that holds edges (wave-uniform test, so every lane takes part in
+    // the reduction), one LDS atomic per mask and wave
+    if ((t & ~63u) < max(h.nA, h.nB)) {
+        amask = wave_or_u32(amask);
+        bmask = wave_or_u32(bmask);
+        if ((t & 63u) == 0) {
+            if (amask) atomicOr(misc + MF_AMASK, amask);
+            if (bmask) atomicOr(misc + MF_BMASK, bmask);
+        }
     }
     const uint32_t base = h.LA + h.LB, Lc = base + h.LA * h.LB;
     uint32_t rule = f.rule;
@@ -310,7 +327,9 @@ __device__ __forceinline__ void stage_pair(const fresh_pref& f, const fresh_hdr&
 enum : int { F3_PART = 0 /* 16 scan segment totals / block-scan partials */, F3_INVALID = MF_INVALID,
              F3_BIGOVF = 17, F3_IDENT = 18, F3_ZERO = 19, F3_KEEP = 20 /* u64 */,
              F3_CLS = 24 /* 8 class counters while rebuilding */, F3_WAVELP = 24 /* 8 x u64 */,
-             F3_HDR = 40 /* 16: next pair's header record */, F3_WORDS = 56 };
+             F3_HDR = 40 /* 16: next pair's header record */, F3_AMASK = MF_AMASK, F3_BMASK = MF_BMASK,
+             F3_WORDS = 60 };
+static_assert(F3_AMASK == 56 && F3_BMASK == 57, "stage_pair ORs the layer masks into misc[56], misc[57]");
 static_assert(F3_INVALID == 16, "stage_pair flags misc[F3_INVALID]");
 constexpr uint32_t kBigCap = 256;   // LDS entries for the slots of buckets with more than 4 slots
 
@@ -430,7 +449,6 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
     uint64_t* pm = (uint64_t*)(lds + Ls.pm);
     uint32_t* remap = (uint32_t*)(lds + Ls.remap);
     uint32_t* misc = (uint32_t*)(lds + Ls.misc);
-    uint64_t* wave_lp = (uint64_t*)(misc + F3_WAVELP);
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t Bm = gq->Bm;
@@ -491,6 +509,8 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
                 gq->C.l_cnt[pr] = 0;
                 gq->C.e_cnt[pr] = 0;
                 misc[F3_INVALID] = 0;
+                misc[F3_AMASK] = 0;
+                misc[F3_BMASK] = 0;
             }
             if (wave == NW - 1 && lane < 16) misc[F3_HDR + lane] = hv;
             __syncthreads();
@@ -678,11 +698,9 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
             ordA[k] = kT16 | (kT16 << 16);
             ordB[k] = kT16;
         }
-        if (lane == 0) wave_lp[wave] = 0;
 #endif
         for (int rep_ = 0; rep_ < PVAC_REP_P2; ++rep_) {   // experiment builds only (tools/exp_fresh3.py)
         {
-            uint64_t myor = 0;
             auto cells = [&](uint64_t x, uint32_t& t, uint32_t& e) {
                 const uint32_t x0 = (uint32_t)x & kT16, x1 = (uint32_t)(x >> 32) & kT16;
                 t = min(x0, x1);
@@ -713,8 +731,6 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
                 uint32_t cE0 = p0 + (f01 ? p1 : 0u) + (f02 ? p2 : 0u);
                 const uint32_t cE1 = p1 + (f01 ? p0 : 0u) + (f12 ? p2 : 0u);
                 const uint32_t cE2 = p2 + (f02 ? p0 : 0u) + (f12 ? p1 : 0u);
-                myor |= (e0 ? 1ull << __umulhi(m0, bdiv) : 0ull) | (e1 ? 1ull << __umulhi(m1, bdiv) : 0ull) |
-                        (e2 ? 1ull << __umulhi(m2, bdiv) : 0ull);
                 if (big) {   // a bucket of more than 3 slots (rare): t_bkt and edges from `members`
                     const uint32_t q0 = rec0[k] & 0xFFFFu, g = rec0[k] >> 16;
                     for (uint32_t q = q0; q < q0 + g; ++q) {
@@ -723,7 +739,6 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
                         cells(tk64[m], t, e);
                         tb0 = min(tb0, t);
                         cE0 += __popc(e);
-                        myor |= e ? 1ull << __umulhi(m, bdiv) : 0ull;
                     }
                 }
                 // G[t_bkt] from the bucket's leader (duplicates of one bucket write the same value)
@@ -734,8 +749,6 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
                 ordA[k] = tb0 | (tb1 << 16);
                 ordB[k] = tb2 | (wi0 << 16) | (wi1 << 19) | (wi2 << 22) | (e0 << 25) | (e1 << 27) | (e2 << 29);
             }
-            myor = wave_or_u64(myor);
-            if (lane == 0) wave_lp[wave] = myor;
         }
         }
         STAMP3_SYNC(3);
@@ -770,9 +783,17 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
         }
         // compact_layers: when every product layer has an edge, every input layer is a direct
         // parent of one, so nothing is removed (ident); only otherwise does wave 0 run the closure
+        // product layers with cells: (la, lb) with edges in A's layer la and in B's layer lb
         uint64_t used_lp = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) used_lp |= wave_lp[w];
+        {
+            uint32_t a = __builtin_amdgcn_readfirstlane(misc[F3_AMASK]);
+            const uint64_t b = __builtin_amdgcn_readfirstlane(misc[F3_BMASK]);
+            while (a) {   // scalar: LA * LB <= 64, so every shift is < 64
+                const uint32_t la = (uint32_t)__builtin_ctz(a);
+                a &= a - 1;
+                used_lp |= b << (la * LB);
+            }
+        }
         const bool all_lp = used_lp == (LP >= 64 ? ~0ull : ((1ull << LP) - 1ull));
         if (wave == 0 && !all_lp) {
             __builtin_amdgcn_s_setprio(3);
@@ -907,6 +928,10 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
             gq->C.e_cnt[pr] = total;
             gq->C.l_cnt[pr] = (uint64_t)__popcll(keep);
             gq->pair_status[pr] = 0;
+            // every thread read the layer masks in P3 (a barrier ago); stage_pair ORs the next
+            // pair's into them after P5's barrier
+            misc[F3_AMASK] = 0;
+            misc[F3_BMASK] = 0;
         }
         // next pair's raw inputs: in flight through P5 and the writer, staged after them
         const fresh_pref pf = prefetch_pair(gq, nxt, opaque(threadIdx.x));
