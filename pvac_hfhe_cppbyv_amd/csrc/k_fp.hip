@@ -2,15 +2,61 @@
 //
 // K1 fp_binop: HBM-bound streaming over SoA limb arrays. Each lane moves 16-byte
 // (2-element) vectors of every input array; UNROLL independent vectors per lane keep
-// 4*UNROLL 16-byte loads in flight. 48 algorithmic bytes per element (2x16 in, 16 out).
+// 4*UNROLL 16-byte loads in flight, non-temporal (the data is touched once). 48 algorithmic
+// bytes per element (2x16 in, 16 out).
 #include "common.hpp"
 
 namespace pvhip {
 
 namespace {
 
+// Streaming (non-temporal) loads and stores, 4 vectors per lane: 6.10-6.25 TB/s against 5.50-5.59
+// with cached accesses and 2 vectors (cfg 2's 2^24-element add / mul, profiles/r06/ab/fp_ab.log)
+#ifndef PVAC_FP_UNROLL   // A/B builds only
+#define PVAC_FP_UNROLL 4
+#endif
+#ifndef PVAC_FP_NT   // A/B builds only
+#define PVAC_FP_NT 1
+#endif
 constexpr int kFpBlock = 256;
-constexpr int kFpUnroll = 2;
+constexpr int kFpUnroll = PVAC_FP_UNROLL;
+
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+#ifndef PVAC_SCALE_NT   // A/B builds only: k_ct_scale's weights read and written non-temporally
+#define PVAC_SCALE_NT 1
+#endif
+__device__ __forceinline__ uint64_t ld_stream64(const uint64_t* p) {
+#if PVAC_SCALE_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream64(uint64_t* p, uint64_t v) {
+#if PVAC_SCALE_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ ulonglong2 ld_stream(const ulonglong2* p) {
+#if PVAC_FP_NT
+    const u64x2_t v = __builtin_nontemporal_load((const u64x2_t*)p);
+    return make_ulonglong2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(ulonglong2* p, const ulonglong2& v) {
+#if PVAC_FP_NT
+    u64x2_t w;
+    w.x = v.x;
+    w.y = v.y;
+    __builtin_nontemporal_store(w, (u64x2_t*)p);
+#else
+    *p = v;
+#endif
+}
 
 template <int OP>
 __device__ __forceinline__ fp apply(const fp& a, const fp& b) {
@@ -38,11 +84,11 @@ __global__ __launch_bounds__(kFpBlock) void k_fp_binop_vec(const ulonglong2* __r
         for (int u = 0; u < kFpUnroll; ++u) {
             const size_t v = base + (size_t)u * kFpBlock;
             if (v < nvec) {
-                al[u] = alo[v];
-                ah[u] = ahi[v];
+                al[u] = ld_stream(alo + v);
+                ah[u] = ld_stream(ahi + v);
                 if constexpr (OP != PVAC_FP_NEG && OP != PVAC_FP_SCALE && OP != PVAC_FP_INV) {
-                    bl[u] = blo[v];
-                    bh[u] = bhi[v];
+                    bl[u] = ld_stream(blo + v);
+                    bh[u] = ld_stream(bhi + v);
                 }
             }
         }
@@ -60,8 +106,8 @@ __global__ __launch_bounds__(kFpBlock) void k_fp_binop_vec(const ulonglong2* __r
                 }
                 const fp r0 = apply<OP>(fp{al[u].x, ah[u].x}, b0);
                 const fp r1 = apply<OP>(fp{al[u].y, ah[u].y}, b1);
-                clo[v] = make_ulonglong2(r0.lo, r1.lo);
-                chi[v] = make_ulonglong2(r0.hi, r1.hi);
+                st_stream(clo + v, make_ulonglong2(r0.lo, r1.lo));
+                st_stream(chi + v, make_ulonglong2(r0.hi, r1.hi));
             }
         }
     }
@@ -237,21 +283,21 @@ __global__ __launch_bounds__(256) void k_ct_scale(pvac_ct_batch X, uint64_t slo,
     for (int u = 0; u < kPre; ++u) {
         const uint64_t e = e0 + 32u * u;
         w[u] = fp{0, 0};
-        if (e < n) w[u] = fp{X.w_lo[o + e], X.w_hi[o + e]};
+        if (e < n) w[u] = fp{ld_stream64(X.w_lo + o + e), ld_stream64(X.w_hi + o + e)};
     }
 #pragma unroll
     for (int u = 0; u < kPre; ++u) {
         const uint64_t e = e0 + 32u * u;
         if (e < n) {
             const fp r = fp_mul(w[u], s);
-            X.w_lo[o + e] = r.lo;
-            X.w_hi[o + e] = r.hi;
+            st_stream64(X.w_lo + o + e, r.lo);
+            st_stream64(X.w_hi + o + e, r.hi);
         }
     }
     for (uint64_t e = e0 + 32u * kPre; e < n; e += 32) {
-        const fp r = fp_mul(fp{X.w_lo[o + e], X.w_hi[o + e]}, s);
-        X.w_lo[o + e] = r.lo;
-        X.w_hi[o + e] = r.hi;
+        const fp r = fp_mul(fp{ld_stream64(X.w_lo + o + e), ld_stream64(X.w_hi + o + e)}, s);
+        st_stream64(X.w_lo + o + e, r.lo);
+        st_stream64(X.w_hi + o + e, r.hi);
     }
 }
 
