@@ -132,12 +132,15 @@ __device__ __forceinline__ argp launder(argp p) { return launder((uint64_t)p); }
 
 // Per-pair header (workgroup-uniform). pr == kNoPair ends the persistent loop.
 constexpr uint64_t kNoPair = ~0ull;
+// Only what every wave needs is decoded into registers (each decoded word costs one v_readlane
+// per wave): the record's other words stay in LDS (misc[F3_HDR ..], written before the pair's
+// prefetch), where prefetch_pair reads its four offsets; the rare users of clo / nb_magic read
+// the record itself (scalar loads).
 struct fresh_hdr {
     uint64_t pr;
     uint32_t LA, LB, nA, nB;
-    uint64_t aeo, beo, alo, blo, clo, ceo;
+    uint64_t ceo;
     uint32_t nbk;        // libstdc++ bucket count after reserve(|A.E||B.E|)
-    uint64_t nb_magic;   // its fastmod64 multiplier
 };
 
 // Header records are read through the constant address space: uniform-index reads become scalar
@@ -151,20 +154,6 @@ __device__ __forceinline__ uint64_t next_small(argp g, uint64_t from) {
     return kNoPair;
 }
 
-__device__ __forceinline__ fresh_hdr load_hdr(argp g, uint64_t pr) {
-    fresh_hdr h{};
-    h.pr = pr;
-    if (pr != kNoPair) {
-        const recp r = (recp)g->recs + pr;
-        h.LA = r->LA; h.LB = r->LB;
-        h.nA = r->shape & 0xFFFFu; h.nB = r->shape >> 16;
-        h.aeo = r->aeo; h.beo = r->beo; h.ceo = r->ceo;
-        h.alo = r->alo; h.blo = r->blo; h.clo = r->clo;
-        h.nbk = r->nbk;
-        h.nb_magic = r->nb_magic;
-    }
-    return h;
-}
 
 // The next pair's header is loaded by VECTOR memory (lane l < 16 of every wave holds dword l of
 // its record): its wait is vmcnt, so it never holds up an LDS wait the way a scalar load would
@@ -174,21 +163,13 @@ __device__ __forceinline__ uint32_t hdr_issue(const fresh_rec* recs, uint64_t n_
     return ((const uint32_t*)(recs + q))[threadIdx.x & 15u];
 }
 
-__device__ __forceinline__ fresh_hdr hdr_next(argp g, uint32_t v, uint64_t q, uint64_t n_pairs) {
+// header of pair q from its record's words (lane l & 15 holds dword l)
+__device__ __forceinline__ fresh_hdr hdr_decode(uint32_t v, uint64_t q) {
     fresh_hdr h{};
-    h.pr = kNoPair;
-    if (q >= n_pairs) return h;
     auto rd = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane(v, k); };
     const uint32_t w15 = rd(15);
-    if ((w15 & 0xFFFFu) == 0) return load_hdr(g, next_small(g, q + gridDim.x));   // not a fresh pair
     h.pr = q;
-    h.aeo = ((uint64_t)rd(1) << 32) | rd(0);
-    h.beo = ((uint64_t)rd(3) << 32) | rd(2);
     h.ceo = ((uint64_t)rd(5) << 32) | rd(4);
-    h.alo = ((uint64_t)rd(7) << 32) | rd(6);
-    h.blo = ((uint64_t)rd(9) << 32) | rd(8);
-    h.clo = ((uint64_t)rd(11) << 32) | rd(10);
-    h.nb_magic = ((uint64_t)rd(13) << 32) | rd(12);
     const uint32_t shape = rd(14);
     h.nA = shape & 0xFFFFu;
     h.nB = shape >> 16;
@@ -196,6 +177,21 @@ __device__ __forceinline__ fresh_hdr hdr_next(argp g, uint32_t v, uint64_t q, ui
     h.LA = (w15 >> 16) & 0xFFu;
     h.LB = w15 >> 24;
     return h;
+}
+
+// The pair after q - gridDim.x: q itself when it is a fresh pair (its words v, from LDS), else the
+// next fresh one, whose record every wave loads and the control wave copies into the LDS words
+// (so a barrier must separate this call from the prefetch that reads them).
+__device__ __forceinline__ fresh_hdr hdr_next(argp g, uint32_t v, uint64_t q, uint64_t n_pairs, uint32_t* hw) {
+    fresh_hdr h{};
+    h.pr = kNoPair;
+    if (q >= n_pairs) return h;
+    if (((uint32_t)__builtin_amdgcn_readlane(v, 15) & 0xFFFFu) != 0) return hdr_decode(v, q);
+    const uint64_t q2 = next_small(g, q + gridDim.x);   // not a fresh pair (rare)
+    if (q2 == kNoPair) return h;
+    const uint32_t v2 = ((const uint32_t*)(g->recs + q2))[threadIdx.x & 15u];
+    if ((threadIdx.x >> 6) == (blockDim.x >> 6) - 1 && (threadIdx.x & 63u) < 16) hw[threadIdx.x & 15u] = v2;
+    return hdr_decode(v2, q2);
 }
 static_assert(offsetof(fresh_rec, nb_magic) == 48 && offsetof(fresh_rec, shape) == 56 && offsetof(fresh_rec, nbk) == 60 &&
                   offsetof(fresh_rec, LA) == 62 && offsetof(fresh_rec, LB) == 63,
@@ -212,7 +208,8 @@ struct fresh_pref {
 #ifndef PVAC_F3_PF_WAVES   // A/B builds: 0 = every wave prefetches (round 4)
 #define PVAC_F3_PF_WAVES 1
 #endif
-__device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h, uint32_t t = threadIdx.x) {
+__device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h, const uint32_t* hw,
+                                                    uint32_t t = threadIdx.x) {
     // every lane of a loading wave loads a valid address (a clamped index, or the argument block
     // itself when there is no pair / no edge), so the waitcnt pass never has to drain earlier loads
     // (or the previous pair's output stores) before issuing these; lanes past the counts ignore what
@@ -225,9 +222,13 @@ __device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h, 
     using gp64 = const __attribute__((address_space(1))) uint64_t*;   // global: never a flat load
     using gpl = const __attribute__((address_space(1))) uint32_t*;
     const gp64 dummy = (gp64)(uint64_t)g;
+    const uint32_t v = hw[t & 15u];   // the pair's record words (only the loading waves decode them)
+    auto rd = [&](int k) { return (uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, k); };
+    const uint64_t aeo = (rd(1) << 32) | rd(0), beo = (rd(3) << 32) | rd(2);
+    const uint64_t alo = (rd(7) << 32) | rd(6), blo = (rd(9) << 32) | rd(8);
     const bool okA = live && h.nA, okB = live && h.nB;
-    const uint64_t ea = okA ? h.aeo + min(t, h.nA - 1u) : 0ull;
-    const uint64_t eb = okB ? h.beo + min(t, h.nB - 1u) : 0ull;
+    const uint64_t ea = okA ? aeo + min(t, h.nA - 1u) : 0ull;
+    const uint64_t eb = okB ? beo + min(t, h.nB - 1u) : 0ull;
     const gp64 am = okA ? (gp64)g->A.meta : dummy;
     const gp64 al = okA ? (gp64)g->A.w_lo : dummy;
     const gp64 ah = okA ? (gp64)g->A.w_hi : dummy;
@@ -237,8 +238,8 @@ __device__ __forceinline__ fresh_pref prefetch_pair(argp g, const fresh_hdr& h, 
     const uint32_t nl = h.LA + h.LB;
     const uint32_t l = min(t, nl - 1u);
     const gpl rec = !(live && nl) ? (gpl)dummy
-                    : l < h.LA    ? (gpl)(g->A.layers + h.alo + l)
-                                  : (gpl)(g->B.layers + h.blo + (l - h.LA));
+                    : l < h.LA    ? (gpl)(g->A.layers + alo + l)
+                                  : (gpl)(g->B.layers + blo + (l - h.LA));
     fresh_pref f;
     f.am = am[ea]; f.al = al[ea]; f.ah = ah[ea];
     f.bm = bm[eb]; f.bl = bl[eb]; f.bh = bh[eb];
@@ -488,8 +489,18 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
 #endif
     const fresh_rec* const recs = gq->recs;
     const uint64_t n_pairs = gq->A.n;
-    fresh_hdr cur = load_hdr(gq, next_small(gq, blockIdx.x));
-    stage_pair(prefetch_pair(gq, cur), cur, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+    fresh_hdr cur{};
+    cur.pr = kNoPair;
+    {   // the first pair's record words into LDS (the control wave), then decoded by every wave
+        const uint64_t q0 = next_small(gq, blockIdx.x);
+        if (q0 != kNoPair) {
+            const uint32_t v0 = ((const uint32_t*)(recs + q0))[threadIdx.x & 15u];
+            if (wave == NW - 1 && lane < 16) misc[F3_HDR + lane] = v0;
+            cur = hdr_decode(v0, q0);
+        }
+    }
+    __syncthreads();
+    stage_pair(prefetch_pair(gq, cur, misc + F3_HDR), cur, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
     __syncthreads();
 
     while (cur.pr != kNoPair) {
@@ -514,8 +525,9 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
             }
             if (wave == NW - 1 && lane < 16) misc[F3_HDR + lane] = hv;
             __syncthreads();
-            const fresh_hdr nx = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs);
-            stage_pair(prefetch_pair(gq, nx), nx, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
+            const fresh_hdr nx = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs, misc + F3_HDR);
+            __syncthreads();   // (hdr_next may have replaced the LDS words)
+            stage_pair(prefetch_pair(gq, nx, misc + F3_HDR), nx, Bm, a_w, a_inf, b_w, b_inf, pm, misc);
             __syncthreads();
             cur = nx;
             continue;
@@ -534,7 +546,7 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
             uint32_t* rnk = boff + nbk;                  // [nbk] rank of a bucket inside its size class
             uint32_t* drec = rnk + nbk;                  // [2 ksa] bin records
             uint16_t* csr = (uint16_t*)(drec + 2u * ksa);   // [ksa] slots in bucket order
-            const fastmod64 fm{nbk, cur.nb_magic};
+            const fastmod64 fm{nbk, ((recp)gq->recs + pr)->nb_magic};
             uint32_t bk[KI];
 #pragma unroll
             for (int k = 0; k < KI; ++k) {
@@ -685,7 +697,7 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
         STAMP3(2);
         gq = launder(gq);
         __builtin_amdgcn_s_setprio(1);
-        const fresh_hdr nxt = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs);
+        const fresh_hdr nxt = hdr_next(gq, misc[F3_HDR + (lane & 15)], qn, n_pairs, misc + F3_HDR);
 
         M3(2);
         // ---- P2: per bin (up to 3 slots whose buckets lie wholly in the bin): key time and emit
@@ -913,7 +925,7 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
         const bool ident = all_lp || misc[F3_IDENT] != 0;
         if (!ident && wave == 1) {   // compact the identity-placed layer records in place
             const uint32_t l = lane;
-            const uint64_t clo = cur.clo;
+            const uint64_t clo = ((recp)gq->recs + pr)->clo;
             pvac_layer y{};
             if (l < Lc) y = gq->C.layers[clo + l];
             if (l < Lc && ((keep >> l) & 1ull)) {
@@ -934,7 +946,7 @@ __global__ __launch_bounds__(BS, PVAC_F3_WPE) void k_ct_mul_fresh3(const mul_fre
             misc[F3_BMASK] = 0;
         }
         // next pair's raw inputs: in flight through P5 and the writer, staged after them
-        const fresh_pref pf = prefetch_pair(gq, nxt, opaque(threadIdx.x));
+        const fresh_pref pf = prefetch_pair(gq, nxt, misc + F3_HDR, opaque(threadIdx.x));
         STAMP3_SYNC(7);
         __syncthreads();
         STAMP3(8);
