@@ -24,7 +24,8 @@
 namespace pvhip {
 namespace {
 
-constexpr int kPB = 256;   // 4 requests per block
+constexpr int kPB = 256;   // 4 requests per block (utility kernels)
+constexpr int kCB = 512;   // k_prf_core: 8 requests per block share the 64 KB table (two blocks per CU)
 
 __constant__ aes_ttables c_aes;
 
@@ -52,31 +53,81 @@ __device__ __forceinline__ void derive(const prf_consts& k, uint64_t ztag, uint6
     for (int i = 0; i < 8; ++i) key[i] = bswap32d(s.h[i]);   // digest bytes -> little-endian key words
 }
 
-// T0 only, replicated kTCopies times in a bank-per-lane layout: entry x of copy c is LDS word
-// x * kTCopies + c, and lane l reads copy l % kTCopies, so the 64 lanes of a lookup hit at most two
-// words per bank (one per lane half) instead of colliding at random; T1..T3 are byte rotations.
-constexpr uint32_t kTCopies = 32;
+// T0 with one private copy per lane: entry x of copy c at LDS byte (x << 8) | (c << 2) (64 copies of
+// 1 KB), so no two lanes of a lookup share a bank, and a lookup's address is one v_perm of the state
+// word: byte k of w into address byte 1, the lane's copy offset (lane * 4) in byte 0. T1..T3 are
+// byte rotations of T0.
+constexpr uint32_t kTBytes = 256u * 256u;
 
-__device__ __forceinline__ uint32_t tlook(const uint32_t* T, uint32_t x) {
-    return T[(x * kTCopies) | (threadIdx.x & (kTCopies - 1))];
+struct ttab {
+    const uint8_t* b;   // LDS table
+    uint32_t c4;        // lane * 4
+    __device__ __forceinline__ uint32_t at(uint32_t addr) const { return *(const uint32_t*)(b + addr); }
+    // T0[byte k of w]
+    __device__ __forceinline__ uint32_t t0(uint32_t w, uint32_t k) const {
+        return at(__builtin_amdgcn_perm(w, c4, 0x0C0C0000u | ((4u + k) << 8)));
+    }
+    __device__ __forceinline__ uint32_t sbox(uint32_t x) const { return (at((x << 8) | c4) >> 8) & 0xFFu; }
+};
+
+__device__ __forceinline__ uint32_t rotl(uint32_t v, int s) { return __builtin_amdgcn_alignbit(v, v, 32 - s); }
+
+// one AES-256 round column: T0[w0.b0] ^ T1[w1.b1] ^ T2[w2.b2] ^ T3[w3.b3] ^ key (aes256_encrypt's order)
+__device__ __forceinline__ uint32_t col(const ttab& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t key) {
+    return T.t0(w0, 0) ^ rotl(T.t0(w1, 1), 8) ^ rotl(T.t0(w2, 2), 16) ^ rotl(T.t0(w3, 3), 24) ^ key;
+}
+// last-round column: the S-box bytes (byte 1 of T0) of w0.b0, w1.b1, w2.b2, w3.b3, packed by v_perm
+__device__ __forceinline__ uint32_t col_last(const ttab& T, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                             uint32_t key) {
+    const uint32_t v0 = T.t0(w0, 0), v1 = T.t0(w1, 1), v2 = T.t0(w2, 2), v3 = T.t0(w3, 3);
+    const uint32_t lo = __builtin_amdgcn_perm(v1, v0, 0x0C0C0501u);   // [v0.b1, v1.b1, 0, 0]
+    const uint32_t hi = __builtin_amdgcn_perm(v3, v2, 0x0C0C0501u);   // [v2.b1, v3.b1, 0, 0]
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u) ^ key;          // [lo.b0, lo.b1, hi.b0, hi.b1]
 }
 
-__device__ __forceinline__ void ctr_block(uint64_t ctr, const uint32_t* T, const uint32_t* rk, uint64_t& lo,
-                                          uint64_t& hi) {
-    uint32_t w0 = (uint32_t)ctr, w1 = (uint32_t)(ctr >> 32), w2 = 0, w3 = 0;
-    aes256_encrypt(w0, w1, w2, w3,
-                   [&](int t, uint32_t x) {
-                       const uint32_t v = tlook(T, x);
-                       return t == 0 ? v : __builtin_amdgcn_alignbit(v, v, 32 - 8 * t);   // rotl(v, 8t)
-                   },
-                   [&](int i) { return rk[i]; });
-    lo = ((uint64_t)w1 << 32) | w0;
-    hi = ((uint64_t)w3 << 32) | w2;
+// AES-256 of counter blocks (ctr, 0) under the round keys rk (LDS, 60 words), NB blocks side by side
+// (independent round chains for the scheduler to overlap); out: the two u64 halves of each block
+template <int NB>
+__device__ __forceinline__ void ctr_blocks(const uint64_t* ctr, const ttab& T, const uint32_t* rk, uint64_t* lo,
+                                           uint64_t* hi) {
+    uint32_t w[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        w[b][0] = (uint32_t)ctr[b] ^ rk[0];
+        w[b][1] = (uint32_t)(ctr[b] >> 32) ^ rk[1];
+        w[b][2] = rk[2];
+        w[b][3] = rk[3];
+    }
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t k0 = rk[4 * r], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint32_t n0 = col(T, w[b][0], w[b][1], w[b][2], w[b][3], k0);
+            const uint32_t n1 = col(T, w[b][1], w[b][2], w[b][3], w[b][0], k1);
+            const uint32_t n2 = col(T, w[b][2], w[b][3], w[b][0], w[b][1], k2);
+            const uint32_t n3 = col(T, w[b][3], w[b][0], w[b][1], w[b][2], k3);
+            w[b][0] = n0; w[b][1] = n1; w[b][2] = n2; w[b][3] = n3;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint32_t n0 = col_last(T, w[b][0], w[b][1], w[b][2], w[b][3], rk[56]);
+        const uint32_t n1 = col_last(T, w[b][1], w[b][2], w[b][3], w[b][0], rk[57]);
+        const uint32_t n2 = col_last(T, w[b][2], w[b][3], w[b][0], w[b][1], rk[58]);
+        const uint32_t n3 = col_last(T, w[b][3], w[b][0], w[b][1], w[b][2], rk[59]);
+        lo[b] = ((uint64_t)n1 << 32) | n0;
+        hi[b] = ((uint64_t)n3 << 32) | n2;
+    }
 }
 
-__device__ void expand_key(const uint32_t key[8], uint32_t* rk, const uint32_t* T) {
+__device__ __forceinline__ void ctr_block(uint64_t ctr, const ttab& T, const uint32_t* rk, uint64_t& lo, uint64_t& hi) {
+    ctr_blocks<1>(&ctr, T, rk, &lo, &hi);
+}
+
+__device__ void expand_key(const uint32_t key[8], uint32_t* rk, const ttab& T) {
     uint32_t r[60];
-    aes256_expand(key, r, [&](uint32_t x) { return (tlook(T, x) >> 8) & 0xFFu; });
+    aes256_expand(key, r, [&](uint32_t x) { return T.sbox(x); });
     for (int i = threadIdx.x & 63; i < 60; i += 64) rk[i] = r[i];
 }
 
@@ -86,15 +137,16 @@ __device__ __forceinline__ uint64_t wave_xor_u64(uint64_t x) {
     return x;
 }
 
-__global__ __launch_bounds__(kPB, 4) void k_prf_core(prf_consts k, const prf_request* req, uint64_t n, uint64_t* out) {
-    __shared__ uint32_t T[256 * kTCopies];
+__global__ __launch_bounds__(kCB) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_prf_core(prf_consts k, const prf_request* req, uint64_t n, uint64_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t Tb[kTBytes];
     __shared__ uint64_t S[64];
-    __shared__ uint32_t RK[kPB / 64][2][60];
-    for (int i = threadIdx.x; i < 256 * (int)kTCopies; i += kPB) T[i] = c_aes.T[0][i / kTCopies];
-    for (int i = threadIdx.x; i < 64; i += kPB) S[i] = i < (int)k.s_words ? k.s_bits[i] : 0ull;
+    __shared__ uint32_t RK[kCB / 64][2][60];
+    for (int i = threadIdx.x; i < (int)(kTBytes / 4); i += kCB) ((uint32_t*)Tb)[i] = c_aes.T[0][i >> 6];
+    for (int i = threadIdx.x; i < 64; i += kCB) S[i] = i < (int)k.s_words ? k.s_bits[i] : 0ull;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t q = (uint64_t)blockIdx.x * (kPB / 64) + wave;
+    const ttab T{Tb, (uint32_t)lane << 2};
+    const uint64_t q = (uint64_t)blockIdx.x * (kCB / 64) + wave;
     if (q >= n) return;   // wave-uniform; no block barrier below
     const prf_request rq = req[q];
     const uint64_t dh = k.dom_hash[rq.dom];
@@ -111,28 +163,39 @@ __global__ __launch_bounds__(kPB, 4) void k_prf_core(prf_consts k, const prf_req
     const uint64_t lim = ~0ull - (~0ull % (uint64_t)k.tau_den);
     const uint32_t sw = k.s_words;           // 64 for lpn_n = 4096
     const uint64_t row_words = sw + 1ull;    // 64 row words + one bounded draw
-    // rows lane and lane + 64
+    // rows lane and lane + 64, their AES blocks interleaved: two independent round chains per lane
+    // keep two sets of T-table lookups in flight (each chain alone waits on its LDS reads). Every
+    // row spans the same number of blocks, (w0 + sw) / 2 - w0 / 2 + 1; lane 63's second row (127)
+    // does not exist and is computed and dropped.
     uint32_t ybit[2] = {0, 0};
     bool rejected = false;
-#pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t r = (uint32_t)lane + 64u * h;
-        if (r >= 127u) continue;
-        const uint64_t w0 = row_words * r;           // first keystream word of the row
-        const uint64_t b0 = w0 >> 1, b1 = (w0 + sw) >> 1;
-        uint64_t acc = 0, x = 0;
-        for (uint64_t b = b0; b <= b1; ++b) {
-            uint64_t lo, hi;
-            ctr_block(nonce + b, T, rk, lo, hi);
-            const uint64_t qlo = 2 * b, qhi = 2 * b + 1;
-            if (qlo >= w0 && qlo < w0 + sw) acc ^= lo & S[qlo - w0];
-            if (qhi >= w0 && qhi < w0 + sw) acc ^= hi & S[qhi - w0];
-            if (qlo == w0 + sw) x = lo;
-            if (qhi == w0 + sw) x = hi;
+    {
+        const uint64_t wa = row_words * (uint32_t)lane, wb = row_words * ((uint32_t)lane + 64u);
+        const uint64_t ba = wa >> 1, bb = wb >> 1;
+        const uint64_t nb = ((wa + sw) >> 1) - ba + 1;   // = for row lane + 64 (row_words odd or even alike)
+        uint64_t acc[2] = {0, 0}, x[2] = {0, 0};
+        const uint64_t w0s[2] = {wa, wb}, b0s[2] = {ba, bb};
+        for (uint64_t kb = 0; kb < nb; ++kb) {
+            uint64_t lo[2], hi[2];
+            const uint64_t ctr[2] = {nonce + ba + kb, nonce + bb + kb};
+            ctr_blocks<2>(ctr, T, rk, lo, hi);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint64_t w0 = w0s[h], b = b0s[h] + kb;
+                const uint64_t qlo = 2 * b, qhi = 2 * b + 1;
+                if (qlo >= w0 && qlo < w0 + sw) acc[h] ^= lo[h] & S[qlo - w0];
+                if (qhi >= w0 && qhi < w0 + sw) acc[h] ^= hi[h] & S[qhi - w0];
+                if (qlo == w0 + sw) x[h] = lo[h];
+                if (qhi == w0 + sw) x[h] = hi[h];
+            }
         }
-        rejected |= x >= lim;
-        const uint32_t e = (x % (uint64_t)k.tau_den) < (uint64_t)k.tau_num ? 1u : 0u;
-        ybit[h] = (uint32_t)__builtin_parityll(acc) ^ e;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if ((uint32_t)lane + 64u * h >= 127u) continue;
+            rejected |= x[h] >= lim;
+            const uint32_t e = (x[h] % (uint64_t)k.tau_den) < (uint64_t)k.tau_num ? 1u : 0u;
+            ybit[h] = (uint32_t)__builtin_parityll(acc[h]) ^ e;
+        }
     }
     uint64_t y0 = __ballot(ybit[0] != 0), y1 = __ballot(ybit[1] != 0) & 0x7FFFFFFFFFFFFFFFull;
     if (__ballot(rejected)) {
@@ -244,9 +307,9 @@ size_t prf_request_bytes() { return sizeof(prf_request); }
 
 hipError_t launch_prf_cores(const prf_consts& k, const void* req, uint64_t n, uint64_t* out, hipStream_t st) {
     if (!n) return hipSuccess;
-    const uint64_t blocks = (n + kPB / 64 - 1) / (kPB / 64);
+    const uint64_t blocks = (n + kCB / 64 - 1) / (kCB / 64);
     if (blocks > 0x7FFFFFFFull || k.s_words > 64 || k.tau_den == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_prf_core, dim3((unsigned)blocks), dim3(kPB), 0, st, k, (const prf_request*)req, n, out);
+    hipLaunchKernelGGL(k_prf_core, dim3((unsigned)blocks), dim3(kCB), 0, st, k, (const prf_request*)req, n, out);
     return hipGetLastError();
 }
 
