@@ -100,37 +100,5 @@ __host__ __device__ inline void aes256_encrypt(uint32_t& w0, uint32_t& w1, uint3
     w0 = n0 ^ rk(56); w1 = n1 ^ rk(57); w2 = n2 ^ rk(58); w3 = n3 ^ rk(59);
 }
 
-// Two blocks under one key, their rounds side by side: independent T-table lookups for the
-// scheduler to overlap (one block's round waits on its own lookups).
-template <class TBL, class RK>
-__host__ __device__ inline void aes256_encrypt2(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t& b0,
-                                                uint32_t& b1, uint32_t& b2, uint32_t& b3, TBL T, RK rk) {
-    a0 ^= rk(0); a1 ^= rk(1); a2 ^= rk(2); a3 ^= rk(3);
-    b0 ^= rk(0); b1 ^= rk(1); b2 ^= rk(2); b3 ^= rk(3);
-#pragma unroll
-    for (int r = 1; r < 14; ++r) {
-        const uint32_t k0 = rk(4 * r), k1 = rk(4 * r + 1), k2 = rk(4 * r + 2), k3 = rk(4 * r + 3);
-        const uint32_t n0 = T(0, a0 & 0xFF) ^ T(1, (a1 >> 8) & 0xFF) ^ T(2, (a2 >> 16) & 0xFF) ^ T(3, a3 >> 24) ^ k0;
-        const uint32_t m0 = T(0, b0 & 0xFF) ^ T(1, (b1 >> 8) & 0xFF) ^ T(2, (b2 >> 16) & 0xFF) ^ T(3, b3 >> 24) ^ k0;
-        const uint32_t n1 = T(0, a1 & 0xFF) ^ T(1, (a2 >> 8) & 0xFF) ^ T(2, (a3 >> 16) & 0xFF) ^ T(3, a0 >> 24) ^ k1;
-        const uint32_t m1 = T(0, b1 & 0xFF) ^ T(1, (b2 >> 8) & 0xFF) ^ T(2, (b3 >> 16) & 0xFF) ^ T(3, b0 >> 24) ^ k1;
-        const uint32_t n2 = T(0, a2 & 0xFF) ^ T(1, (a3 >> 8) & 0xFF) ^ T(2, (a0 >> 16) & 0xFF) ^ T(3, a1 >> 24) ^ k2;
-        const uint32_t m2 = T(0, b2 & 0xFF) ^ T(1, (b3 >> 8) & 0xFF) ^ T(2, (b0 >> 16) & 0xFF) ^ T(3, b1 >> 24) ^ k2;
-        const uint32_t n3 = T(0, a3 & 0xFF) ^ T(1, (a0 >> 8) & 0xFF) ^ T(2, (a1 >> 16) & 0xFF) ^ T(3, a2 >> 24) ^ k3;
-        const uint32_t m3 = T(0, b3 & 0xFF) ^ T(1, (b0 >> 8) & 0xFF) ^ T(2, (b1 >> 16) & 0xFF) ^ T(3, b2 >> 24) ^ k3;
-        a0 = n0; a1 = n1; a2 = n2; a3 = n3;
-        b0 = m0; b1 = m1; b2 = m2; b3 = m3;
-    }
-    auto S = [&](uint32_t x) { return (T(0, x) >> 8) & 0xFFu; };
-    auto last = [&](uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) {
-        const uint32_t n0 = S(w0 & 0xFF) | (S((w1 >> 8) & 0xFF) << 8) | (S((w2 >> 16) & 0xFF) << 16) | (S(w3 >> 24) << 24);
-        const uint32_t n1 = S(w1 & 0xFF) | (S((w2 >> 8) & 0xFF) << 8) | (S((w3 >> 16) & 0xFF) << 16) | (S(w0 >> 24) << 24);
-        const uint32_t n2 = S(w2 & 0xFF) | (S((w3 >> 8) & 0xFF) << 8) | (S((w0 >> 16) & 0xFF) << 16) | (S(w1 >> 24) << 24);
-        const uint32_t n3 = S(w3 & 0xFF) | (S((w0 >> 8) & 0xFF) << 8) | (S((w1 >> 16) & 0xFF) << 16) | (S(w2 >> 24) << 24);
-        w0 = n0 ^ rk(56); w1 = n1 ^ rk(57); w2 = n2 ^ rk(58); w3 = n3 ^ rk(59);
-    };
-    last(a0, a1, a2, a3);
-    last(b0, b1, b2, b3);
-}
 
 }  // namespace pvhip
