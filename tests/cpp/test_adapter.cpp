@@ -536,6 +536,17 @@ int main(int argc, char** argv) {
             MUST(write_ct({ct_view(one[p])}) == write_ct({ct_view(two[p])}) && same_edges(one[p], two[p], true) &&
                      same_edges(one[p], three[p], true),
                  "multi-device batch pair %d", p);
+        // the engine's kept arrays handed back, then grown again: the same bytes; and a batch of
+        // one pair after the 8-pair one (the kept arrays larger than needed) equals its own pair
+        pvac_hip::engine_for(pk).trim();
+        const auto again = pvac_hip::ct_mul_batch(pk, A, B, true, os_splitmix(7), std::vector<int>{});
+        for (int p = 0; p < 8; ++p)
+            MUST(write_ct({ct_view(one[p])}) == write_ct({ct_view(again[p])}) && same_edges(one[p], again[p], true),
+                 "batch after trim, pair %d", p);
+        // (edges and weights do not depend on the random source, only layer nonces and sigmas do)
+        const std::vector<Cipher> A1{A[3]}, B1{B[3]};
+        const auto solo = pvac_hip::ct_mul_batch(pk, A1, B1, false, os_splitmix(9), std::vector<int>{});
+        MUST(solo.size() == 1 && same_edges(solo[0], one[3], false), "one-pair batch on grown arrays");
     }
 
     // fp_binop through the adapter on the golden vectors (core/field.hpp:50-213)
