@@ -190,7 +190,8 @@ int pvac_hip_ct_mul_exec(pvac_hip_ctx* ctx, const pvac_hip_plan* plan, const pva
  * one shape, no host round trip between the two): C->l_off / e_off / l_cnt / e_cnt hold A->n,
  * C->layers layer_cap slots, C->meta / w_lo / w_hi (and C->sigma) edge_cap slots. When this plan
  * needs more, nothing is launched after it and the call returns PVAC_ENOMEM with *plan (nullable)
- * holding the sizes to allocate. nonces / salts as for pvac_hip_ct_mul_exec (the nonce slots are
+ * holding the sizes to allocate (the plan has rewritten C's offset and count arrays by then; C's
+ * rows are untouched). nonces / salts as for pvac_hip_ct_mul_exec (the nonce slots are
  * C's planned layer slots, so they are valid only while the plan's offsets are: batches of one
  * shape plan the same offsets). */
 int pvac_hip_ct_mul(pvac_hip_ctx* ctx, const pvac_ct_batch* A, const pvac_ct_batch* B, pvac_ct_batch* C,
